@@ -1,0 +1,110 @@
+"""ctypes binding of libmiattack.so (the C ABI declared in include/miattack.h).
+
+The product path has no CPU fallback: if the library is missing or no GPU is present, the first
+call raises. torch is imported before the library is opened so that the process holds ONE HIP
+runtime (torch's libamdhip64, whose SONAME the library's dependency resolves to).
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmiattack.so")
+
+c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
+P = c_void_p
+
+MIA_F32, MIA_F16, MIA_BF16 = 0, 1, 2
+ACT_NONE, ACT_RELU, ACT_LRELU_S2 = 0, 1, 2
+
+
+class ConvArgs(ctypes.Structure):
+    """Mirror of ``mia_conv_args`` (include/miattack.h)."""
+    _fields_ = [
+        ("x", P), ("w", P), ("y", P),
+        ("N", c_int), ("H", c_int), ("W", c_int), ("Cin", c_int), ("Cout", c_int), ("Kpad", c_int),
+        ("y_cstride", c_int), ("act_in", c_int),
+        ("in_scale", P), ("out_scale", P), ("bias", P), ("noise", P), ("noise_w", c_float),
+        ("act_out", c_int), ("shuffle_out", c_int),
+        ("aux_x", P), ("act_aux", c_int), ("sdot", P),
+        ("tap_a", P), ("tap_t", P), ("tap_coef", c_float), ("mask_a", P),
+        ("accumulate", c_int),
+    ]
+
+
+# name -> (restype, argtypes); every function declared in include/miattack.h
+SIGNATURES = {
+    "mia_version": (c_int, []),
+    "mia_last_error_string": (ctypes.c_char_p, []),
+    "mia_conv_kpad": (c_int, [c_int, c_int]),
+    "mia_conv3x3": (c_int, [ctypes.POINTER(ConvArgs), c_int, P]),
+    "mia_modconv_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P,
+                                c_float, P, c_int, c_int, P]),
+    "mia_modconv_bwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, P, P,
+                                c_int, P]),
+    "mia_vgg_conv_relu_fwd": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                      P]),
+    "mia_vgg_conv_dgrad": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P,
+                                   c_float, P, c_int, P]),
+    "mia_bias_act_fwd": (c_int, [P, P, c_float, P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "mia_bias_act_bwd": (c_int, [P, P, P, c_float, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
+                                 c_int, P]),
+    "mia_upfirdn2d_fwd": (c_int, [P, P, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, c_int,
+                                  P]),
+    "mia_upfirdn2d_bwd": (c_int, [P, P, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, c_int,
+                                  P]),
+    "mia_torgb_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "mia_torgb_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    "mia_maxpool2_fwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    "mia_maxpool2_bwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_float, c_int,
+                                 c_int, P]),
+    "mia_avgpool_fwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P]),
+    "mia_avgpool_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "mia_image_to_nhwc": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "mia_mse_sum": (c_int, [P, P, P, c_int, c_int64, c_int, P]),
+    "mia_mse_grad_f32": (c_int, [P, P, P, c_int64, c_float, c_int, P]),
+    "mia_tap_grad": (c_int, [P, P, P, c_int64, c_float, c_int, c_int, P]),
+    "mia_image_grad": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_float, c_int, P]),
+    "mia_pgd_update": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, c_float,
+                               c_float, c_float, c_float, c_int, P]),
+    "mia_random_start": (c_int, [P, P, P, c_int64, c_float, c_float, c_float, P]),
+    "mia_sign_project": (c_int, [P, P, P, c_int64, c_float, c_float, c_float, c_float, P]),
+    "mia_adam_step": (c_int, [P, P, P, P, c_int64, c_float, c_float, c_float, c_float, c_int, P]),
+    "mia_gemm_f32": (c_int, [c_int, c_int, c_int, c_float, P, c_int64, c_int64, P, c_int64,
+                             c_int64, c_float, P, c_int64, c_int64, P, P]),
+    "mia_style_demod": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
+    "mia_demod_bwd": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
+    "mia_repeat": (c_int, [P, P, c_int64, c_int, P]),
+    "mia_memset": (c_int, [P, c_int, c_int64, P]),
+}
+
+_lib = None
+
+
+class MiaError(RuntimeError):
+    pass
+
+
+def load():
+    """Open the library (once). Raises if it was not built — there is no fallback path."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (one HIP runtime per process: torch's)
+    if not os.path.exists(LIB_PATH):
+        raise MiaError(f"{LIB_PATH} missing: build it with __graft_entry__.build() "
+                       "(make -C csrc); the attack path has no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise MiaError(f"{name} failed ({rc}): {lib.mia_last_error_string().decode()}")
+    return rc

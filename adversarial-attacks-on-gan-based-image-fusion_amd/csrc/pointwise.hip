@@ -1,0 +1,827 @@
+// HBM-bound kernels of the attack step (gfx950): bias/act, StyledConv backward front, ToRGB,
+// upfirdn2d, max/avg pooling, MSE pieces, image layout changes and the PGD sign-project step.
+// Feature maps are NHWC and moved in 16-byte vectors (4 fp32 / 8 fp16|bf16 per lane).
+#include "mia_common.h"
+
+namespace mia {
+
+constexpr int TPB = 256;
+
+static inline int blocks_for(int64_t n, int per_block = TPB, int cap = 1 << 20) {
+  int64_t b = (n + per_block - 1) / per_block;
+  if (b < 1) b = 1;
+  return (int)(b > cap ? cap : b);
+}
+
+// ---------------------------------------------------------------------------------------------
+// K4 forward, standalone: y = lrelu(x + nw·noise[p] + b[c])·√2 (rosinality FusedLeakyReLU after
+// NoiseInjection). The fused path writes `pre` from the conv epilogue instead.
+template <typename T>
+__global__ void bias_act_fwd_kernel(const T* __restrict__ x, const float* __restrict__ noise,
+                                    float nw, const float* __restrict__ bias, T* __restrict__ y,
+                                    int64_t nvec, int C, int HW) {
+  typedef typename Vec<T>::type VT;
+  constexpr int V = Vec<T>::N;
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * TPB) {
+    const int64_t e0 = i * V;
+    const int c0 = (int)(e0 % C);
+    const int p = (int)((e0 / C) % HW);
+    VT v = ((const VT*)x)[i];
+    const float nz = noise ? nw * noise[p] : 0.f;
+#pragma unroll
+    for (int e = 0; e < V; ++e) v[e] = from_f<T>(lrelu_s2(to_f(v[e]) + nz + (bias ? bias[c0 + e] : 0.f)));
+    ((VT*)y)[i] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// StyledConv backward front. One block = a run of pixels of one image, all channels.
+template <typename T>
+__global__ void bias_act_bwd_kernel(const T* __restrict__ g_a, const T* __restrict__ pre,
+                                    const float* __restrict__ noise, float nw,
+                                    const float* __restrict__ bias, const float* __restrict__ demod,
+                                    T* __restrict__ gy, float* __restrict__ q, int H, int W, int C,
+                                    int unshuffle, int pix_per_block) {
+  typedef typename Vec<T>::type VT;
+  constexpr int V = Vec<T>::N;
+  __shared__ float red[TPB * 8];
+  const int n = blockIdx.y;
+  const int HW = H * W;
+  const int tpp = C / V;             // threads per pixel (≤ 256)
+  const int ppp = TPB / tpp;         // pixels per pass
+  const int t = threadIdx.x;
+  const int chunk = t % tpp, sub = t / tpp;
+  const int c0 = chunk * V;
+  float qa[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) qa[e] = 0.f;
+  float dm[V], bs[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    dm[e] = demod[(size_t)n * C + c0 + e];
+    bs[e] = bias ? bias[c0 + e] : 0.f;
+  }
+  const int p_begin = blockIdx.x * pix_per_block;
+  const int p_end = min(p_begin + pix_per_block, HW);
+  if (sub < ppp) {
+    for (int p = p_begin + sub; p < p_end; p += ppp) {
+      const size_t off = ((size_t)n * HW + p) * C + c0;
+      const VT ga = *(const VT*)(g_a + off);
+      const VT pr = *(const VT*)(pre + off);
+      const float nz = noise ? nw * noise[p] : 0.f;
+      VT o;
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float pv = to_f(pr[e]);
+        const float gp = to_f(ga[e]) * lrelu_s2_grad(pv);
+        qa[e] += gp * (pv - nz - bs[e]);
+        o[e] = from_f<T>(gp * dm[e]);
+      }
+      size_t ooff = off;
+      if (unshuffle) {
+        const int y = p / W, x = p - (p / W) * W;
+        const int R = H / 2, Rw = W / 2;
+        const int ph = ((y & 1) << 1) | (x & 1);
+        ooff = (((size_t)n * R + (y >> 1)) * Rw + (x >> 1)) * (4 * C) + ph * C + c0;
+      }
+      *(VT*)(gy + ooff) = o;
+    }
+  }
+  // reduce q over the `ppp` pixel lanes sharing a channel chunk
+#pragma unroll
+  for (int e = 0; e < V; ++e) red[t * V + e] = qa[e];
+  __syncthreads();
+  if (sub == 0) {
+    for (int s = 1; s < ppp; ++s)
+#pragma unroll
+      for (int e = 0; e < V; ++e) qa[e] += red[(s * tpp + chunk) * V + e];
+#pragma unroll
+    for (int e = 0; e < V; ++e) atomicAdd(&q[(size_t)n * C + c0 + e], qa[e]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// upfirdn2d on fp32 NCHW planes with a separable kernel (rosinality op/upfirdn2d semantics).
+__device__ __forceinline__ float upfir_at(const float* __restrict__ x, int H, int W, int oy, int ox,
+                                          const float* kf, int kt, int up, int down, int pad0) {
+  float acc = 0.f;
+  for (int jy = 0; jy < kt; ++jy) {
+    const int ty = oy * down + jy - pad0;
+    if (ty < 0 || ty % up) continue;
+    const int iy = ty / up;
+    if (iy >= H) continue;
+    for (int jx = 0; jx < kt; ++jx) {
+      const int tx = ox * down + jx - pad0;
+      if (tx < 0 || tx % up) continue;
+      const int ix = tx / up;
+      if (ix >= W) continue;
+      acc += x[iy * W + ix] * kf[jy] * kf[jx];
+    }
+  }
+  return acc;
+}
+
+struct Taps8 { float k[8]; };
+
+__global__ void upfirdn2d_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int planes,
+                                     int H, int W, int Ho, int Wo, Taps8 kf, int kt, int up,
+                                     int down, int pad0) {
+  const int64_t total = (int64_t)planes * Ho * Wo;
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
+    const int ox = (int)(i % Wo);
+    const int oy = (int)((i / Wo) % Ho);
+    const int64_t pl = i / ((int64_t)Wo * Ho);
+    y[i] = upfir_at(x + pl * H * W, H, W, oy, ox, kf.k, kt, up, down, pad0);
+  }
+}
+
+__global__ void upfirdn2d_bwd_kernel(const float* __restrict__ gy, float* __restrict__ gx,
+                                     int planes, int H, int W, int Ho, int Wo, Taps8 kf, int kt,
+                                     int up, int down, int pad0) {
+  const int64_t total = (int64_t)planes * H * W;
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
+    const int ix = (int)(i % W);
+    const int iy = (int)((i / W) % H);
+    const int64_t pl = i / ((int64_t)W * H);
+    const float* g = gy + pl * Ho * Wo;
+    float acc = 0.f;
+    for (int jy = 0; jy < kt; ++jy) {
+      const int sy = iy * up + pad0 - jy;  // = oy*down
+      if (sy < 0 || sy % down) continue;
+      const int oy = sy / down;
+      if (oy >= Ho) continue;
+      for (int jx = 0; jx < kt; ++jx) {
+        const int sx = ix * up + pad0 - jx;
+        if (sx < 0 || sx % down) continue;
+        const int ox = sx / down;
+        if (ox >= Wo) continue;
+        acc += g[oy * Wo + ox] * kf.k[jy] * kf.k[jx];
+      }
+    }
+    gx[i] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// ToRGB (1x1 modulated conv without demod) + bias + up-sampled skip. A group of `tpp` lanes owns a
+// pixel (each lane a slice of channels); the 3 partial dot products are reduced by shuffles.
+__constant__ float kUp4[4] = {0.25f, 0.75f, 0.75f, 0.25f};  // [1,3,3,1]/sum · 2 (per axis)
+
+template <typename T>
+__global__ void torgb_fwd_kernel(const T* __restrict__ pre, const float* __restrict__ s,
+                                 const float* __restrict__ wr, const float* __restrict__ bias,
+                                 const float* __restrict__ skip, float* __restrict__ rgb, int H,
+                                 int W, int Cin, int tpp, int cpt, int pix_per_block) {
+  typedef typename Vec<T>::type VT;
+  constexpr int V = Vec<T>::N;
+  extern __shared__ float wm[];  // [3][Cin]
+  const int n = blockIdx.y;
+  for (int i = threadIdx.x; i < 3 * Cin; i += TPB) wm[i] = wr[i] * s[(size_t)n * Cin + (i % Cin)];
+  __syncthreads();
+  const int HW = H * W;
+  const int t = threadIdx.x;
+  const int g = t % tpp, sub = t / tpp, ppp = TPB / tpp;
+  const int p_begin = blockIdx.x * pix_per_block;
+  const int p_end = min(p_begin + pix_per_block, HW);
+  for (int pb = p_begin; pb < p_end; pb += ppp) {
+    const int p = pb + sub;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    if (p < p_end) {
+      const T* row = pre + ((size_t)n * HW + p) * Cin;
+      for (int cc = 0; cc < cpt; ++cc) {
+        const int c0 = (g + cc * tpp) * V;
+        const VT v = *(const VT*)(row + c0);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          const float a = lrelu_s2(to_f(v[e]));
+          a0 += a * wm[c0 + e];
+          a1 += a * wm[Cin + c0 + e];
+          a2 += a * wm[2 * Cin + c0 + e];
+        }
+      }
+    }
+    for (int o = 1; o < tpp; o <<= 1) {
+      a0 += __shfl_xor(a0, o, 64);
+      a1 += __shfl_xor(a1, o, 64);
+      a2 += __shfl_xor(a2, o, 64);
+    }
+    if (g == 0 && p < p_end) {
+      const int y = p / W, x = p - (p / W) * W;
+      float r[3] = {a0 + bias[0], a1 + bias[1], a2 + bias[2]};
+      if (skip) {
+        const int Hs = H / 2, Ws = W / 2;
+        for (int c = 0; c < 3; ++c)
+          r[c] += upfir_at(skip + ((size_t)n * 3 + c) * Hs * Ws, Hs, Ws, y, x, kUp4, 4, 2, 1, 2);
+      }
+      for (int c = 0; c < 3; ++c) rgb[((size_t)n * 3 + c) * HW + p] = r[c];
+    }
+  }
+}
+
+template <typename T>
+__global__ void torgb_bwd_kernel(const float* __restrict__ grgb, const T* __restrict__ pre,
+                                 const float* __restrict__ s, const float* __restrict__ wr,
+                                 T* __restrict__ g_a, float* __restrict__ gs, int H, int W, int Cin,
+                                 int accumulate, int pix_per_block) {
+  typedef typename Vec<T>::type VT;
+  constexpr int V = Vec<T>::N;
+  extern __shared__ float sh[];  // wr [3][Cin], s [Cin], partials [TPB/tpp][Cin]
+  const int n = blockIdx.y;
+  float* w3 = sh;
+  float* sn = sh + 3 * Cin;
+  float* part = sh + 4 * Cin;
+  for (int i = threadIdx.x; i < 3 * Cin; i += TPB) w3[i] = wr[i];
+  for (int i = threadIdx.x; i < Cin; i += TPB) sn[i] = s[(size_t)n * Cin + i];
+  __syncthreads();
+  const int HW = H * W;
+  const int nch = Cin / V;                // chunks per pixel
+  const int tpp = nch < TPB ? nch : TPB;  // one chunk per thread
+  const int ppp = TPB / tpp;
+  const int t = threadIdx.x;
+  const int chunk = t % tpp, sub = t / tpp;
+  const int c0 = chunk * V;
+  float acc[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc[e] = 0.f;
+  const int p_begin = blockIdx.x * pix_per_block;
+  const int p_end = min(p_begin + pix_per_block, HW);
+  if (sub < ppp) {
+    for (int p = p_begin + sub; p < p_end; p += ppp) {
+      const float g0 = grgb[((size_t)n * 3 + 0) * HW + p];
+      const float g1 = grgb[((size_t)n * 3 + 1) * HW + p];
+      const float g2 = grgb[((size_t)n * 3 + 2) * HW + p];
+      const size_t off = ((size_t)n * HW + p) * Cin + c0;
+      const VT pr = *(const VT*)(pre + off);
+      VT ga;
+      if (accumulate) ga = *(const VT*)(g_a + off);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const int c = c0 + e;
+        const float u = g0 * w3[c] + g1 * w3[Cin + c] + g2 * w3[2 * Cin + c];
+        acc[e] += lrelu_s2(to_f(pr[e])) * u;
+        const float gv = sn[c] * u + (accumulate ? to_f(ga[e]) : 0.f);
+        ga[e] = from_f<T>(gv);
+      }
+      *(VT*)(g_a + off) = ga;
+    }
+  }
+  if (sub < ppp) {
+#pragma unroll
+    for (int e = 0; e < V; ++e) part[sub * Cin + c0 + e] = acc[e];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < Cin; c += TPB) {
+    float sum = 0.f;
+    for (int sb = 0; sb < ppp; ++sb) sum += part[sb * Cin + c];
+    atomicAdd(&gs[(size_t)n * Cin + c], sum);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// MaxPool 2x2 stride 2 (NHWC), PyTorch semantics incl. ceil_mode and first-max tie rule.
+template <typename T>
+__global__ void maxpool2_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int H,
+                                    int W, int C, int Ho, int Wo) {
+  typedef typename Vec<T>::type VT;
+  constexpr int V = Vec<T>::N;
+  const int nc = C / V;
+  const int64_t total = (int64_t)N * Ho * Wo * nc;
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
+    const int cv = (int)(i % nc);
+    const int64_t pix = i / nc;
+    const int ox = (int)(pix % Wo);
+    const int oy = (int)((pix / Wo) % Ho);
+    const int n = (int)(pix / ((int64_t)Wo * Ho));
+    VT best;
+    bool first = true;
+    for (int dy = 0; dy < 2; ++dy) {
+      const int yy = 2 * oy + dy;
+      if (yy >= H) continue;
+      for (int dx = 0; dx < 2; ++dx) {
+        const int xx = 2 * ox + dx;
+        if (xx >= W) continue;
+        const VT v = *(const VT*)(x + (((size_t)n * H + yy) * W + xx) * C + cv * V);
+        if (first) { best = v; first = false; }
+        else {
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            const float fv = to_f(v[e]), fb = to_f(best[e]);
+            if (fv > fb || fv != fv) best[e] = v[e];
+          }
+        }
+      }
+    }
+    *(VT*)(y + pix * C + cv * V) = best;
+  }
+}
+
+template <typename T>
+__global__ void maxpool2_bwd_kernel(const T* __restrict__ x, const T* __restrict__ gout,
+                                    T* __restrict__ gin, int N, int H, int W, int C, int Ho, int Wo,
+                                    const T* __restrict__ tap_t, float tap_coef, int mask) {
+  typedef typename Vec<T>::type VT;
+  constexpr int V = Vec<T>::N;
+  const int nc = C / V;
+  const int64_t total = (int64_t)N * H * W * nc;
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
+    const int cv = (int)(i % nc);
+    const int64_t pix = i / nc;
+    const int xx = (int)(pix % W);
+    const int yy = (int)((pix / W) % H);
+    const int n = (int)(pix / ((int64_t)W * H));
+    const int oy = yy >> 1, ox = xx >> 1;
+    float res[V];
+    const VT xv = *(const VT*)(x + pix * C + cv * V);
+    if (oy < Ho && ox < Wo) {
+      // first-max position of the window, per channel
+      float bv[V];
+      int bpos[V];
+      bool first = true;
+      for (int dy = 0; dy < 2; ++dy) {
+        const int y2 = 2 * oy + dy;
+        if (y2 >= H) continue;
+        for (int dx = 0; dx < 2; ++dx) {
+          const int x2 = 2 * ox + dx;
+          if (x2 >= W) continue;
+          const VT v = *(const VT*)(x + (((size_t)n * H + y2) * W + x2) * C + cv * V);
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            const float fv = to_f(v[e]);
+            if (first || fv > bv[e] || fv != fv) { bv[e] = fv; bpos[e] = dy * 2 + dx; }
+          }
+          first = false;
+        }
+      }
+      const VT go = *(const VT*)(gout + (((size_t)n * Ho + oy) * Wo + ox) * C + cv * V);
+      const int me = (yy - 2 * oy) * 2 + (xx - 2 * ox);
+#pragma unroll
+      for (int e = 0; e < V; ++e) res[e] = bpos[e] == me ? to_f(go[e]) : 0.f;
+    } else {
+#pragma unroll
+      for (int e = 0; e < V; ++e) res[e] = 0.f;
+    }
+    VT out;
+    VT tt;
+    if (tap_t) tt = *(const VT*)(tap_t + pix * C + cv * V);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      float r = res[e];
+      const float xf = to_f(xv[e]);
+      if (tap_t) r += tap_coef * (xf - to_f(tt[e]));
+      if (mask && !(xf > 0.f)) r = 0.f;
+      out[e] = from_f<T>(r);
+    }
+    *(VT*)(gin + pix * C + cv * V) = out;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// avg_pool2d(k, stride k) on fp32 NCHW planes and its backward.
+__global__ void avgpool_fwd_kernel(const float* __restrict__ x, float* __restrict__ y, int planes,
+                                   int H, int W, int k) {
+  const int Ho = H / k, Wo = W / k;
+  const int64_t total = (int64_t)planes * Ho * Wo;
+  const float inv = 1.f / (float)(k * k);
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
+    const int ox = (int)(i % Wo);
+    const int oy = (int)((i / Wo) % Ho);
+    const int64_t pl = i / ((int64_t)Wo * Ho);
+    const float* xp = x + pl * H * W + (size_t)oy * k * W + ox * k;
+    float acc = 0.f;
+    for (int dy = 0; dy < k; ++dy)
+      for (int dx = 0; dx < k; ++dx) acc += xp[dy * W + dx];
+    y[i] = acc * inv;
+  }
+}
+
+__global__ void avgpool_bwd_kernel(const float* __restrict__ gy, float* __restrict__ gx,
+                                   int planes, int H, int W, int k, int accumulate) {
+  const int Ho = H / k, Wo = W / k;
+  const int64_t total = (int64_t)planes * H * W;
+  const float inv = 1.f / (float)(k * k);
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
+    const int ix = (int)(i % W);
+    const int iy = (int)((i / W) % H);
+    const int64_t pl = i / ((int64_t)W * H);
+    const int oy = iy / k, ox = ix / k;
+    float v = (oy < Ho && ox < Wo) ? gy[pl * Ho * Wo + oy * Wo + ox] * inv : 0.f;
+    if (accumulate) v += gx[i];
+    gx[i] = v;
+  }
+}
+
+// NCHW fp32 (N,3,S,S) → avg_pool(pf) → NHWC (N,S/pf,S/pf,cpad) in T, channels ≥ 3 zero.
+template <typename T>
+__global__ void image_to_nhwc_kernel(const float* __restrict__ x, T* __restrict__ y, int N, int S,
+                                     int pf, int cpad) {
+  const int R = S / pf;
+  const int64_t total = (int64_t)N * R * R * cpad;
+  const float inv = 1.f / (float)(pf * pf);
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
+    const int c = (int)(i % cpad);
+    const int64_t pix = i / cpad;
+    const int xo = (int)(pix % R);
+    const int yo = (int)((pix / R) % R);
+    const int n = (int)(pix / ((int64_t)R * R));
+    float v = 0.f;
+    if (c < 3) {
+      const float* xp = x + (((size_t)n * 3 + c) * S + (size_t)yo * pf) * S + xo * pf;
+      for (int dy = 0; dy < pf; ++dy)
+        for (int dx = 0; dx < pf; ++dx) v += xp[dy * S + dx];
+      v *= inv;
+    }
+    y[i] = from_f<T>(v);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// MSE pieces (K10).
+template <typename T>
+__global__ void mse_sum_kernel(const T* __restrict__ a, const T* __restrict__ b,
+                               float* __restrict__ loss, int64_t len) {
+  const int n = blockIdx.y;
+  const T* pa = a + (size_t)n * len;
+  const T* pb = b + (size_t)n * len;
+  float acc = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < len; i += (int64_t)gridDim.x * TPB) {
+    const float d = to_f(pa[i]) - to_f(pb[i]);
+    acc += d * d;
+  }
+  __shared__ float red[TPB / 64];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < TPB / 64; ++w) s += red[w];
+    atomicAdd(&loss[n], s);
+  }
+}
+
+__global__ void mse_grad_f32_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                    float* __restrict__ g, int64_t len, float coef, int accumulate) {
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < len; i += (int64_t)gridDim.x * TPB) {
+    float v = coef * (a[i] - b[i]);
+    if (accumulate) v += g[i];
+    g[i] = v;
+  }
+}
+
+template <typename T>
+__global__ void tap_grad_kernel(const T* __restrict__ a, const T* __restrict__ t, T* __restrict__ g,
+                                int64_t len, float coef, int mask) {
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < len; i += (int64_t)gridDim.x * TPB) {
+    const float av = to_f(a[i]);
+    float v = coef * (av - to_f(t[i]));
+    if (mask && !(av > 0.f)) v = 0.f;
+    g[i] = from_f<T>(v);
+  }
+}
+
+template <typename T>
+__global__ void image_grad_kernel(const float* __restrict__ rec, const float* __restrict__ t,
+                                  const T* __restrict__ gv, float* __restrict__ gimg, int N, int S,
+                                  int pf, int cpad, float coef) {
+  const int R = S / pf;
+  const int64_t total = (int64_t)N * 3 * S * S;
+  const float inv = 1.f / (float)(pf * pf);
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
+    const int x = (int)(i % S);
+    const int y = (int)((i / S) % S);
+    const int c = (int)((i / ((int64_t)S * S)) % 3);
+    const int n = (int)(i / ((int64_t)S * S * 3));
+    float g = coef * (rec[i] - t[i]);
+    if (gv) g += to_f(gv[(((size_t)n * R + y / pf) * R + x / pf) * cpad + c]) * inv;
+    gimg[i] = g;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K11: PGD step with cost = −L (interpolation.py:92-94; torchattacks targeted form :83-86).
+// Every operation is a single fp32 op with no contraction opportunity (a·sign is exact), so for an
+// identical gradient the result is bit-identical to torch's fp32 CPU ops.
+__device__ __forceinline__ float project1(float xa, float x0, float g, float a, float e, float lo,
+                                          float hi) {
+#pragma clang fp contract(off)
+  const float sg = g < 0.f ? 1.f : (g > 0.f ? -1.f : 0.f);  // sign(−g)
+  float adv = xa + a * sg;
+  float d = adv - x0;
+  d = fminf(fmaxf(d, -e), e);
+  float r = x0 + d;
+  return fminf(fmaxf(r, lo), hi);
+}
+
+__global__ void random_start_kernel(float* __restrict__ x, const float* __restrict__ x0,
+                                    const float* __restrict__ u, int64_t len, float e, float lo,
+                                    float hi) {
+#pragma clang fp contract(off)
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < len; i += (int64_t)gridDim.x * TPB) {
+    const float ue = e * u[i];  // rounded separately (no contraction), as torch mul then add
+    x[i] = fminf(fmaxf(x0[i] + ue, lo), hi);
+  }
+}
+
+__global__ void sign_project_kernel(float* __restrict__ x, const float* __restrict__ x0,
+                                    const float* __restrict__ g, int64_t len, float a, float e,
+                                    float lo, float hi) {
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < len; i += (int64_t)gridDim.x * TPB)
+    x[i] = project1(x[i], x0[i], g[i], a, e, lo, hi);
+}
+
+template <typename T>
+__global__ void pgd_update_kernel(float* __restrict__ x, const float* __restrict__ x0,
+                                  const T* __restrict__ gv, const float* __restrict__ genc, int N,
+                                  int S, int pf, int cpad, int enc_res, float coef_img, float a,
+                                  float e, float lo, float hi) {
+  const int R = S / pf;
+  const int ek = S / enc_res;
+  const float inv_pf = 1.f / (float)(pf * pf);
+  const float inv_ek = 1.f / (float)(ek * ek);
+  const int64_t total = (int64_t)N * 3 * S * S;
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
+    const int xx = (int)(i % S);
+    const int yy = (int)((i / S) % S);
+    const int c = (int)((i / ((int64_t)S * S)) % 3);
+    const int n = (int)(i / ((int64_t)S * S * 3));
+    const float xv = x[i], x0v = x0[i];
+    float g = coef_img * (xv - x0v);
+    if (gv) g += to_f(gv[(((size_t)n * R + yy / pf) * R + xx / pf) * cpad + c]) * inv_pf;
+    if (genc) g += genc[(((size_t)n * 3 + c) * enc_res + yy / ek) * enc_res + xx / ek] * inv_ek;
+    x[i] = project1(xv, x0v, g, a, e, lo, hi);
+  }
+}
+
+// K12: Adam on pixels (torch.optim.Adam single-tensor semantics, no weight decay).
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, int64_t len, float lr, float b1, float b2,
+                            float eps, float bc1, float bc2sqrt) {
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < len; i += (int64_t)gridDim.x * TPB) {
+    const float gi = g[i];
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2sqrt + eps;
+    p[i] = p[i] - (lr / bc1) * (mi / denom);
+  }
+}
+
+__global__ void repeat_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                              int64_t bytes, int count) {
+  const int64_t total = bytes * count;
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB)
+    dst[i] = src[i % bytes];
+}
+
+}  // namespace mia
+
+using namespace mia;
+
+#define MIA_LAUNCH(kern, grid, block, shmem, ...)                                  \
+  do {                                                                             \
+    hipLaunchKernelGGL(kern, grid, block, shmem, (hipStream_t)stream, __VA_ARGS__); \
+    return check_launch(#kern);                                                    \
+  } while (0)
+
+extern "C" int mia_bias_act_fwd(const void* x, const float* noise, float noise_w,
+                                const float* bias, void* y, int N, int H, int W, int C, int dtype,
+                                void* stream) {
+  MIA_CHECK_ARG(x && y && N > 0 && H > 0 && W > 0 && C > 0, "bad args");
+  const int V = dtype == MIA_F32 ? 4 : 8;
+  MIA_CHECK_ARG(C % V == 0, "C must be a multiple of the vector width");
+  const int64_t nvec = (int64_t)N * H * W * C / V;
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH(bias_act_fwd_kernel<T>, dim3(blocks_for(nvec, TPB, 65536)), dim3(TPB), 0,
+                 (const T*)x, noise, noise_w, bias, (T*)y, nvec, C, H * W));
+  return MIA_OK;
+}
+
+extern "C" int mia_bias_act_bwd(const void* g_a, const void* pre, const float* noise,
+                                float noise_w, const float* bias, const float* demod, void* gy,
+                                float* q, int N, int H, int W, int C, int unshuffle, int dtype,
+                                void* stream) {
+  MIA_CHECK_ARG(g_a && pre && demod && gy && q, "bad args");
+  const int V = dtype == MIA_F32 ? 4 : 8;
+  MIA_CHECK_ARG(C % V == 0 && C / V <= TPB && (TPB % (C / V)) == 0, "C/V must divide 256");
+  MIA_CHECK_ARG(!unshuffle || (H % 2 == 0 && W % 2 == 0), "unshuffle needs even H, W");
+  const int HW = H * W;
+  const int ppp = TPB / (C / V);
+  const int ppb = ppp * 16;
+  dim3 grid((HW + ppb - 1) / ppb, N);
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH(bias_act_bwd_kernel<T>, grid, dim3(TPB), 0, (const T*)g_a, (const T*)pre, noise,
+                 noise_w, bias, demod, (T*)gy, q, H, W, C, unshuffle, ppb));
+  return MIA_OK;
+}
+
+static int make_taps(const float* k1d, int ktaps, Taps8* kf) {
+  if (ktaps < 1 || ktaps > 8) return mia::set_error("upfirdn2d: 1..8 taps");
+  for (int j = 0; j < 8; ++j) kf->k[j] = 0.f;
+  for (int j = 0; j < ktaps; ++j) kf->k[j] = k1d[ktaps - 1 - j];  // flipped (correlation form)
+  return MIA_OK;
+}
+
+extern "C" int mia_upfirdn2d_fwd(const float* x, float* y, int planes, int H, int W,
+                                 const float* k1d, int ktaps, int up, int down, int pad0, int pad1,
+                                 void* stream) {
+  MIA_CHECK_ARG(x && y && k1d && up >= 1 && down >= 1, "bad args");
+  Taps8 kf;
+  if (make_taps(k1d, ktaps, &kf)) return MIA_EINVAL;
+  const int Ho = (H * up + pad0 + pad1 - ktaps) / down + 1;
+  const int Wo = (W * up + pad0 + pad1 - ktaps) / down + 1;
+  MIA_CHECK_ARG(Ho > 0 && Wo > 0, "empty output");
+  const int64_t total = (int64_t)planes * Ho * Wo;
+  MIA_LAUNCH(upfirdn2d_fwd_kernel, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0, x, y, planes,
+             H, W, Ho, Wo, kf, ktaps, up, down, pad0);
+}
+
+extern "C" int mia_upfirdn2d_bwd(const float* gy, float* gx, int planes, int H, int W,
+                                 const float* k1d, int ktaps, int up, int down, int pad0, int pad1,
+                                 void* stream) {
+  MIA_CHECK_ARG(gy && gx && k1d && up >= 1 && down >= 1, "bad args");
+  Taps8 kf;
+  if (make_taps(k1d, ktaps, &kf)) return MIA_EINVAL;
+  const int Ho = (H * up + pad0 + pad1 - ktaps) / down + 1;
+  const int Wo = (W * up + pad0 + pad1 - ktaps) / down + 1;
+  MIA_CHECK_ARG(Ho > 0 && Wo > 0, "empty output");
+  const int64_t total = (int64_t)planes * H * W;
+  MIA_LAUNCH(upfirdn2d_bwd_kernel, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0, gy, gx,
+             planes, H, W, Ho, Wo, kf, ktaps, up, down, pad0);
+}
+
+extern "C" int mia_torgb_fwd(const void* pre, const float* style, const float* wr,
+                             const float* bias, const float* skip, float* rgb, int N, int H, int W,
+                             int Cin, int dtype, void* stream) {
+  MIA_CHECK_ARG(pre && style && wr && bias && rgb, "bad args");
+  const int V = dtype == MIA_F32 ? 4 : 8;
+  MIA_CHECK_ARG(Cin % V == 0, "Cin must be a multiple of the vector width");
+  int nch = Cin / V;
+  int tpp = 1;
+  while (tpp * 2 <= nch && tpp * 2 <= 64) tpp *= 2;
+  MIA_CHECK_ARG(nch % tpp == 0, "Cin/V must be a power of two times tpp");
+  const int cpt = nch / tpp;
+  const int ppb = (TPB / tpp) * 8;
+  dim3 grid((H * W + ppb - 1) / ppb, N);
+  const size_t sh = 3 * Cin * sizeof(float);
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH(torgb_fwd_kernel<T>, grid, dim3(TPB), sh, (const T*)pre, style, wr, bias, skip,
+                 rgb, H, W, Cin, tpp, cpt, ppb));
+  return MIA_OK;
+}
+
+extern "C" int mia_torgb_bwd(const float* g_rgb, const void* pre, const float* style,
+                             const float* wr, void* g_a, float* gs, int N, int H, int W, int Cin,
+                             int accumulate, int dtype, void* stream) {
+  MIA_CHECK_ARG(g_rgb && pre && style && wr && g_a && gs, "bad args");
+  const int V = dtype == MIA_F32 ? 4 : 8;
+  MIA_CHECK_ARG(Cin % V == 0 && Cin / V <= TPB && TPB % (Cin / V) == 0, "Cin/V must divide 256");
+  const int ppp = TPB / (Cin / V);
+  const int ppb = ppp * 16;
+  dim3 grid((H * W + ppb - 1) / ppb, N);
+  const size_t sh = (4 * Cin + (size_t)ppp * Cin) * sizeof(float);
+  MIA_CHECK_ARG(sh <= 64 * 1024, "LDS budget");
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH(torgb_bwd_kernel<T>, grid, dim3(TPB), sh, g_rgb, (const T*)pre, style, wr, (T*)g_a,
+                 gs, H, W, Cin, accumulate, ppb));
+  return MIA_OK;
+}
+
+static inline int pool_out(int H, int ceil_mode) { return ceil_mode ? (H + 1) / 2 : H / 2; }
+
+extern "C" int mia_maxpool2_fwd(const void* x, void* y, int N, int H, int W, int C, int ceil_mode,
+                                int dtype, void* stream) {
+  MIA_CHECK_ARG(x && y && H >= 2 && W >= 2, "bad args");
+  const int V = dtype == MIA_F32 ? 4 : 8;
+  MIA_CHECK_ARG(C % V == 0, "C must be a multiple of the vector width");
+  const int Ho = pool_out(H, ceil_mode), Wo = pool_out(W, ceil_mode);
+  const int64_t total = (int64_t)N * Ho * Wo * (C / V);
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH(maxpool2_fwd_kernel<T>, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0,
+                 (const T*)x, (T*)y, N, H, W, C, Ho, Wo));
+  return MIA_OK;
+}
+
+extern "C" int mia_maxpool2_bwd(const void* x, const void* g_out, void* g_in, int N, int H, int W,
+                                int C, int ceil_mode, const void* tap_t, float tap_coef, int mask,
+                                int dtype, void* stream) {
+  MIA_CHECK_ARG(x && g_out && g_in && H >= 2 && W >= 2, "bad args");
+  const int V = dtype == MIA_F32 ? 4 : 8;
+  MIA_CHECK_ARG(C % V == 0, "C must be a multiple of the vector width");
+  const int Ho = pool_out(H, ceil_mode), Wo = pool_out(W, ceil_mode);
+  const int64_t total = (int64_t)N * H * W * (C / V);
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH(maxpool2_bwd_kernel<T>, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0,
+                 (const T*)x, (const T*)g_out, (T*)g_in, N, H, W, C, Ho, Wo, (const T*)tap_t,
+                 tap_coef, mask));
+  return MIA_OK;
+}
+
+extern "C" int mia_avgpool_fwd(const float* x, float* y, int planes, int H, int W, int k,
+                               void* stream) {
+  MIA_CHECK_ARG(x && y && k >= 1 && H >= k && W >= k, "bad args");
+  const int64_t total = (int64_t)planes * (H / k) * (W / k);
+  MIA_LAUNCH(avgpool_fwd_kernel, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0, x, y, planes,
+             H, W, k);
+}
+
+extern "C" int mia_avgpool_bwd(const float* gy, float* gx, int planes, int H, int W, int k,
+                               int accumulate, void* stream) {
+  MIA_CHECK_ARG(gy && gx && k >= 1 && H >= k && W >= k, "bad args");
+  const int64_t total = (int64_t)planes * H * W;
+  MIA_LAUNCH(avgpool_bwd_kernel, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0, gy, gx, planes,
+             H, W, k, accumulate);
+}
+
+extern "C" int mia_image_to_nhwc(const float* x, void* y, int N, int S, int pf, int cpad,
+                                 int dtype, void* stream) {
+  MIA_CHECK_ARG(x && y && pf >= 1 && S % pf == 0 && cpad >= 3, "bad args");
+  const int R = S / pf;
+  const int64_t total = (int64_t)N * R * R * cpad;
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH(image_to_nhwc_kernel<T>, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0, x,
+                 (T*)y, N, S, pf, cpad));
+  return MIA_OK;
+}
+
+extern "C" int mia_mse_sum(const void* a, const void* b, float* loss, int n, int64_t len,
+                           int dtype, void* stream) {
+  MIA_CHECK_ARG(a && b && loss && n > 0 && len > 0, "bad args");
+  dim3 grid(blocks_for(len, TPB, 1024), n);
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH(mse_sum_kernel<T>, grid, dim3(TPB), 0, (const T*)a, (const T*)b, loss, len));
+  return MIA_OK;
+}
+
+extern "C" int mia_mse_grad_f32(const float* a, const float* b, float* g, int64_t len, float coef,
+                                int accumulate, void* stream) {
+  MIA_CHECK_ARG(a && b && g && len > 0, "bad args");
+  MIA_LAUNCH(mse_grad_f32_kernel, dim3(blocks_for(len, TPB, 65536)), dim3(TPB), 0, a, b, g, len,
+             coef, accumulate);
+}
+
+extern "C" int mia_tap_grad(const void* a, const void* t, void* g, int64_t len, float coef,
+                            int mask, int dtype, void* stream) {
+  MIA_CHECK_ARG(a && t && g && len > 0, "bad args");
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH(tap_grad_kernel<T>, dim3(blocks_for(len, TPB, 65536)), dim3(TPB), 0, (const T*)a,
+                 (const T*)t, (T*)g, len, coef, mask));
+  return MIA_OK;
+}
+
+extern "C" int mia_image_grad(const float* rec, const float* t, const void* g_vgg, float* g_img,
+                              int N, int S, int pf, int cpad, float coef, int dtype, void* stream) {
+  MIA_CHECK_ARG(rec && t && g_img && pf >= 1 && S % pf == 0, "bad args");
+  const int64_t total = (int64_t)N * 3 * S * S;
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH(image_grad_kernel<T>, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0, rec, t,
+                 (const T*)g_vgg, g_img, N, S, pf, cpad, coef));
+  return MIA_OK;
+}
+
+extern "C" int mia_pgd_update(float* x, const float* x0, const void* g_vgg, const float* g_enc,
+                              int N, int S, int pf, int cpad, int enc_res, float coef_img, float a,
+                              float e, float lo, float hi, int dtype, void* stream) {
+  MIA_CHECK_ARG(x && x0 && pf >= 1 && S % pf == 0 && enc_res >= 1 && S % enc_res == 0, "bad args");
+  const int64_t total = (int64_t)N * 3 * S * S;
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH(pgd_update_kernel<T>, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0, x, x0,
+                 (const T*)g_vgg, g_enc, N, S, pf, cpad, enc_res, coef_img, a, e, lo, hi));
+  return MIA_OK;
+}
+
+extern "C" int mia_random_start(float* x, const float* x0, const float* u, int64_t len, float e,
+                                float lo, float hi, void* stream) {
+  MIA_CHECK_ARG(x && x0 && u && len > 0, "bad args");
+  MIA_LAUNCH(random_start_kernel, dim3(blocks_for(len, TPB, 65536)), dim3(TPB), 0, x, x0, u, len,
+             e, lo, hi);
+}
+
+extern "C" int mia_sign_project(float* x, const float* x0, const float* g, int64_t len, float a,
+                                float e, float lo, float hi, void* stream) {
+  MIA_CHECK_ARG(x && x0 && g && len > 0, "bad args");
+  MIA_LAUNCH(sign_project_kernel, dim3(blocks_for(len, TPB, 65536)), dim3(TPB), 0, x, x0, g, len,
+             a, e, lo, hi);
+}
+
+extern "C" int mia_adam_step(float* p, const float* g, float* m, float* v, int64_t len, float lr,
+                             float beta1, float beta2, float eps, int t, void* stream) {
+  MIA_CHECK_ARG(p && g && m && v && len > 0 && t >= 1, "bad args");
+  const float bc1 = 1.f - powf(beta1, (float)t);
+  const float bc2sqrt = sqrtf(1.f - powf(beta2, (float)t));
+  MIA_LAUNCH(adam_kernel, dim3(blocks_for(len, TPB, 65536)), dim3(TPB), 0, p, g, m, v, len, lr,
+             beta1, beta2, eps, bc1, bc2sqrt);
+}
+
+extern "C" int mia_repeat(const void* src, void* dst, int64_t bytes, int count, void* stream) {
+  MIA_CHECK_ARG(src && dst && bytes > 0 && count > 0, "bad args");
+  MIA_LAUNCH(repeat_kernel, dim3(blocks_for(bytes * count, TPB, 65536)), dim3(TPB), 0,
+             (const uint8_t*)src, (uint8_t*)dst, bytes, count);
+}
+
+extern "C" int mia_memset(void* dst, int value, int64_t bytes, void* stream) {
+  MIA_CHECK_ARG(dst && bytes >= 0, "bad args");
+  if (bytes == 0) return MIA_OK;
+  if (hipMemsetAsync(dst, value, (size_t)bytes, (hipStream_t)stream) != hipSuccess)
+    return mia::set_error("hipMemsetAsync failed");
+  return MIA_OK;
+}

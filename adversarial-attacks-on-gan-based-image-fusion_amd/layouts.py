@@ -1,0 +1,68 @@
+"""Host-side (once per model) weight re-layout for the MFMA conv kernel.
+
+The kernel computes y[n,p,co] = Σ_{tap,ci} x[n,p+tap,ci]·w[co][tap·Cin+ci] over a 3×3 / pad-1
+window (tap = 3·ty + tx, offsets ty−1, tx−1). These helpers produce its weight matrices:
+
+* ``fwd_matrix``      — [Cout][Kpad] from an OIHW 3×3 kernel (VGG conv, StyledConv).
+* ``dgrad_matrix``    — [Cin][Kpad'] for the input gradient of that conv: flipped taps, swapped
+                        channel roles (a stride-1 pad-1 conv's transpose is again such a conv).
+* ``upconv_phases``   — folds ``conv_transpose2d(stride 2, pad 0)`` followed by rosinality's Blur
+                        (upfirdn2d, k = [1,3,3,1]⊗[1,3,3,1]/64·4, pad (1,1)) into four 3×3 phase
+                        kernels on the low-resolution grid: output pixel (2m+py, 2m'+px) =
+                        Σ_t x[m+ty−1, m'+tx−1]·V[py,px][ty,tx] with
+                        V[p][t] = Σ_j f[j]·W[1 − 2t + p + j] per axis, f = [1,3,3,1]/4.
+                        Demodulation commutes with the (per-channel, linear) blur, so the phase
+                        kernels carry the original weights' demod (ModulatedConv2d upsample branch).
+"""
+import torch
+
+BLUR_F = (0.25, 0.75, 0.75, 0.25)
+
+
+def kpad_for(cin, dtype):
+    bk = 16 if dtype == torch.float32 else 32
+    return (9 * cin + bk - 1) // bk * bk
+
+
+def fwd_matrix(w, dtype, cin_pad=None):
+    """w: (Cout, Cin, 3, 3) → (Cout, Kpad) with K index = tap·Cin' + ci (Cin' = cin_pad or Cin)."""
+    cout, cin = w.shape[:2]
+    cp = cin_pad or cin
+    wp = torch.zeros(cout, cp, 3, 3, dtype=torch.float64)
+    wp[:, :cin] = w.double()
+    m = wp.permute(0, 2, 3, 1).reshape(cout, 9 * cp)  # [co][ty][tx][ci]
+    out = torch.zeros(cout, kpad_for(cp, dtype), dtype=torch.float64)
+    out[:, :9 * cp] = m
+    return out.to(dtype)
+
+
+def dgrad_matrix(w, dtype, cin_pad=None):
+    """Weights of the input-gradient conv: Wd[ci][tap'·Cout + co] = w[co][ci][2−ty][2−tx]."""
+    cout, cin = w.shape[:2]
+    cp = cin_pad or cin
+    wt = torch.zeros(cp, cout, 3, 3, dtype=torch.float64)
+    wt[:cin] = w.double().transpose(0, 1).flip(2, 3)
+    return fwd_matrix(wt, dtype)
+
+
+def upconv_phases(w):
+    """(Cout, Cin, 3, 3) → (4·Cout, Cin, 3, 3) phase kernels, row index = (2·py+px)·Cout + co."""
+    cout, cin = w.shape[:2]
+    w = w.double()
+    v = torch.zeros(2, 2, cout, cin, 3, 3, dtype=torch.float64)
+    for py in range(2):
+        for px in range(2):
+            for ty in range(3):
+                for tx in range(3):
+                    acc = torch.zeros(cout, cin, dtype=torch.float64)
+                    for jy in range(4):
+                        ky = 1 - 2 * ty + py + jy
+                        if not 0 <= ky <= 2:
+                            continue
+                        for jx in range(4):
+                            kx = 1 - 2 * tx + px + jx
+                            if not 0 <= kx <= 2:
+                                continue
+                            acc += BLUR_F[jy] * BLUR_F[jx] * w[:, :, ky, kx]
+                    v[py, px, :, :, ty, tx] = acc
+    return v.reshape(4 * cout, cin, 3, 3)

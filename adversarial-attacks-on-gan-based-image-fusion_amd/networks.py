@@ -1,0 +1,122 @@
+"""Reference-shaped module objects around the device networks.
+
+* ``Decoder``  — ``net.decoder``: ``decoder([w+], input_is_latent=True, randomize_noise=False,
+  return_latents=True) -> (img, latents)`` and ``.size`` (code/attack/attack_main2.py:590,619-621).
+* ``Encoder``  — ``net.encoder(x) -> (N, n_latent, 512)`` (attack_main2.py:597,622).
+* ``PSPNet``   — the pSp bundle: encoder, decoder, latent_avg, opts.start_from_latent_avg
+  (attack_main2.py:137-146; utils/model_utils.py:7-18).
+* ``VGGBase`` / ``vgg16(pth)`` — code/vgg.py:6-81: ``vgg(x) -> (conv1_1, conv1_2, conv3_2, conv4_2)``.
+* ``get_latents(net, x)`` — attack_main2.py:137-146 (adds latent_avg when the option is set).
+
+Forward calls here allocate their outputs and return NCHW fp32 tensors (reference layout); the
+attack itself works on the NHWC device buffers directly.
+"""
+import argparse
+
+import torch
+
+from .encoder import SyntheticEncoder
+from .stylegan2 import SynthesisNet
+from .vgg import CPAD, VGGNet
+from .weights import make_encoder_weights, make_generator_weights, make_vgg_weights
+from .workspace import Workspace
+from . import ops
+
+
+class Decoder:
+    def __init__(self, params, size, dtype=torch.float32, device="cuda"):
+        self.impl = SynthesisNet(params, size, dtype=dtype, device=device)
+        self.size = self.impl.size
+        self.n_latent = self.impl.n_latent
+        self.device = self.impl.device
+        self._ws = Workspace(self.device)
+
+    def __call__(self, styles, input_is_latent=True, randomize_noise=False, return_latents=False,
+                 truncation=1, truncation_latent=None):
+        if not input_is_latent:
+            raise ValueError("only input_is_latent=True is supported (the mapping MLP is not part "
+                             "of the attack path, attack_main2.py:619)")
+        if randomize_noise:
+            raise ValueError("randomize_noise=False only (fixed noise buffers, attack_main2.py:620)")
+        lat = styles[0] if isinstance(styles, (list, tuple)) else styles
+        if lat.dim() == 2:
+            lat = lat.unsqueeze(1).repeat(1, self.n_latent, 1)
+        if truncation != 1:
+            lat = truncation_latent + truncation * (lat - truncation_latent)
+        lat = lat.to(self.device, torch.float32).contiguous()
+        img = self.impl.forward(lat, self._ws).clone()
+        return img, (lat if return_latents else None)
+
+
+class Encoder:
+    def __init__(self, params, size, device="cuda"):
+        self.impl = SyntheticEncoder(params, size, device=device)
+        self._ws = Workspace(torch.device(device))
+
+    def __call__(self, x):
+        x = x.to(self.impl.w.device, torch.float32).contiguous()
+        return self.impl.forward(x, self._ws).clone()
+
+
+class PSPNet:
+    def __init__(self, encoder, decoder, latent_avg, start_from_latent_avg=True):
+        self.encoder = encoder
+        self.decoder = decoder
+        self.latent_avg = latent_avg
+        self.opts = argparse.Namespace(start_from_latent_avg=start_from_latent_avg)
+        self.vgg = None
+        self.default_target = None
+
+    def eval(self):
+        return self
+
+
+class VGGBase:
+    """code/vgg.py VGGBase: forward returns the four taps (NCHW fp32)."""
+
+    def __init__(self, pth, dtype=torch.float32, device="cuda"):
+        self.pth = pth
+        self.impl = VGGNet(pth, dtype=dtype, device=device)
+        self._ws = Workspace(torch.device(device))
+
+    def __call__(self, image):
+        x = image.to(self.impl.device, torch.float32).contiguous()
+        N, _, H, W = x.shape
+        if H != W:
+            raise ValueError("square images only")
+        xin = self._ws.get("in", (N, H, W, CPAD), self.impl.dtype)
+        ops.image_to_nhwc(x, xin, 1, CPAD)
+        a = self.impl.forward(xin, self._ws, "")
+        return tuple(t.permute(0, 3, 1, 2).float().contiguous() for t in VGGNet.taps(a))
+
+    def eval(self):
+        return self
+
+
+def vgg16(pth, dtype=torch.float32, device="cuda"):
+    return VGGBase(pth, dtype=dtype, device=device)
+
+
+def get_latents(net, x, is_cars=False):
+    """attack_main2.py:137-146."""
+    codes = net.encoder(x)
+    if net.opts.start_from_latent_avg:
+        codes = codes + net.latent_avg.to(codes.device).unsqueeze(0)
+    if codes.shape[1] == 18 and is_cars:
+        codes = codes[:, :16, :]
+    return codes
+
+
+def build_net(size=256, seed=0, dtype=torch.float32, device="cuda", vgg_seed=1234,
+              with_vgg=True):
+    """Seeded synthetic pSp bundle (+ VGG) — no checkpoints exist offline."""
+    gp = make_generator_weights(size, seed=seed)
+    ep = make_encoder_weights(size, seed=seed + 1)
+    net = PSPNet(Encoder(ep, size, device=device), Decoder(gp, size, dtype=dtype, device=device),
+                 ep["latent_avg"].to(device), ep["start_from_latent_avg"])
+    net.params = dict(generator=gp, encoder=ep)
+    if with_vgg:
+        vs = make_vgg_weights(vgg_seed)
+        net.vgg = VGGBase(vs, dtype=dtype, device=device)
+        net.params["vgg"] = vs
+    return net

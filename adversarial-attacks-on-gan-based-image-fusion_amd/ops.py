@@ -1,0 +1,367 @@
+"""Typed host wrappers over the C ABI: torch tensors in, device pointers + the current HIP stream
+out. Every wrapper validates shapes/dtypes/contiguity on the host before a kernel is launched, so a
+malformed call raises here instead of faulting on the GPU."""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import ACT_LRELU_S2, ACT_NONE, ACT_RELU, ConvArgs, call  # noqa: F401
+
+DTYPES = {torch.float32: _lib.MIA_F32, torch.float16: _lib.MIA_F16, torch.bfloat16: _lib.MIA_BF16}
+VEC = {torch.float32: 4, torch.float16: 8, torch.bfloat16: 8}
+
+
+def dt(t_or_dtype):
+    d = t_or_dtype if isinstance(t_or_dtype, torch.dtype) else t_or_dtype.dtype
+    if d not in DTYPES:
+        raise TypeError(f"unsupported dtype {d}")
+    return DTYPES[d]
+
+
+def ptr(t):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("device tensor required (the attack path runs on the GPU only)")
+    if not t.is_contiguous():
+        raise ValueError("contiguous tensor required")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _need(t, shape, dtype=None, name="tensor"):
+    if t is None:
+        raise ValueError(f"{name} is required")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: shape {tuple(t.shape)} != {tuple(shape)}")
+    if dtype is not None and t.dtype != dtype:
+        raise ValueError(f"{name}: dtype {t.dtype} != {dtype}")
+
+
+def _numel_ok(t, n, dtype=None, name="tensor"):
+    if t is None:
+        return
+    if t.numel() != n:
+        raise ValueError(f"{name}: numel {t.numel()} != {n}")
+    if dtype is not None and t.dtype != dtype:
+        raise ValueError(f"{name}: dtype {t.dtype} != {dtype}")
+
+
+def conv_kpad(cin, dtype):
+    bk = 16 if dtype == torch.float32 else 32
+    return (9 * cin + bk - 1) // bk * bk
+
+
+# Live per-launch timing of the conv kernel (bench.py roofline): when PROFILE is a list, every
+# conv3x3 call is bracketed by HIP events on the launch stream and (start, end, algorithmic
+# FLOPs) is appended. None (default) = no events.
+PROFILE = None
+
+
+def conv3x3(x, w, y, *, cout, act_in=ACT_NONE, in_scale=None, out_scale=None, bias=None,
+            noise=None, noise_w=0.0, act_out=ACT_NONE, shuffle_out=False, aux_x=None,
+            act_aux=ACT_NONE, sdot=None, tap_a=None, tap_t=None, tap_coef=0.0, mask_a=None,
+            accumulate=False, y_cstride=0, flops=None):
+    """Generic MFMA implicit-GEMM conv (mia_conv3x3). x: (N,H,W,Cin); w: (Cout,Kpad).
+    ``flops``: algorithmic FLOPs of this launch for profiling (default 2·N·H·W·9·Cin·Cout)."""
+    N, H, W, Cin = x.shape
+    T = x.dtype
+    kpad = conv_kpad(Cin, T)
+    _need(w, (cout, kpad), T, "w")
+    if Cin % VEC[T]:
+        raise ValueError("Cin must be a multiple of the 16-byte vector")
+    cm = cout // 4 if shuffle_out else cout
+    ys = y_cstride or cm
+    if y is not None:
+        if shuffle_out:
+            _need(y, (N, 2 * H, 2 * W, ys), T, "y")
+        else:
+            _need(y, (N, H, W, ys), T, "y")
+    f32 = torch.float32
+    _numel_ok(in_scale, N * Cin, f32, "in_scale")
+    _numel_ok(out_scale, N * cm, f32, "out_scale")
+    _numel_ok(bias, cm, f32, "bias")
+    Ho, Wo = (2 * H, 2 * W) if shuffle_out else (H, W)
+    _numel_ok(noise, Ho * Wo, f32, "noise")
+    for name, a in (("aux_x", aux_x), ("tap_a", tap_a), ("tap_t", tap_t), ("mask_a", mask_a)):
+        if a is not None:
+            _need(a, (N, H, W, cout), T, name)
+    _numel_ok(sdot, N * cout, f32, "sdot")
+    a = ConvArgs()
+    a.x, a.w, a.y = ptr(x), ptr(w), ptr(y)
+    a.N, a.H, a.W, a.Cin, a.Cout, a.Kpad = N, H, W, Cin, cout, kpad
+    a.y_cstride = ys
+    a.act_in = act_in
+    a.in_scale, a.out_scale, a.bias, a.noise = ptr(in_scale), ptr(out_scale), ptr(bias), ptr(noise)
+    a.noise_w = float(noise_w)
+    a.act_out = act_out
+    a.shuffle_out = int(bool(shuffle_out))
+    a.aux_x, a.act_aux, a.sdot = ptr(aux_x), act_aux, ptr(sdot)
+    a.tap_a, a.tap_t, a.tap_coef, a.mask_a = ptr(tap_a), ptr(tap_t), float(tap_coef), ptr(mask_a)
+    a.accumulate = int(bool(accumulate))
+    prof = PROFILE
+    if prof is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    call("mia_conv3x3", ctypes.byref(a), dt(T), stream())
+    if prof is not None:
+        e1.record()
+        prof.append((e0, e1, flops if flops is not None else 2 * N * H * W * 9 * Cin * cout))
+    return y
+
+
+def bias_act_fwd(x, noise, noise_w, bias, y):
+    N, H, W, C = x.shape
+    _need(y, x.shape, x.dtype, "y")
+    _numel_ok(noise, H * W, torch.float32, "noise")
+    _numel_ok(bias, C, torch.float32, "bias")
+    call("mia_bias_act_fwd", ptr(x), ptr(noise), float(noise_w), ptr(bias), ptr(y), N, H, W, C,
+         dt(x), stream())
+    return y
+
+
+def bias_act_bwd(g_a, pre, noise, noise_w, bias, demod, gy, q, unshuffle=False):
+    N, H, W, C = pre.shape
+    _need(g_a, pre.shape, pre.dtype, "g_a")
+    _numel_ok(noise, H * W, torch.float32, "noise")
+    _numel_ok(bias, C, torch.float32, "bias")
+    _numel_ok(demod, N * C, torch.float32, "demod")
+    _numel_ok(q, N * C, torch.float32, "q")
+    if unshuffle:
+        _need(gy, (N, H // 2, W // 2, 4 * C), pre.dtype, "gy")
+    else:
+        _need(gy, pre.shape, pre.dtype, "gy")
+    call("mia_bias_act_bwd", ptr(g_a), ptr(pre), ptr(noise), float(noise_w), ptr(bias), ptr(demod),
+         ptr(gy), ptr(q), N, H, W, C, int(bool(unshuffle)), dt(pre), stream())
+    return gy
+
+
+def _updn_out(H, up, down, p0, p1, kt):
+    return (H * up + p0 + p1 - kt) // down + 1
+
+
+def upfirdn2d_fwd(x, y, k1d, up=1, down=1, pad=(0, 0)):
+    """x: (..., H, W) fp32; k1d: host list of taps."""
+    H, W = x.shape[-2:]
+    planes = x.numel() // (H * W)
+    kt = len(k1d)
+    Ho, Wo = _updn_out(H, up, down, pad[0], pad[1], kt), _updn_out(W, up, down, pad[0], pad[1], kt)
+    _need(y, tuple(x.shape[:-2]) + (Ho, Wo), torch.float32, "y")
+    k = (ctypes.c_float * kt)(*k1d)
+    call("mia_upfirdn2d_fwd", ptr(x), ptr(y), planes, H, W, k, kt, up, down, pad[0], pad[1],
+         stream())
+    return y
+
+
+def upfirdn2d_bwd(gy, gx, k1d, up=1, down=1, pad=(0, 0)):
+    H, W = gx.shape[-2:]
+    planes = gx.numel() // (H * W)
+    kt = len(k1d)
+    Ho, Wo = _updn_out(H, up, down, pad[0], pad[1], kt), _updn_out(W, up, down, pad[0], pad[1], kt)
+    _need(gy, tuple(gx.shape[:-2]) + (Ho, Wo), torch.float32, "gy")
+    k = (ctypes.c_float * kt)(*k1d)
+    call("mia_upfirdn2d_bwd", ptr(gy), ptr(gx), planes, H, W, k, kt, up, down, pad[0], pad[1],
+         stream())
+    return gx
+
+
+def torgb_fwd(pre, style, wr, bias, skip, rgb):
+    N, H, W, Cin = pre.shape
+    _numel_ok(style, N * Cin, torch.float32, "style")
+    _need(wr, (3, Cin), torch.float32, "wr")
+    _numel_ok(bias, 3, torch.float32, "bias")
+    if skip is not None:
+        _need(skip, (N, 3, H // 2, W // 2), torch.float32, "skip")
+    _need(rgb, (N, 3, H, W), torch.float32, "rgb")
+    call("mia_torgb_fwd", ptr(pre), ptr(style), ptr(wr), ptr(bias), ptr(skip), ptr(rgb), N, H, W,
+         Cin, dt(pre), stream())
+    return rgb
+
+
+def torgb_bwd(g_rgb, pre, style, wr, g_a, gs, accumulate):
+    N, H, W, Cin = pre.shape
+    _need(g_rgb, (N, 3, H, W), torch.float32, "g_rgb")
+    _numel_ok(style, N * Cin, torch.float32, "style")
+    _need(wr, (3, Cin), torch.float32, "wr")
+    _need(g_a, pre.shape, pre.dtype, "g_a")
+    _numel_ok(gs, N * Cin, torch.float32, "gs")
+    call("mia_torgb_bwd", ptr(g_rgb), ptr(pre), ptr(style), ptr(wr), ptr(g_a), ptr(gs), N, H, W,
+         Cin, int(bool(accumulate)), dt(pre), stream())
+
+
+def pool_out(H, ceil_mode):
+    return (H + 1) // 2 if ceil_mode else H // 2
+
+
+def maxpool2_fwd(x, y, ceil_mode=False):
+    N, H, W, C = x.shape
+    _need(y, (N, pool_out(H, ceil_mode), pool_out(W, ceil_mode), C), x.dtype, "y")
+    call("mia_maxpool2_fwd", ptr(x), ptr(y), N, H, W, C, int(bool(ceil_mode)), dt(x), stream())
+    return y
+
+
+def maxpool2_bwd(x, g_out, g_in, ceil_mode=False, tap_t=None, tap_coef=0.0, mask=False):
+    N, H, W, C = x.shape
+    _need(g_out, (N, pool_out(H, ceil_mode), pool_out(W, ceil_mode), C), x.dtype, "g_out")
+    _need(g_in, x.shape, x.dtype, "g_in")
+    if tap_t is not None:
+        _need(tap_t, x.shape, x.dtype, "tap_t")
+    call("mia_maxpool2_bwd", ptr(x), ptr(g_out), ptr(g_in), N, H, W, C, int(bool(ceil_mode)),
+         ptr(tap_t), float(tap_coef), int(bool(mask)), dt(x), stream())
+    return g_in
+
+
+def avgpool_fwd(x, y, k):
+    H, W = x.shape[-2:]
+    planes = x.numel() // (H * W)
+    _need(y, tuple(x.shape[:-2]) + (H // k, W // k), torch.float32, "y")
+    call("mia_avgpool_fwd", ptr(x), ptr(y), planes, H, W, k, stream())
+    return y
+
+
+def avgpool_bwd(gy, gx, k, accumulate=False):
+    H, W = gx.shape[-2:]
+    planes = gx.numel() // (H * W)
+    _need(gy, tuple(gx.shape[:-2]) + (H // k, W // k), torch.float32, "gy")
+    call("mia_avgpool_bwd", ptr(gy), ptr(gx), planes, H, W, k, int(bool(accumulate)), stream())
+    return gx
+
+
+def image_to_nhwc(x, y, pf, cpad):
+    N, C, S, _ = x.shape
+    if C != 3 or x.dtype != torch.float32:
+        raise ValueError("x must be (N,3,S,S) fp32")
+    _need(y, (N, S // pf, S // pf, cpad), None, "y")
+    call("mia_image_to_nhwc", ptr(x), ptr(y), N, S, pf, cpad, dt(y), stream())
+    return y
+
+
+def mse_sum(a, b, loss):
+    n = a.shape[0]
+    _need(b, a.shape, a.dtype, "b")
+    _numel_ok(loss, n, torch.float32, "loss")
+    call("mia_mse_sum", ptr(a), ptr(b), ptr(loss), n, a.numel() // n, dt(a), stream())
+    return loss
+
+
+def mse_grad_f32(a, b, g, coef, accumulate=False):
+    _need(b, a.shape, torch.float32, "b")
+    _need(g, a.shape, torch.float32, "g")
+    call("mia_mse_grad_f32", ptr(a), ptr(b), ptr(g), a.numel(), float(coef),
+         int(bool(accumulate)), stream())
+    return g
+
+
+def tap_grad(a, t, g, coef, mask=True):
+    _need(t, a.shape, a.dtype, "t")
+    _need(g, a.shape, a.dtype, "g")
+    call("mia_tap_grad", ptr(a), ptr(t), ptr(g), a.numel(), float(coef), int(bool(mask)), dt(a),
+         stream())
+    return g
+
+
+def image_grad(rec, t, g_vgg, g_img, pf, coef):
+    N, _, S, _ = rec.shape
+    _need(t, rec.shape, torch.float32, "t")
+    _need(g_img, rec.shape, torch.float32, "g_img")
+    cpad = 8
+    if g_vgg is not None:
+        _need(g_vgg, (N, S // pf, S // pf, g_vgg.shape[-1]), None, "g_vgg")
+        cpad = g_vgg.shape[-1]
+    gdt = dt(g_vgg) if g_vgg is not None else _lib.MIA_F32
+    call("mia_image_grad", ptr(rec), ptr(t), ptr(g_vgg), ptr(g_img), N, S, pf, cpad, float(coef),
+         gdt, stream())
+    return g_img
+
+
+def pgd_update(x, x0, g_vgg, g_enc, pf, enc_res, coef_img, a, e, lo=-1.0, hi=1.0):
+    N, _, S, _ = x.shape
+    _need(x0, x.shape, torch.float32, "x0")
+    cpad = 8
+    if g_vgg is not None:
+        _need(g_vgg, (N, S // pf, S // pf, g_vgg.shape[-1]), None, "g_vgg")
+        cpad = g_vgg.shape[-1]
+    if g_enc is not None:
+        _numel_ok(g_enc, N * 3 * enc_res * enc_res, torch.float32, "g_enc")
+    gdt = dt(g_vgg) if g_vgg is not None else _lib.MIA_F32
+    call("mia_pgd_update", ptr(x), ptr(x0), ptr(g_vgg), ptr(g_enc), N, S, pf, cpad, enc_res,
+         float(coef_img), float(a), float(e), float(lo), float(hi), gdt, stream())
+    return x
+
+
+def random_start(x, x0, u, e, lo=-1.0, hi=1.0):
+    _need(x0, x.shape, torch.float32, "x0")
+    _need(u, x.shape, torch.float32, "u")
+    call("mia_random_start", ptr(x), ptr(x0), ptr(u), x.numel(), float(e), float(lo), float(hi),
+         stream())
+    return x
+
+
+def sign_project(x, x0, g, a, e, lo=-1.0, hi=1.0):
+    _need(x0, x.shape, torch.float32, "x0")
+    _need(g, x.shape, torch.float32, "g")
+    call("mia_sign_project", ptr(x), ptr(x0), ptr(g), x.numel(), float(a), float(e), float(lo),
+         float(hi), stream())
+    return x
+
+
+def adam_step(p, g, m, v, lr, beta1, beta2, eps, t):
+    for name, z in (("g", g), ("m", m), ("v", v)):
+        _need(z, p.shape, torch.float32, name)
+    call("mia_adam_step", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), float(lr), float(beta1),
+         float(beta2), float(eps), int(t), stream())
+    return p
+
+
+def gemm(M, N, K, alpha, A, sam, sak, B, sbk, sbn, beta, C, scm, scn, bias=None):
+    """C[m,n] = alpha Σ_k A[m*sam+k*sak] B[k*sbk+n*sbn] + beta C[m*scm+n*scn] + bias[n] (fp32).
+    Offsets into A/B/C are given by passing views (data_ptr of a strided view is honoured)."""
+    for name, t, span in (("A", A, (M - 1) * sam + (K - 1) * sak),
+                          ("B", B, (K - 1) * sbk + (N - 1) * sbn),
+                          ("C", C, (M - 1) * scm + (N - 1) * scn)):
+        if t.dtype != torch.float32 or not t.is_cuda:
+            raise ValueError(f"gemm {name}: cuda fp32 required")
+        avail = t.untyped_storage().nbytes() // 4 - t.storage_offset()
+        if span >= avail:
+            raise ValueError(f"gemm {name}: strided span {span} exceeds storage {avail}")
+    _numel_ok(bias, N, torch.float32, "bias")
+    c = ctypes.c_void_p
+    call("mia_gemm_f32", M, N, K, float(alpha), c(A.data_ptr()), sam, sak, c(B.data_ptr()), sbk,
+         sbn, float(beta), c(C.data_ptr()), scm, scn, ptr(bias), stream())
+    return C
+
+
+def style_demod(s, wsq, demod, scale2=1.0):
+    N, Cin = s.shape
+    Cout = wsq.shape[0]
+    _need(wsq, (Cout, Cin), torch.float32, "wsq")
+    _need(demod, (N, Cout), torch.float32, "demod")
+    call("mia_style_demod", ptr(s), ptr(wsq), ptr(demod), N, Cin, Cout, float(scale2), stream())
+    return demod
+
+
+def demod_bwd(q, demod, wsq, s, gs, scale2=1.0):
+    N, Cin = s.shape
+    Cout = wsq.shape[0]
+    _need(q, (N, Cout), torch.float32, "q")
+    _need(demod, (N, Cout), torch.float32, "demod")
+    _need(gs, (N, Cin), torch.float32, "gs")
+    call("mia_demod_bwd", ptr(q), ptr(demod), ptr(wsq), ptr(s), ptr(gs), N, Cin, Cout,
+         float(scale2), stream())
+    return gs
+
+
+def repeat(src, dst, count):
+    if dst.numel() != src.numel() * count or dst.dtype != src.dtype:
+        raise ValueError("repeat: size mismatch")
+    call("mia_repeat", ptr(src), ptr(dst), src.numel() * src.element_size(), count, stream())
+    return dst
+
+
+def zero_(t):
+    call("mia_memset", ptr(t), 0, t.numel() * t.element_size(), stream())
+    return t

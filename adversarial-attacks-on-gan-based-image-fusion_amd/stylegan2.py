@@ -1,0 +1,191 @@
+"""StyleGAN2 synthesis network on libmiattack kernels: forward and input/style backward.
+
+Behind the reference's ``net.decoder`` slot: ``decoder([w+], input_is_latent=True,
+randomize_noise=False, return_latents=True) -> (img, latents)`` (code/attack/attack_main2.py:619-621,
+code/attack/interpolation.py:780-782) and ``decoder.size`` (attack_main2.py:590). The network is the
+rosinality generator (un-vendored dependency, see oracle/stylegan2_ref.py) with the mapping MLP
+omitted (the attack always passes W+ latents).
+
+Layout in HBM: every feature map is NHWC in the compute dtype. Each StyledConv stores only its
+pre-activation ``pre = demod·conv(x̃) + noise_w·noise + bias`` (one tensor per layer); consumers
+apply lrelu·√2 on load (next conv's A-operand prologue, ToRGB, backward masks). The image/skip path
+(3 channels) is fp32 NCHW. Styles, demod coefficients and their gradients are fp32 [N][C].
+
+Backward computes ∂L/∂w+ only (no weight gradients: the pixel gradient does not need them,
+SURVEY.md §2.1 note). Per StyledConv, with g_pre = ∂L/∂pre:
+    gy = g_pre·demod;  gx̃ = dgrad(gy);  ∂x = gx̃·s;  ∂s = Σ_p gx̃·x − s·Σ_co (Σ_p g_pre·o)·demod²·Wsq
+where o = pre − noise_w·noise − bias = demod·conv(x̃) and Wsq[co][ci] = Σ_k (scale·W)².
+"""
+import math
+
+import torch
+
+from . import layouts, ops
+from .ops import ACT_LRELU_S2, ACT_NONE
+from .weights import STYLE_DIM, generator_layout, n_latent_for
+
+UP_K = list(layouts.BLUR_F)  # separable ToRGB skip up-sampler (Upsample(blur_kernel), factor 2)
+
+
+class SynthesisNet:
+    def __init__(self, params, size, dtype=torch.float32, device="cuda", channel_multiplier=2):
+        self.size = int(size)
+        self.n_latent = n_latent_for(self.size)
+        self.dtype = dtype
+        self.device = torch.device(device)
+        convs, torgbs = generator_layout(self.size, channel_multiplier)
+        dev, f32 = self.device, torch.float32
+
+        def style_params(prefix, cin):
+            a = params[prefix + ".modulation.weight"].double() / math.sqrt(STYLE_DIM)
+            return (a.to(f32).contiguous().to(dev),
+                    params[prefix + ".modulation.bias"].to(f32).contiguous().to(dev))
+
+        self.convs = []
+        for c in convs:
+            pre = c["name"]
+            w = params[pre + ".conv.weight"][0].double()  # (cout, cin, 3, 3)
+            cin, cout = c["cin"], c["cout"]
+            scale = 1.0 / math.sqrt(cin * 9)
+            ws = w * scale
+            L = dict(c)
+            if c["up"]:
+                ph = layouts.upconv_phases(ws)
+                L["wf"] = layouts.fwd_matrix(ph, dtype).contiguous().to(dev)
+                L["wd"] = layouts.dgrad_matrix(ph, dtype).contiguous().to(dev)
+            else:
+                L["wf"] = layouts.fwd_matrix(ws, dtype).contiguous().to(dev)
+                L["wd"] = layouts.dgrad_matrix(ws, dtype).contiguous().to(dev)
+            L["wsq"] = (ws ** 2).sum(dim=(2, 3)).to(f32).contiguous().to(dev)  # [cout][cin]
+            L["A"], L["Ab"] = style_params(pre + ".conv", cin)
+            L["noise"] = params[f"noises.noise_{c['noise']}"].reshape(-1).to(f32).contiguous().to(dev)
+            L["noise_w"] = float(params[pre + ".noise.weight"].reshape(-1)[0])
+            L["bias"] = params[pre + ".activate.bias"].to(f32).contiguous().to(dev)
+            self.convs.append(L)
+        self.torgbs = []
+        for t in torgbs:
+            pre = t["name"]
+            w = params[pre + ".conv.weight"][0, :, :, 0, 0].double()  # (3, cin)
+            L = dict(t)
+            L["wr"] = (w / math.sqrt(t["cin"])).to(f32).contiguous().to(dev)
+            L["A"], L["Ab"] = style_params(pre + ".conv", t["cin"])
+            L["bias"] = params[pre + ".bias"].reshape(3).to(f32).contiguous().to(dev)
+            self.torgbs.append(L)
+        const = params["input.input"][0].permute(1, 2, 0).contiguous()  # (4,4,512) NHWC
+        self.const = const.to(dtype).to(dev)
+        self.flops_fwd_per_image = sum(self._alg_flops(L, 1) for L in self.convs)
+
+    @staticmethod
+    def _alg_flops(L, N):
+        """Algorithmic FLOPs of one StyledConv GEMM: 3×3 conv at the
+        output resolution, or conv_transpose2d at the input resolution for up-convs (the blur
+        folded into the 4-phase kernels is extra work the count does not credit)."""
+        r = L["res"] // 2 if L["up"] else L["res"]
+        return 2 * N * r * r * 9 * L["cin"] * L["cout"]
+
+    # --------------------------------------------------------------------------------------
+    def styles(self, lat, ws):
+        """s = w+[:, idx]·(A/√512)ᵀ + b for every modulated conv; demod for the StyledConvs."""
+        N = lat.shape[0]
+        nl = self.n_latent
+        for i, L in enumerate(self.convs + self.torgbs):
+            cin = L["cin"]
+            s = ws.get(f"g.s{i}", (N, cin), torch.float32)
+            wrow = lat[:, L["latent"], :]
+            ops.gemm(N, cin, STYLE_DIM, 1.0, wrow, nl * STYLE_DIM, 1, L["A"], 1, STYLE_DIM, 0.0, s,
+                     cin, 1, bias=L["Ab"])
+            L["_s"] = s
+            if "wsq" in L:
+                d = ws.get(f"g.d{i}", (N, L["cout"]), torch.float32)
+                ops.style_demod(s, L["wsq"], d)
+                L["_d"] = d
+
+    def forward(self, lat, ws):
+        """lat: (N, n_latent, 512) fp32 → image (N,3,S,S) fp32 (the rosinality ``skip``)."""
+        N = lat.shape[0]
+        if tuple(lat.shape[1:]) != (self.n_latent, STYLE_DIM) or lat.dtype != torch.float32:
+            raise ValueError(f"latent must be (N,{self.n_latent},512) fp32")
+        T = self.dtype
+        self.styles(lat, ws)
+        x0 = ws.get("g.const", (N, 4, 4, self.const.shape[-1]), T)
+        ops.repeat(self.const, x0, N)
+        x, act = x0, ACT_NONE
+        rgb = None
+        ti = 0
+        for i, L in enumerate(self.convs):
+            r, cout = L["res"], L["cout"]
+            pre = ws.get(f"g.pre{i}", (N, r, r, cout), T)
+            ops.conv3x3(x, L["wf"], pre, cout=4 * cout if L["up"] else cout, act_in=act,
+                        in_scale=L["_s"], out_scale=L["_d"], noise=L["noise"],
+                        noise_w=L["noise_w"], bias=L["bias"], shuffle_out=L["up"],
+                        flops=self._alg_flops(L, N))
+            L["_x"], L["_xact"], L["_pre"] = x, act, pre
+            x, act = pre, ACT_LRELU_S2
+            if not L["up"]:  # every non-up conv closes a resolution → ToRGB
+                t = self.torgbs[ti]
+                out = ws.get(f"g.rgb{ti}", (N, 3, r, r), torch.float32)
+                ops.torgb_fwd(pre, t["_s"], t["wr"], t["bias"], rgb, out)
+                t["_pre"], t["_skip"] = pre, rgb
+                rgb = out
+                ti += 1
+        return rgb
+
+    # --------------------------------------------------------------------------------------
+    def backward(self, g_img, g_lat, ws):
+        """g_img = ∂L/∂image (N,3,S,S) fp32; accumulates ∂L/∂w+ into g_lat (N,n_latent,512)."""
+        N = g_img.shape[0]
+        T = self.dtype
+        nl = self.n_latent
+        g_rgb = g_img
+        ti = len(self.torgbs) - 1
+        g_a_next = None  # ∂L/∂act of the current conv's output, written by the conv above
+        for i in range(len(self.convs) - 1, -1, -1):
+            L = self.convs[i]
+            r, cout, cin = L["res"], L["cout"], L["cin"]
+            pre = L["_pre"]
+            if not L["up"]:
+                # ToRGB consumes this conv's activation: add its gradient, route the skip gradient
+                t = self.torgbs[ti]
+                gs_t = ws.get(f"g.gs_rgb{ti}", (N, t["cin"]), torch.float32)
+                ops.zero_(gs_t)
+                if g_a_next is None:
+                    g_a_next = ws.get(f"g.ga{i}", (N, r, r, cout), T)
+                    acc = False
+                else:
+                    acc = True
+                ops.torgb_bwd(g_rgb, pre, t["_s"], t["wr"], g_a_next, gs_t, accumulate=acc)
+                t["_gs"] = gs_t
+                if t["_skip"] is not None:
+                    g_skip = ws.get(f"g.gskip{ti}", (N, 3, r // 2, r // 2), torch.float32)
+                    ops.upfirdn2d_bwd(g_rgb, g_skip, UP_K, up=2, pad=(2, 1))
+                    g_rgb = g_skip
+                ti -= 1
+            # StyledConv backward front: g_pre, q, gy
+            q = ws.get(f"g.q{i}", (N, cout), torch.float32)
+            ops.zero_(q)
+            if L["up"]:
+                gy = ws.get(f"g.gy{i}", (N, r // 2, r // 2, 4 * cout), T)
+            else:
+                gy = ws.get(f"g.gy{i}", (N, r, r, cout), T)
+            ops.bias_act_bwd(g_a_next, pre, L["noise"], L["noise_w"], L["bias"], L["_d"], gy, q,
+                             unshuffle=L["up"])
+            # dgrad + style sdot
+            gs = ws.get(f"g.gs{i}", (N, cin), torch.float32)
+            ops.zero_(gs)
+            rin = r // 2 if L["up"] else r
+            if i > 0:
+                gx = ws.get(f"g.ga{i - 1}", (N, rin, rin, cin), T)
+            else:
+                gx = None
+            ops.conv3x3(gy, L["wd"], gx, cout=cin, out_scale=L["_s"], aux_x=L["_x"],
+                        act_aux=L["_xact"], sdot=gs, flops=self._alg_flops(L, N))
+            ops.demod_bwd(q, L["_d"], L["wsq"], L["_s"], gs)
+            L["_gs"] = gs
+            g_a_next = gx
+        # style affine backward: ∂w+[:, idx] += ∂s · (A/√512)
+        for L in self.convs + self.torgbs:
+            cin = L["cin"]
+            gl = g_lat[:, L["latent"], :]
+            ops.gemm(N, STYLE_DIM, cin, 1.0, L["_gs"], cin, 1, L["A"], STYLE_DIM, 1, 1.0, gl,
+                     nl * STYLE_DIM, 1)
+        return g_lat

@@ -1,0 +1,147 @@
+"""Seeded synthetic weights for the three networks on the attack path.
+
+There are no checkpoints offline, so every network is built from a seed on the
+host (CPU, ``torch.Generator``) and copied to the device. The same dicts feed the product path and
+the CPU oracle, so parity tests compare like with like.
+
+Names follow the state-dict keys of the modules the reference calls:
+
+* StyleGAN2 generator (rosinality ``model.py`` API, used as ``net.decoder`` at
+  ``code/attack/attack_main2.py:619-621`` and as ``SFGenerator_hook`` at
+  ``code/style_fusion_simple.py:51``): ``input.input``, ``conv1.*``, ``to_rgb1.*``, ``convs.{i}.*``,
+  ``to_rgbs.{i}.*``, ``noises.noise_{i}``. The mapping MLP is omitted: the attack always calls the
+  decoder with ``input_is_latent=True`` (``attack_main2.py:619``).
+* VGG16 trunk (``code/vgg.py:12-39``): positional list of 13 convs, loaded like
+  ``VGGBase.load_pretrained_layers`` (``code/vgg.py:66-76``).
+* Encoder: a deterministic linear stand-in for e4e behind the ``net.encoder`` slot
+  (SURVEY.md §2 row 8, §7 step 1).
+"""
+import math
+
+import torch
+
+STYLE_DIM = 512
+
+
+def generator_channels(channel_multiplier=2):
+    """rosinality Generator.channels for channel_multiplier."""
+    cm = channel_multiplier
+    return {4: 512, 8: 512, 16: 512, 32: 512, 64: 256 * cm, 128: 128 * cm, 256: 64 * cm,
+            512: 32 * cm, 1024: 16 * cm}
+
+
+def n_latent_for(size):
+    """n_latent = 2*log2(size) - 2 (14/16/18 for 256/512/1024: style_fusion_simple.py:31,35,39)."""
+    log_size = int(math.log2(size))
+    assert 2 ** log_size == size and size >= 8
+    return log_size * 2 - 2
+
+
+def generator_layout(size, channel_multiplier=2):
+    """Per-layer description of the synthesis network.
+
+    Returns (convs, torgbs): lists of dicts. Each conv: name, cin, cout, res (output resolution),
+    up (bool), latent (index into w+), noise (index of noises.noise_i). Each torgb: name, cin,
+    res, latent, has_skip. Order and latent/noise indexing follow rosinality Generator.forward
+    (latent[:,0] → conv1, latent[:,1] → to_rgb1, then (i, i+1, i+2) per resolution).
+    """
+    ch = generator_channels(channel_multiplier)
+    log_size = int(math.log2(size))
+    convs = [dict(name="conv1", cin=ch[4], cout=ch[4], res=4, up=False, latent=0, noise=0)]
+    torgbs = [dict(name="to_rgb1", cin=ch[4], res=4, latent=1, has_skip=False)]
+    in_ch = ch[4]
+    li = 1
+    ci = 0
+    for i in range(3, log_size + 1):
+        r = 2 ** i
+        out_ch = ch[r]
+        convs.append(dict(name=f"convs.{ci}", cin=in_ch, cout=out_ch, res=r, up=True, latent=li,
+                          noise=2 * (i - 3) + 1))
+        convs.append(dict(name=f"convs.{ci + 1}", cin=out_ch, cout=out_ch, res=r, up=False,
+                          latent=li + 1, noise=2 * (i - 3) + 2))
+        torgbs.append(dict(name=f"to_rgbs.{(ci) // 2}", cin=out_ch, res=r, latent=li + 2,
+                           has_skip=True))
+        ci += 2
+        li += 2
+        in_ch = out_ch
+    return convs, torgbs
+
+
+def make_generator_weights(size, seed=0, channel_multiplier=2, noise_weight=0.1,
+                           bias_std=0.1):
+    """Seeded rosinality-layout generator weights (fp32, CPU).
+
+    Initialisation follows rosinality (weights ~ N(0,1), runtime equalised-lr scaling; modulation
+    bias = 1). Conv/ToRGB biases and noise strengths are made non-zero (bias_std, noise_weight) so
+    every term of the synthesis contributes.
+    """
+    g = torch.Generator().manual_seed(int(seed))
+    ch = generator_channels(channel_multiplier)
+    convs, torgbs = generator_layout(size, channel_multiplier)
+    p = {}
+    p["input.input"] = torch.randn(1, ch[4], 4, 4, generator=g)
+
+    def modconv(prefix, cin, cout, k):
+        p[prefix + ".weight"] = torch.randn(1, cout, cin, k, k, generator=g)
+        p[prefix + ".modulation.weight"] = torch.randn(cin, STYLE_DIM, generator=g)
+        p[prefix + ".modulation.bias"] = torch.ones(cin) + 0.1 * torch.randn(cin, generator=g)
+
+    for c in convs:
+        modconv(c["name"] + ".conv", c["cin"], c["cout"], 3)
+        p[c["name"] + ".noise.weight"] = torch.full((1,), float(noise_weight))
+        p[c["name"] + ".activate.bias"] = bias_std * torch.randn(c["cout"], generator=g)
+    for t in torgbs:
+        modconv(t["name"] + ".conv", t["cin"], 3, 1)
+        p[t["name"] + ".bias"] = bias_std * torch.randn(1, 3, 1, 1, generator=g)
+    log_size = int(math.log2(size))
+    for i in range((log_size - 2) * 2 + 1):
+        r = 2 ** ((i + 5) // 2)
+        p[f"noises.noise_{i}"] = torch.randn(1, 1, r, r, generator=g)
+    return p
+
+
+# VGG16 feature convs in order (code/vgg.py:12-33); the first 9 are run by VGGBase.forward.
+VGG_CONVS = [("conv1_1", 3, 64), ("conv1_2", 64, 64), ("conv2_1", 64, 128), ("conv2_2", 128, 128),
+             ("conv3_1", 128, 256), ("conv3_2", 256, 256), ("conv3_3", 256, 256),
+             ("conv4_1", 256, 512), ("conv4_2", 512, 512), ("conv4_3", 512, 512),
+             ("conv5_1", 512, 512), ("conv5_2", 512, 512), ("conv5_3", 512, 512)]
+VGG_USED = 9
+
+
+def make_vgg_weights(seed=0, n_convs=13):
+    """Seeded He-normal VGG16 conv weights, positional order (as a pretrained VGG16 state dict).
+
+    Keys are ``features.{idx}.weight/bias`` with torchvision VGG16 indices; ``VGGBase``-style
+    loading is positional (code/vgg.py:70-74), so only the order matters.
+    """
+    g = torch.Generator().manual_seed(int(seed))
+    sd = {}
+    idx = 0
+    feat_idx = [0, 2, 5, 7, 10, 12, 14, 17, 19, 21, 24, 26, 28]
+    for (name, cin, cout), fi in zip(VGG_CONVS[:n_convs], feat_idx):
+        std = math.sqrt(2.0 / (cin * 9))
+        sd[f"features.{fi}.weight"] = torch.randn(cout, cin, 3, 3, generator=g) * std
+        sd[f"features.{fi}.bias"] = 0.05 * torch.randn(cout, generator=g)
+        idx += 1
+    return sd
+
+
+ENC_POOL_RES = 16  # the synthetic encoder sees a 16x16 average-pooled image (3*16*16 = 768)
+
+
+def make_encoder_weights(size, seed=0, start_from_latent_avg=True):
+    """Synthetic linear encoder weights (stand-in for e4e).
+
+    E(x) = W_E · vec(avgpool(x, 256/16)) / sqrt(768) + b_E, reshaped to (N, n_latent, 512).
+    ``latent_avg`` is exposed for ``get_latents`` (attack_main2.py:137-146) but, like the
+    reference's optimize_vgg (interpolation.py:780), the attack objective does not add it.
+    """
+    g = torch.Generator().manual_seed(int(seed))
+    nl = n_latent_for(size)
+    d_in = 3 * ENC_POOL_RES * ENC_POOL_RES
+    return {
+        "enc.weight": torch.randn(nl * STYLE_DIM, d_in, generator=g),
+        "enc.bias": 0.1 * torch.randn(nl * STYLE_DIM, generator=g),
+        "latent_avg": 0.1 * torch.randn(nl, STYLE_DIM, generator=g),
+        "start_from_latent_avg": bool(start_from_latent_avg),
+    }

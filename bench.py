@@ -1,0 +1,175 @@
+"""Benchmark: attacked images/sec, PGD-20 L∞ ε=8/255 at 256², 1/2/4/8 MI355X (BASELINE.json).
+
+One "step" = one complete PGD-20 attack (target precompute + 20 iterations + the final RCCL
+all-gather when N>1) over this rank's batch of 128 synthetic 256² image pairs (BASELINE config #4:
+batch 1024 over 8 GPUs = 128 per GPU; weak scaling). Inputs are resident in HBM before the timed
+region. Rank 0 prints ONE JSON line.
+
+    python bench.py [--gpus N --steps K --warmup W --batch B --dtype fp16|bf16|fp32]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import gfa_import  # noqa: E402,F401
+from gfa_amd import ops, pgd  # noqa: E402
+from gfa_amd.dist import gather_shards  # noqa: E402
+from gfa_amd.encoder import SyntheticEncoder  # noqa: E402
+from gfa_amd.stylegan2 import SynthesisNet  # noqa: E402
+from gfa_amd.vgg import VGGNet  # noqa: E402
+from gfa_amd.weights import (make_encoder_weights, make_generator_weights,  # noqa: E402
+                             make_vgg_weights)
+
+DT = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
+DT_NAME = {"fp32": "f32", "fp16": "f16", "bf16": "bf16"}
+# MI355X_MICROARCH.md chip table: dense MFMA peaks (TFLOP/s)
+PEAK_TFLOPS = {"fp32": 157.3, "fp16": 2500.0, "bf16": 2500.0}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=128, help="images per GPU")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--pgd-steps", type=int, default=20)
+    ap.add_argument("--dtype", default="fp16", choices=list(DT))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-steps", type=int, default=1)
+    ap.add_argument("--no-roofline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(size, pgd_steps, sample_steps):
+    """The oracle (CPU restatement, fp32, all host cores) on a bounded sample: one 256² image,
+    `sample_steps` PGD iterations, extrapolated to a PGD-`pgd_steps` attack."""
+    from oracle import attack_ref, vgg_ref
+    # the box's CPU share (OMP_NUM_THREADS is set to it there); affinity shows the whole machine
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    cores = max(1, min(cores, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(cores)
+    gp = make_generator_weights(size, seed=0)
+    ep = make_encoder_weights(size, seed=1)
+    vp = vgg_ref.load_positional(make_vgg_weights(1234))
+    g = torch.Generator().manual_seed(123)
+    x0 = torch.rand(1, 3, size, size, generator=g) * 2 - 1
+    t = torch.rand(1, 3, size, size, generator=g) * 2 - 1
+    refs = attack_ref.Refs(gp, vp, ep, x0, t, size)
+    attack_ref.loss_grad(gp, vp, ep, x0, refs, size)  # warm-up
+    t0 = time.perf_counter()
+    adv = x0.clone()
+    for _ in range(sample_steps):
+        _, gr = attack_ref.loss_grad(gp, vp, ep, adv, refs, size)
+        adv = attack_ref.project_step(adv, x0, gr, 2 * 8 / 255, 2 * 2 / 255)
+    dt = (time.perf_counter() - t0) / sample_steps
+    return {"value": 1.0 / (dt * pgd_steps), "unit": "attacked images/s", "cores": cores,
+            "kind": "port",
+            "sample": f"oracle fp32 CPU, 1 image @{size}², {sample_steps} PGD step(s) timed "
+                      f"({dt:.2f} s/step) extrapolated to PGD-{pgd_steps}; "
+                      f"torch.set_num_threads({cores})"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("launch N>1 with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    T = DT[args.dtype]
+    S, B = args.size, args.batch
+    gp = make_generator_weights(S, seed=0)
+    ep = make_encoder_weights(S, seed=1)
+    vs = make_vgg_weights(1234)
+    eng = pgd.AttackEngine(SyntheticEncoder(ep, S, device=dev),
+                           SynthesisNet(gp, S, dtype=T, device=dev),
+                           VGGNet(vs, dtype=T, device=dev))
+    g = torch.Generator().manual_seed(1000 + rank)
+    x0 = (torch.rand(B, 3, S, S, generator=g) * 2 - 1).to(dev)
+    tgt = (torch.rand(B, 3, S, S, generator=g) * 2 - 1).to(dev)
+    eps, alpha = 8 / 255, 2 / 255
+    n_total = B * world
+
+    def one_step():
+        adv = eng.run(x0, tgt, args.pgd_steps, eps, alpha)
+        if world > 1:
+            gather_shards(adv, n_total)
+        return adv
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    prof = []
+    if not args.no_roofline:
+        ops.PROFILE = prof
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ops.PROFILE = None
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = tt.item()
+    ms = elapsed / args.steps * 1e3
+    value = n_total * args.steps / elapsed
+    flops_img_step = pgd.algorithmic_flops_per_image_step(eng.G, eng.V)
+    out = {
+        "metric": "attacked images/sec, PGD-20 L∞ ε=8/255 at 256², 1/2/4/8 MI355X",
+        "value": value, "unit": "attacked images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": DT_NAME[args.dtype],
+        "data": "synthetic: seeded U(-1,1) image/target pairs, seeded random-init StyleGAN2 "
+                "(256², cm=2), VGG16 trunk and linear encoder (no checkpoints offline)",
+        "config": {"workload": f"PGD-{args.pgd_steps} L∞ eps=8/255 alpha=2/255 at {S}², "
+                               f"{B} images/GPU (BASELINE config #4 per-GPU share), "
+                               f"RCCL all-gather of outputs when N>1",
+                   "images_per_gpu": B, "global_batch": n_total, "size": S,
+                   "pgd_steps": args.pgd_steps, "parallelism": f"dp{world}",
+                   "algorithmic_gflop_per_image_step": flops_img_step / 1e9,
+                   "effective_tflops": flops_img_step * B * args.pgd_steps * world
+                   / (elapsed / args.steps) / 1e12},
+    }
+    if prof:
+        durs = [a.elapsed_time(b) for a, b, _ in prof]  # ms
+        tot_ms = sum(durs)
+        tot_fl = sum(f for _, _, f in prof)
+        n = len(prof)
+        ach = tot_fl / (tot_ms * 1e-3) / 1e12
+        peak = PEAK_TFLOPS[args.dtype]
+        out["roofline"] = {
+            "kernel": "mia::conv3x3_kernel (all launches: StyledConv fwd/dgrad, VGG fwd/dgrad)",
+            "bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
+            "traffic": None, "launches": n, "avg_launch_us": tot_ms / n * 1e3,
+            "algorithmic_gflop_per_launch": tot_fl / n / 1e9,
+            "share_of_step_time": tot_ms / (elapsed * 1e3)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(S, args.pgd_steps, args.cpu_sample_steps)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

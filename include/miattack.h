@@ -1,0 +1,198 @@
+/*
+ * libmiattack — C ABI of the MI355X (gfx950 / CDNA4) adversarial-perturbation engine.
+ *
+ * Hot path (BASELINE.json north_star): PGD/FGSM over  encoder → StyleGAN2 synthesis → VGG feature
+ * loss → ∇ wrt pixels → sign-project onto the L∞ ball. The reference has no FFI for this path: it
+ * runs PyTorch modules (cuDNN + un-vendored rosinality CUDA ops). Each entry point below replaces
+ * one device computation the reference performs, cited as file:line into /root/reference
+ * ([ext] = the un-vendored rosinality op the reference calls through net.decoder).
+ *
+ * Conventions
+ *   - All pointers are DEVICE pointers owned by the caller (PyTorch caching allocator).
+ *   - Feature maps are NHWC, element type given by `dtype` (MIA_F32 / MIA_F16 / MIA_BF16);
+ *     style, demod, bias, noise, reduction buffers and image-space tensors are fp32.
+ *     Images at the API boundary are NCHW fp32 in [-1,1].
+ *   - `stream` is a hipStream_t; every call is asynchronous on it, stateless and re-entrant.
+ *   - Every call returns 0 on success or a negative MIA_E* code; mia_last_error_string() (per
+ *     thread) gives detail. No C++ exception crosses the ABI.
+ */
+#ifndef MIATTACK_H
+#define MIATTACK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIA_F32 0
+#define MIA_F16 1
+#define MIA_BF16 2
+
+#define MIA_OK 0
+#define MIA_EINVAL (-1)
+#define MIA_ELAUNCH (-2)
+
+#define MIA_ACT_NONE 0
+#define MIA_ACT_RELU 1
+#define MIA_ACT_LRELU_S2 2 /* leaky_relu(v, 0.2) * sqrt(2)  (FusedLeakyReLU) */
+
+int mia_version(void);
+const char* mia_last_error_string(void);
+/* K-padding the conv weights need for `dtype` (weights are [Cout][Kpad], K = 9*Cin). */
+int mia_conv_kpad(int cin, int dtype);
+
+/*
+ * Generic 3x3 / stride 1 / pad 1 implicit-GEMM convolution on MFMA (NHWC).
+ *   y[n,p,co] = epilogue( Σ_{tap,ci} in(x)[n, p+tap, ci] · w[co][tap*Cin + ci] )
+ * Replaces: the cuDNN convs of code/vgg.py:45-62 (VGG fwd and, with flipped/transposed weights,
+ * their input-gradient), the grouped conv of ModulatedConv2d [ext] (modulation folded into
+ * in_scale, demodulation into out_scale), and the conv_transpose2d + Blur of the up-sampling
+ * StyledConv [ext] (4-phase weights + shuffle_out).
+ * Prologue on the A operand:  in(x) = act_in(x) * in_scale[n][ci].
+ * Epilogue, in this order (each step optional):
+ *   sdot[n][co] += acc * act_aux(aux_x[n,p,co])       (style gradient, Σ over pixels)
+ *   v = acc * out_scale[n][co % cout_mod]
+ *   v += noise_w * noise[pixel_out] ; v += bias[co % cout_mod]
+ *   v += tap_coef * (tap_a - tap_t) ; v *= (mask_a > 0) ; v = act_out(v) ; v += y (accumulate)
+ *   y[...] = v           (pixel-shuffled to (2H, 2W, Cout/4) when shuffle_out)
+ */
+typedef struct mia_conv_args {
+  const void* x;          /* [N][H][W][Cin] */
+  const void* w;          /* [Cout][Kpad] */
+  void* y;                /* [N][H][W][y_cstride] or shuffled; may be NULL (sdot only) */
+  int N, H, W, Cin, Cout, Kpad;
+  int y_cstride;          /* channel stride of y (0 → Cout, or Cout/4 when shuffle_out) */
+  int act_in;             /* MIA_ACT_* applied to x before in_scale */
+  const float* in_scale;  /* [N][Cin] or NULL */
+  const float* out_scale; /* [N][cout_mod] or NULL */
+  const float* bias;      /* [cout_mod] or NULL */
+  const float* noise;     /* [Hout*Wout] or NULL */
+  float noise_w;
+  int act_out;            /* MIA_ACT_* applied at the end */
+  int shuffle_out;        /* 1: Cout = 4*cout_mod phases (py,px) → output (2H,2W,cout_mod) */
+  const void* aux_x;      /* [N][H][W][Cout] (same layout as y, un-shuffled) for sdot */
+  int act_aux;
+  float* sdot;            /* [N][Cout] fp32, accumulated with atomics */
+  const void* tap_a;      /* [N][H][W][Cout] */
+  const void* tap_t;
+  float tap_coef;
+  const void* mask_a;     /* [N][H][W][Cout] */
+  int accumulate;
+} mia_conv_args;
+
+int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream);
+
+/* ---- named entry points (thin wrappers over mia_conv3x3) ------------------------------- */
+/* ModulatedConv2d + NoiseInjection + FusedLeakyReLU bias, forward [ext]
+ * (net.decoder at code/attack/attack_main2.py:619-621). Writes pre = demod·conv(act(x)·s) +
+ * noise_w·noise + bias; the lrelu·√2 is applied by the consumer (act_in / act_aux). upsample=1
+ * expects 4-phase up-conv weights (Cout = 4*cout) and writes (2H,2W,cout). */
+int mia_modconv_fwd(const void* x, const void* w, void* pre, int N, int H, int W, int Cin,
+                    int Cout, int Kpad, int act_in, const float* style, const float* demod,
+                    const float* noise, float noise_w, const float* bias, int upsample, int dtype,
+                    void* stream);
+/* Input gradient + style sdot of the modulated conv (K15, no weight gradient). gy is the
+ * demod-scaled pre-activation gradient (mia_bias_act_bwd), w_t the flipped/transposed weights
+ * ([Cin][Kpad'] over K' = 9*Cout, or 9*4*cout for up-convs), x_fwd/act_x the forward input. */
+int mia_modconv_bwd(const void* gy, const void* w_t, void* gx, int N, int H, int W, int Cin_g,
+                    int Cout_g, int Kpad, const void* x_fwd, int act_x, const float* style,
+                    float* sdot, int dtype, void* stream);
+/* VGG conv3x3 + bias + ReLU forward (code/vgg.py:45-62). */
+int mia_vgg_conv_relu_fwd(const void* x, const void* w, const float* bias, void* y, int N,
+                          int H, int W, int Cin, int Cout, int Kpad, int dtype, void* stream);
+/* VGG conv input-gradient with the tap-MSE term and ReLU mask of the layer below fused
+ * (code/vgg.py:45-62 backward; feature MSE interpolation.py:786-817). */
+int mia_vgg_conv_dgrad(const void* g, const void* w_t, void* gx, int N, int H, int W, int Cin_g,
+                       int Cout_g, int Kpad, const void* tap_a, const void* tap_t,
+                       float tap_coef, const void* mask_a, int dtype, void* stream);
+
+/* ---- elementwise / reduction kernels ----------------------------------------------------- */
+/* FusedLeakyReLU + NoiseInjection forward, standalone (K4): y = lrelu(x + nw·noise + b)·√2 (NHWC). */
+int mia_bias_act_fwd(const void* x, const float* noise, float noise_w, const float* bias,
+                     void* y, int N, int H, int W, int C, int dtype, void* stream);
+/* StyledConv backward front (K4 bwd + demod): from g_a = ∂L/∂a and pre:
+ *   g_pre = g_a·lrelu_s2'(pre); q[n][c] += Σ_p g_pre·(pre − nw·noise − b); gy = g_pre·demod[n][c]
+ * gy is written un-shuffled (N,H/2,W/2,4C) when unshuffle=1 (up-conv dgrad input). */
+int mia_bias_act_bwd(const void* g_a, const void* pre, const float* noise, float noise_w,
+                     const float* bias, const float* demod, void* gy, float* q, int N, int H,
+                     int W, int C, int unshuffle, int dtype, void* stream);
+/* upfirdn2d (K3) on fp32 NCHW planes, separable 1-D kernel (taps ≤ 8):
+ * zero-insert `up`, pad (pad0,pad1), correlate with the flipped kernel, keep every `down`-th. */
+int mia_upfirdn2d_fwd(const float* x, float* y, int planes, int H, int W, const float* k1d,
+                      int ktaps, int up, int down, int pad0, int pad1, void* stream);
+int mia_upfirdn2d_bwd(const float* gy, float* gx, int planes, int H, int W, const float* k1d,
+                      int ktaps, int up, int down, int pad0, int pad1, void* stream);
+/* ToRGB (K5): rgb = Σ_ci act(pre)·wr[c][ci]·s[n][ci] + bias[c] (+ upfirdn2d(skip, up 2, pad (2,1)))
+ * pre NHWC (dtype), rgb/skip fp32 NCHW (N,3,H,W)/(N,3,H/2,W/2). */
+int mia_torgb_fwd(const void* pre, const float* style, const float* wr, const float* bias,
+                  const float* skip, float* rgb, int N, int H, int W, int Cin, int dtype,
+                  void* stream);
+/* ToRGB backward: u = Σ_c g[c]·wr[c][ci]; g_a (+)= s·u; gs[n][ci] += Σ_p act(pre)·u. */
+int mia_torgb_bwd(const float* g_rgb, const void* pre, const float* style, const float* wr,
+                  void* g_a, float* gs, int N, int H, int W, int Cin, int accumulate, int dtype,
+                  void* stream);
+/* MaxPool 2x2/2 (K8) NHWC, ceil_mode for odd sizes (code/vgg.py:14,18,24). */
+int mia_maxpool2_fwd(const void* x, void* y, int N, int H, int W, int C, int ceil_mode,
+                     int dtype, void* stream);
+/* MaxPool backward per input pixel (first-max tie rule) + optional tap-MSE term and ReLU mask:
+ *   g_in = [p is argmax]·g_out + tap_coef·(x − tap_t);  g_in *= (x > 0) if mask. */
+int mia_maxpool2_bwd(const void* x, const void* g_out, void* g_in, int N, int H, int W, int C,
+                     int ceil_mode, const void* tap_t, float tap_coef, int mask, int dtype,
+                     void* stream);
+/* avg_pool2d(k) on fp32 NCHW (K9; attack_main2.py:590-591) and its backward. */
+int mia_avgpool_fwd(const float* x, float* y, int planes, int H, int W, int k, void* stream);
+int mia_avgpool_bwd(const float* gy, float* gx, int planes, int H, int W, int k, int accumulate,
+                    void* stream);
+/* NCHW fp32 image (N,3,S,S) → avg_pool(pf) → NHWC (N,S/pf,S/pf,cpad) dtype, channels ≥3 zero. */
+int mia_image_to_nhwc(const float* x, void* y, int N, int S, int pf, int cpad, int dtype,
+                      void* stream);
+/* Σ over an image of (a − b)² for a [n][len] pair (fp32 or dtype), into loss[n] (+=). K10 value. */
+int mia_mse_sum(const void* a, const void* b, float* loss, int n, int64_t len, int dtype,
+                void* stream);
+/* K10 gradient for flat fp32 tensors: g (+)= coef·(a − b). */
+int mia_mse_grad_f32(const float* a, const float* b, float* g, int64_t len, float coef,
+                     int accumulate, void* stream);
+/* Tap-MSE seed for the deepest VGG tap: g = coef·(a − t)·[a > 0 if mask] (dtype, flat). */
+int mia_tap_grad(const void* a, const void* t, void* g, int64_t len, float coef, int mask,
+                 int dtype, void* stream);
+/* d(image) of the reconstruction: g_img = coef·(rec − t) + unpool_pf(g_vgg[n,y,x,c]) (fp32 NCHW). */
+int mia_image_grad(const float* rec, const float* t, const void* g_vgg, float* g_img, int N,
+                   int S, int pf, int cpad, float coef, int dtype, void* stream);
+/* Sign-project step (K11, interpolation.py:92-94, cost = −L):
+ *   g = unpool_pf(g_vgg)/pf² + coef_img·(x − x0) + unpool(g_enc)/(pool_enc²)   [fp32]
+ *   adv = x + a·sign(−g); δ = clamp(adv − x0, −e, e); x = clamp(x0 + δ, lo, hi)   (in place)
+ * g_vgg may be NULL; g_enc may be NULL (else (N,3,enc_res,enc_res) fp32). */
+int mia_pgd_update(float* x, const float* x0, const void* g_vgg, const float* g_enc, int N,
+                   int S, int pf, int cpad, int enc_res, float coef_img, float a, float e,
+                   float lo, float hi, int dtype, void* stream);
+/* PGD random start (torchattacks PGD.forward, interpolation.py:73-76): x = clamp(x0 + e·u, lo, hi),
+ * u = host-seeded U(-1,1) draws. */
+int mia_random_start(float* x, const float* x0, const float* u, int64_t len, float e, float lo,
+                     float hi, void* stream);
+/* K11 alone, given a full fp32 gradient (bit-exact contract vs torch fp32). */
+int mia_sign_project(float* x, const float* x0, const float* g, int64_t len, float a, float e,
+                     float lo, float hi, void* stream);
+/* Adam on pixels (K12, optim.Adam at interpolation.py:767,822): fp32 state, step t ≥ 1. */
+int mia_adam_step(float* p, const float* g, float* m, float* v, int64_t len, float lr,
+                  float beta1, float beta2, float eps, int t, void* stream);
+
+/* ---- small fp32 linear algebra (styles, demod, encoder) ----------------------------------- */
+/* C[m,n] = alpha·Σ_k A[m*sam + k*sak]·B[k*sbk + n*sbn] + beta·C[m*scm + n*scn] + bias[n] */
+int mia_gemm_f32(int M, int Nn, int K, float alpha, const float* A, int64_t sam, int64_t sak,
+                 const float* B, int64_t sbk, int64_t sbn, float beta, float* C, int64_t scm,
+                 int64_t scn, const float* bias, void* stream);
+/* demod[n][co] = rsqrt(scale2·Σ_ci s[n][ci]²·wsq[co][ci] + 1e-8)  (ModulatedConv2d demod [ext]) */
+int mia_style_demod(const float* s, const float* wsq, float* demod, int N, int Cin, int Cout,
+                    float scale2, void* stream);
+/* gs[n][ci] += −scale2·s[n][ci]·Σ_co q[n][co]·demod[n][co]²·wsq[co][ci] */
+int mia_demod_bwd(const float* q, const float* demod, const float* wsq, const float* s, float* gs,
+                  int N, int Cin, int Cout, float scale2, void* stream);
+/* dst[i*bytes .. ] = src for i < count (broadcast the constant input over the batch). */
+int mia_repeat(const void* src, void* dst, int64_t bytes, int count, void* stream);
+int mia_memset(void* dst, int value, int64_t bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MIATTACK_H */

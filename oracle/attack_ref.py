@@ -1,0 +1,102 @@
+"""CPU oracle: white-box objective + PGD/FGSM (TEST INFRASTRUCTURE ONLY, see oracle/__init__).
+
+* Objective — ``code/attack/interpolation.py:743-818`` (``optimize_vgg``), per image, every MSE
+  with ``reduction='mean'`` (``:766``)::
+
+    L = (10·MSE(E(x'), E(t')) − MSE(E(x'), E(x0')))                       # latent terms
+      + (MSE(t, G(E(x'))) + 0.1·Σ_k MSE(V_k(G(E(x'))'), V_k(t')))           # reconstruction terms
+      + (10·MSE(x0, x) + Σ_k MSE(V_k(x'), V_k(x0')))                        # input-fidelity terms
+
+  with ' = avg_pool2d(·, S/256) (``:749-750,780-785``). The decoder gets the raw encoder output
+  (no latent_avg, ``:780``). Images are independent, so a batch's loss is the SUM of per-image
+  losses (each image's gradient equals the reference's batch-1 gradient).
+* PGD update — torchattacks ``PGD.forward`` copied in comments at ``interpolation.py:62-96``:
+  adv += α·sign(∇cost); δ = clamp(adv − x, −ε, ε); adv = clamp(x + δ, lo, hi). The reference
+  minimises L, so cost = −L (the targeted form, ``:83-86``). ε, α are in [0,1] pixel units and the
+  tensors live in [-1,1]: e = 2ε, a = 2α, lo/hi = −1/+1.
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import encoder_ref, stylegan2_ref, vgg_ref
+
+LOSS_WEIGHTS = dict(lat_t=10.0, lat_o=-1.0, img_rec_t=1.0, vgg_rec_t=0.1, img_o=10.0, vgg_img=1.0)
+
+
+def _mse_per_image(a, b):
+    return ((a - b) ** 2).reshape(a.shape[0], -1).mean(dim=1)
+
+
+class Refs:
+    """Precomputed (no_grad) targets: interpolation.py:757-764."""
+
+    def __init__(self, gp, vp, ep, x0, t, size):
+        with torch.no_grad():
+            pf = max(1, size // 256)
+            self.x0, self.t = x0, t
+            self.x0p = F.avg_pool2d(x0, pf) if pf > 1 else x0
+            self.tp = F.avg_pool2d(t, pf) if pf > 1 else t
+            self.lat_t = encoder_ref.encode(ep, self.tp)
+            self.lat_o = encoder_ref.encode(ep, self.x0p)
+            self.taps_t = vgg_ref.vgg_forward(vp, self.tp)
+            self.taps_o = vgg_ref.vgg_forward(vp, self.x0p)
+
+
+def objective(gp, vp, ep, x, refs, size, weights=LOSS_WEIGHTS, per_image=False):
+    pf = max(1, size // 256)
+    xp = F.avg_pool2d(x, pf) if pf > 1 else x
+    lat = encoder_ref.encode(ep, xp)
+    rec = stylegan2_ref.synthesis(gp, lat, size)
+    recp = F.avg_pool2d(rec, pf) if pf > 1 else rec
+    taps_rec = vgg_ref.vgg_forward(vp, recp)
+    taps_x = vgg_ref.vgg_forward(vp, xp)
+    l_lat_t = _mse_per_image(refs.lat_t, lat)
+    l_lat_o = _mse_per_image(refs.lat_o, lat)
+    l_img_rec_t = _mse_per_image(refs.t, rec)
+    l_vgg_rec_t = sum(_mse_per_image(a, b) for a, b in zip(taps_rec, refs.taps_t))
+    l_img_o = _mse_per_image(refs.x0, x)
+    l_vgg_img = sum(_mse_per_image(a, b) for a, b in zip(taps_x, refs.taps_o))
+    w = weights
+    L = (w["lat_t"] * l_lat_t + w["lat_o"] * l_lat_o + w["img_rec_t"] * l_img_rec_t
+         + w["vgg_rec_t"] * l_vgg_rec_t + w["img_o"] * l_img_o + w["vgg_img"] * l_vgg_img)
+    return L if per_image else L.sum()
+
+
+def loss_grad(gp, vp, ep, x, refs, size):
+    """∇_x L (summed over images) and the per-image losses."""
+    xx = x.detach().clone().requires_grad_(True)
+    L = objective(gp, vp, ep, xx, refs, size, per_image=True)
+    (g,) = torch.autograd.grad(L.sum(), xx)
+    return L.detach(), g
+
+
+def project_step(adv, x0, g, e, a, lo=-1.0, hi=1.0):
+    """interpolation.py:92-94 with cost = −L: adv + a·sign(−g), then the ε-ball and range clamps.
+    Scalars are rounded to fp32 first, as torch does for a float32 tensor."""
+    a32 = float(np.float32(a))
+    e32 = float(np.float32(e))
+    adv = adv.detach() + a32 * torch.sign(-g)
+    delta = torch.clamp(adv - x0, min=-e32, max=e32)
+    return torch.clamp(x0 + delta, min=lo, max=hi).detach()
+
+
+def pgd(gp, vp, ep, x0, t, size, eps, alpha, steps, random_start=False, start_noise=None,
+        dtype=torch.float32, return_grads=False):
+    """PGD-`steps` in [-1,1] space (FGSM = steps 1, alpha = eps, no random start).
+
+    ``start_noise``: U(-1,1) draws, scaled by e here (host-seeded so the GPU path shares it)."""
+    e, a = 2.0 * eps, 2.0 * alpha
+    x0 = x0.to(dtype)
+    t = t.to(dtype)
+    refs = Refs(gp, vp, ep, x0, t, size)
+    adv = x0.clone()
+    if random_start:
+        adv = torch.clamp(adv + float(np.float32(e)) * start_noise.to(dtype), -1.0, 1.0)
+    grads = []
+    for _ in range(steps):
+        _, g = loss_grad(gp, vp, ep, adv, refs, size)
+        if return_grads:
+            grads.append(g)
+        adv = project_step(adv, x0, g, e, a)
+    return (adv, grads) if return_grads else adv

@@ -1,0 +1,116 @@
+"""CPU oracle: StyleGAN2 synthesis (TEST INFRASTRUCTURE ONLY, see oracle/__init__).
+
+**Parity unpinned.** The reference calls an un-vendored rosinality-style generator
+(``net.decoder([w+], input_is_latent=True, randomize_noise=False, return_latents=True)``,
+``code/attack/attack_main2.py:619-621``; ``SFGenerator_hook`` at ``code/style_fusion_simple.py:51``).
+This module restates that published algorithm in the reference's own per-sample formulation
+(per-sample modulated weights + grouped conv / grouped transposed conv + FIR blur), which is
+structurally different from the product's factorised kernels, so agreement is meaningful:
+
+* ModulatedConv2d: w = (1/sqrt(Cin k²)) · W · s[n,ci]; demod = rsqrt(Σ w² + 1e-8); grouped conv,
+  or for ``upsample``: grouped conv_transpose2d(stride 2) then Blur = upfirdn2d(k=[1,3,3,1]⊗[1,3,3,1]
+  normalised × 4, pad (1,1)).
+* style s = EqualLinear(w) = w · (A/sqrt(512))ᵀ + b_A.
+* StyledConv = ModulatedConv2d → NoiseInjection (x + strength·noise) → FusedLeakyReLU
+  (leaky_relu(x + b, 0.2)·sqrt 2).
+* ToRGB = 1×1 modulated conv without demod + bias + upfirdn2d(skip, up=2, pad (2,1)).
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+BLUR_1D = [1.0, 3.0, 3.0, 1.0]
+
+
+def make_kernel(k1d, dtype=torch.float32):
+    k = torch.tensor(k1d, dtype=dtype)
+    k = k[None, :] * k[:, None]
+    return k / k.sum()
+
+
+def upfirdn2d(x, kernel, up=1, down=1, pad=(0, 0)):
+    """Zero-insert upsample by ``up``, pad (pad0, pad1) on both axes, correlate with the flipped
+    kernel, then keep every ``down``-th sample (rosinality op/upfirdn2d native semantics)."""
+    n, c, h, w = x.shape
+    kh, kw = kernel.shape
+    p0, p1 = pad
+    out = x.reshape(n * c, 1, h, w)
+    if up > 1:
+        z = out.new_zeros(n * c, 1, h * up, w * up)
+        z[:, :, ::up, ::up] = out
+        out = z
+    out = F.pad(out, [max(p0, 0), max(p1, 0), max(p0, 0), max(p1, 0)])
+    if p0 < 0 or p1 < 0:
+        hh, ww = out.shape[2], out.shape[3]
+        out = out[:, :, max(-p0, 0):hh - max(-p1, 0), max(-p0, 0):ww - max(-p1, 0)]
+    wk = torch.flip(kernel, [0, 1]).to(out.dtype).view(1, 1, kh, kw)
+    out = F.conv2d(out, wk)
+    out = out[:, :, ::down, ::down]
+    return out.reshape(n, c, out.shape[2], out.shape[3])
+
+
+def style_affine(p, prefix, w):
+    a = p[prefix + ".modulation.weight"].to(w.dtype)
+    b = p[prefix + ".modulation.bias"].to(w.dtype)
+    return F.linear(w, a * (1.0 / math.sqrt(a.shape[1])), b)
+
+
+def modulated_conv2d(p, prefix, x, w, demodulate=True, upsample=False):
+    weight = p[prefix + ".weight"].to(x.dtype)  # (1, out, in, k, k)
+    _, cout, cin, k, _ = weight.shape
+    n = x.shape[0]
+    style = style_affine(p, prefix, w).view(n, 1, cin, 1, 1)
+    scale = 1.0 / math.sqrt(cin * k * k)
+    wt = scale * weight * style
+    if demodulate:
+        demod = torch.rsqrt(wt.pow(2).sum([2, 3, 4]) + 1e-8)
+        wt = wt * demod.view(n, cout, 1, 1, 1)
+    h, ww = x.shape[2], x.shape[3]
+    if upsample:
+        xin = x.reshape(1, n * cin, h, ww)
+        wt = wt.view(n, cout, cin, k, k).transpose(1, 2).reshape(n * cin, cout, k, k)
+        out = F.conv_transpose2d(xin, wt, padding=0, stride=2, groups=n)
+        out = out.view(n, cout, out.shape[2], out.shape[3])
+        blur = make_kernel(BLUR_1D, x.dtype) * 4.0  # upsample_factor ** 2
+        out = upfirdn2d(out, blur, pad=(1, 1))
+    else:
+        xin = x.reshape(1, n * cin, h, ww)
+        out = F.conv2d(xin, wt.view(n * cout, cin, k, k), padding=k // 2, groups=n)
+        out = out.view(n, cout, out.shape[2], out.shape[3])
+    return out
+
+
+def styled_conv(p, prefix, x, w, noise, upsample=False):
+    out = modulated_conv2d(p, prefix + ".conv", x, w, demodulate=True, upsample=upsample)
+    out = out + p[prefix + ".noise.weight"].to(x.dtype) * noise.to(x.dtype)
+    b = p[prefix + ".activate.bias"].to(x.dtype)
+    return F.leaky_relu(out + b.view(1, -1, 1, 1), 0.2) * math.sqrt(2.0)
+
+
+def to_rgb(p, prefix, x, w, skip=None):
+    out = modulated_conv2d(p, prefix + ".conv", x, w, demodulate=False)
+    out = out + p[prefix + ".bias"].to(x.dtype)
+    if skip is not None:
+        up = make_kernel(BLUR_1D, x.dtype) * 4.0
+        out = out + upfirdn2d(skip, up, up=2, pad=(2, 1))
+    return out
+
+
+def synthesis(p, latent, size):
+    """Generator.forward with input_is_latent=True, randomize_noise=False, w+ of (N, n_latent, 512).
+    Returns the image (N, 3, size, size)."""
+    n = latent.shape[0]
+    dt = latent.dtype
+    log_size = int(math.log2(size))
+    noises = [p[f"noises.noise_{i}"].to(dt) for i in range((log_size - 2) * 2 + 1)]
+    out = p["input.input"].to(dt).repeat(n, 1, 1, 1)
+    out = styled_conv(p, "conv1", out, latent[:, 0], noises[0])
+    skip = to_rgb(p, "to_rgb1", out, latent[:, 1])
+    i = 1
+    for k in range(log_size - 2):
+        out = styled_conv(p, f"convs.{2 * k}", out, latent[:, i], noises[2 * k + 1], upsample=True)
+        out = styled_conv(p, f"convs.{2 * k + 1}", out, latent[:, i + 1], noises[2 * k + 2])
+        skip = to_rgb(p, f"to_rgbs.{k}", out, latent[:, i + 2], skip)
+        i += 2
+    return skip

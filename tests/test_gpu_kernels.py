@@ -1,0 +1,314 @@
+"""Kernel-level parity of libmiattack against plain PyTorch fp32/fp64 references (GPU)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from gfa_amd import layouts, ops
+from oracle import attack_ref, stylegan2_ref
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float32: 2e-5, torch.float16: 2e-2, torch.bfloat16: 8e-2}  # rel. to max |ref|
+
+
+def rel_err(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def nhwc(x, dtype):
+    return x.permute(0, 2, 3, 1).contiguous().to(dtype)
+
+
+def nchw(y):
+    return y.permute(0, 3, 1, 2).double()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,H,Cin,Cout", [(2, 8, 8, 64), (3, 17, 64, 128), (1, 16, 128, 192),
+                                          (4, 4, 512, 512), (2, 33, 32, 8)])
+def test_conv3x3_bias_relu(cuda, dtype, N, H, Cin, Cout):
+    g = torch.Generator().manual_seed(N * 1000 + H * 10 + Cin)
+    x = torch.randn(N, Cin, H, H + 1, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)
+    b = torch.randn(Cout, generator=g) * 0.1
+    xq = x.to(dtype).double()
+    wq = w.to(dtype).double()
+    ref = F.relu(F.conv2d(xq, wq, b.double(), padding=1))
+    y = torch.empty(N, H, H + 1, Cout, dtype=dtype, device=cuda)
+    ops.conv3x3(nhwc(x, dtype).to(cuda), layouts.fwd_matrix(w, dtype).to(cuda), y, cout=Cout,
+                bias=b.to(cuda), act_out=ops.ACT_RELU)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(y), ref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_conv3x3_dgrad_tap_mask(cuda, dtype):
+    g = torch.Generator().manual_seed(7)
+    N, H, Cin, Cout = 2, 12, 64, 128
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)
+    gout = torch.randn(N, Cout, H, H, generator=g)
+    a = torch.randn(N, Cin, H, H, generator=g).relu()
+    t = torch.randn(N, Cin, H, H, generator=g)
+    coef = 0.37
+    wq, gq = w.to(dtype).double(), gout.to(dtype).double()
+    aq, tq = a.to(dtype).double(), t.to(dtype).double()
+    xx = torch.zeros(N, Cin, H, H, dtype=torch.float64, requires_grad=True)
+    (gx,) = torch.autograd.grad((F.conv2d(xx, wq, padding=1) * gq).sum(), xx)
+    ref = (gx + coef * (aq - tq)) * (aq > 0)
+    y = torch.empty(N, H, H, Cin, dtype=dtype, device=cuda)
+    ops.conv3x3(nhwc(gout, dtype).to(cuda), layouts.dgrad_matrix(w, dtype).to(cuda), y, cout=Cin,
+                tap_a=nhwc(a, dtype).to(cuda), tap_t=nhwc(t, dtype).to(cuda), tap_coef=coef,
+                mask_a=nhwc(a, dtype).to(cuda))
+    torch.cuda.synchronize()
+    assert rel_err(nchw(y), ref) < TOL[dtype]
+
+
+def _modconv_setup(seed, N, cin, cout, R):
+    g = torch.Generator().manual_seed(seed)
+    p = {
+        "m.weight": torch.randn(1, cout, cin, 3, 3, generator=g),
+        "m.modulation.weight": torch.randn(cin, 512, generator=g),
+        "m.modulation.bias": torch.ones(cin),
+    }
+    wlat = torch.randn(N, 512, generator=g)
+    x = torch.randn(N, cin, R, R, generator=g)
+    noise = torch.randn(1, 1, 2 * R, 2 * R, generator=g)
+    bias = 0.1 * torch.randn(cout, generator=g)
+    return p, wlat, x, noise, bias
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("up", [False, True])
+def test_modconv_fwd(cuda, dtype, up):
+    N, cin, cout, R = 3, 64, 128, 8
+    p, wlat, x, noise, bias = _modconv_setup(11, N, cin, cout, R)
+    Ro = 2 * R if up else R
+    noise = noise[..., :Ro, :Ro].contiguous()
+    # reference: the oracle's per-sample formulation on lrelu·√2(x) (stored pre-activations)
+    xa = F.leaky_relu(x.double(), 0.2) * math.sqrt(2)
+    ref = stylegan2_ref.modulated_conv2d({k: v.double() for k, v in p.items()}, "m", xa,
+                                         wlat.double(), demodulate=True, upsample=up)
+    ref = ref + 0.1 * noise.double() + bias.double().view(1, -1, 1, 1)
+    # device path
+    scale = 1.0 / math.sqrt(cin * 9)
+    ws = p["m.weight"][0].double() * scale
+    wm = layouts.upconv_phases(ws) if up else ws
+    s = F.linear(wlat.double(), p["m.modulation.weight"].double() / math.sqrt(512),
+                 p["m.modulation.bias"].double()).float().to(cuda)
+    wsq = (ws ** 2).sum((2, 3)).float().to(cuda)
+    demod = torch.empty(N, cout, device=cuda)
+    ops.style_demod(s, wsq, demod)
+    y = torch.empty(N, Ro, Ro, cout, dtype=dtype, device=cuda)
+    ops.conv3x3(nhwc(x, dtype).to(cuda), layouts.fwd_matrix(wm, dtype).to(cuda), y,
+                cout=4 * cout if up else cout, act_in=ops.ACT_LRELU_S2, in_scale=s,
+                out_scale=demod, noise=noise.reshape(-1).to(cuda), noise_w=0.1,
+                bias=bias.to(cuda), shuffle_out=up)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(y), ref) < 2 * TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("up", [False, True])
+def test_modconv_bwd_input_and_style(cuda, dtype, up):
+    """bias_act_bwd + dgrad(sdot) + demod_bwd reproduce autograd's ∂x and ∂s of a StyledConv."""
+    N, cin, cout, R = 2, 32, 64, 8
+    p, wlat, x, noise, bias = _modconv_setup(5, N, cin, cout, R)
+    Ro = 2 * R if up else R
+    noise = noise[..., :Ro, :Ro].contiguous()
+    g = torch.Generator().manual_seed(99)
+    g_a = torch.randn(N, cout, Ro, Ro, generator=g)
+    pd = {k: v.double() for k, v in p.items()}
+    scale = 1.0 / math.sqrt(cin * 9)
+    x_in = x.double().clone().requires_grad_(True)
+    s_in = F.linear(wlat.double(), pd["m.modulation.weight"] / math.sqrt(512),
+                    pd["m.modulation.bias"]).requires_grad_(True)
+    xa = F.leaky_relu(x_in, 0.2) * math.sqrt(2)
+    xa.retain_grad()
+    # per-sample formulation with style given explicitly
+    wt = scale * pd["m.weight"] * s_in.view(N, 1, cin, 1, 1)
+    dm = torch.rsqrt(wt.pow(2).sum([2, 3, 4]) + 1e-8)
+    wt = (wt * dm.view(N, cout, 1, 1, 1))
+    if up:
+        wt2 = wt.transpose(1, 2).reshape(N * cin, cout, 3, 3)
+        o = F.conv_transpose2d(xa.reshape(1, N * cin, R, R), wt2, stride=2, groups=N)
+        o = o.view(N, cout, o.shape[2], o.shape[3])
+        o = stylegan2_ref.upfirdn2d(o, stylegan2_ref.make_kernel([1, 3, 3, 1], torch.float64) * 4,
+                                    pad=(1, 1))
+    else:
+        o = F.conv2d(xa.reshape(1, N * cin, R, R), wt.reshape(N * cout, cin, 3, 3), padding=1,
+                     groups=N).view(N, cout, R, R)
+    pre = o + 0.1 * noise.double() + bias.double().view(1, -1, 1, 1)
+    act = F.leaky_relu(pre, 0.2) * math.sqrt(2)
+    # the dgrad epilogue returns ∂L/∂(activation of the previous layer); its lrelu' is applied by
+    # that layer's bias_act_bwd
+    gx_ref, gs_ref = torch.autograd.grad((act * g_a.double()).sum(), [xa, s_in])
+    # device path
+    ws_ = pd["m.weight"][0] * scale
+    wm = layouts.upconv_phases(ws_) if up else ws_
+    s = s_in.detach().float().to(cuda)
+    wsq = (ws_ ** 2).sum((2, 3)).float().to(cuda)
+    demod = torch.empty(N, cout, device=cuda)
+    ops.style_demod(s, wsq, demod)
+    xd = nhwc(x, dtype).to(cuda)
+    pre_d = torch.empty(N, Ro, Ro, cout, dtype=dtype, device=cuda)
+    nz = noise.reshape(-1).to(cuda)
+    bz = bias.to(cuda)
+    ops.conv3x3(xd, layouts.fwd_matrix(wm, dtype).to(cuda), pre_d, cout=4 * cout if up else cout,
+                act_in=ops.ACT_LRELU_S2, in_scale=s, out_scale=demod, noise=nz, noise_w=0.1,
+                bias=bz, shuffle_out=up)
+    q = torch.zeros(N, cout, device=cuda)
+    gy = torch.empty((N, R, R, 4 * cout) if up else (N, R, R, cout), dtype=dtype, device=cuda)
+    ops.bias_act_bwd(nhwc(g_a, dtype).to(cuda), pre_d, nz, 0.1, bz, demod, gy, q, unshuffle=up)
+    gs = torch.zeros(N, cin, device=cuda)
+    gx = torch.empty(N, R, R, cin, dtype=dtype, device=cuda)
+    ops.conv3x3(gy, layouts.dgrad_matrix(wm, dtype).to(cuda), gx, cout=cin, out_scale=s, aux_x=xd,
+                act_aux=ops.ACT_LRELU_S2, sdot=gs)
+    ops.demod_bwd(q, demod, wsq, s, gs)
+    torch.cuda.synchronize()
+    tol = 1e-4 if dtype == torch.float32 else 5e-2
+    assert rel_err(nchw(gx), gx_ref) < tol
+    assert rel_err(gs, gs_ref) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("H", [8, 9, 36])
+def test_maxpool_fwd_bwd(cuda, dtype, H):
+    g = torch.Generator().manual_seed(H)
+    N, C = 2, 16
+    x = torch.randn(N, C, H, H, generator=g).relu()
+    x[:, :, 0:2, 0:2] = 0.5  # ties → first max wins
+    xq = x.to(dtype).double().requires_grad_(True)
+    ceil = H % 2 == 1
+    y = F.max_pool2d(xq, 2, 2, ceil_mode=ceil)
+    go = torch.randn(y.shape, generator=g, dtype=torch.float64).to(dtype).double()
+    t = torch.randn(N, C, H, H, generator=g)
+    (gx,) = torch.autograd.grad((y * go).sum(), xq)
+    ref_b = (gx + 0.5 * (xq.detach() - t.to(dtype).double())) * (xq.detach() > 0)
+    xd = nhwc(x, dtype).to(cuda)
+    yd = torch.empty(N, y.shape[2], y.shape[3], C, dtype=dtype, device=cuda)
+    ops.maxpool2_fwd(xd, yd, ceil_mode=ceil)
+    gi = torch.empty_like(xd)
+    ops.maxpool2_bwd(xd, nhwc(go, dtype).to(cuda), gi, ceil_mode=ceil,
+                     tap_t=nhwc(t, dtype).to(cuda), tap_coef=0.5, mask=True)
+    torch.cuda.synchronize()
+    assert torch.equal(nchw(yd).cpu(), y.detach())
+    assert rel_err(nchw(gi), ref_b) < TOL[dtype]
+
+
+@pytest.mark.parametrize("up,down,pad", [(2, 1, (2, 1)), (1, 1, (1, 1)), (1, 2, (1, 1)),
+                                         (2, 2, (1, 2))])
+def test_upfirdn2d(cuda, up, down, pad):
+    g = torch.Generator().manual_seed(3)
+    k1 = [1.0, 3.0, 3.0, 1.0]
+    kn = [v / 4.0 for v in k1]
+    x = torch.randn(2, 3, 9, 9, generator=g, dtype=torch.float64).requires_grad_(True)
+    k2 = torch.tensor(kn, dtype=torch.float64)
+    k2 = k2[:, None] * k2[None, :]
+    ref = stylegan2_ref.upfirdn2d(x, k2, up=up, down=down, pad=pad)
+    gy = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    (gx,) = torch.autograd.grad((ref * gy).sum(), x)
+    y = torch.empty(ref.shape, device=cuda)
+    ops.upfirdn2d_fwd(x.detach().float().to(cuda), y, kn, up=up, down=down, pad=pad)
+    gxd = torch.empty(x.shape, device=cuda)
+    ops.upfirdn2d_bwd(gy.float().to(cuda), gxd, kn, up=up, down=down, pad=pad)
+    torch.cuda.synchronize()
+    assert rel_err(y, ref.detach()) < 1e-5
+    assert rel_err(gxd, gx) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("cin", [32, 128, 512])
+def test_torgb_fwd_bwd(cuda, dtype, cin):
+    g = torch.Generator().manual_seed(cin)
+    N, R = 2, 8
+    pre = torch.randn(N, cin, R, R, generator=g)
+    s = torch.randn(N, cin, generator=g, dtype=torch.float64).requires_grad_(True)
+    wr = torch.randn(3, cin, generator=g, dtype=torch.float64) / math.sqrt(cin)
+    b = torch.randn(3, generator=g, dtype=torch.float64)
+    skip = torch.randn(N, 3, R // 2, R // 2, generator=g, dtype=torch.float64)
+    preq = pre.to(dtype).double().requires_grad_(True)
+    a = F.leaky_relu(preq, 0.2) * math.sqrt(2)
+    wm = wr.view(1, 3, cin) * s.view(N, 1, cin)
+    out = torch.einsum("nchw,noc->nohw", a, wm) + b.view(1, 3, 1, 1)
+    up = torch.tensor([1.0, 3.0, 3.0, 1.0], dtype=torch.float64)
+    up = (up[:, None] * up[None, :]) / 16.0
+    out = out + stylegan2_ref.upfirdn2d(skip, up, up=2, pad=(2, 1))
+    grgb = torch.randn(out.shape, generator=g, dtype=torch.float64)
+    gpre, gsr = torch.autograd.grad((out * grgb).sum(), [a, s])  # ∂L/∂activation, ∂L/∂s
+    pd = nhwc(pre, dtype).to(cuda)
+    rgb = torch.empty(N, 3, R, R, device=cuda)
+    sd = s.detach().float().to(cuda)
+    wrd = wr.float().to(cuda)
+    ops.torgb_fwd(pd, sd, wrd, b.float().to(cuda), skip.float().to(cuda), rgb)
+    ga = torch.full((N, R, R, cin), 0.25, dtype=dtype, device=cuda)
+    gs = torch.zeros(N, cin, device=cuda)
+    ops.torgb_bwd(grgb.float().to(cuda), pd, sd, wrd, ga, gs, accumulate=True)
+    torch.cuda.synchronize()
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert rel_err(rgb, out.detach()) < tol
+    assert rel_err(nchw(ga) - 0.25, gpre) < tol
+    assert rel_err(gs, gsr) < tol
+
+
+def test_sign_project_bit_exact(cuda):
+    """K11 vs the oracle's torch fp32 formula, including g == 0 and the clamp edges."""
+    g = torch.Generator().manual_seed(0)
+    n = 1 << 16
+    x0 = (torch.rand(n, generator=g) * 2 - 1)
+    x0[:64] = 1.0
+    x0[64:128] = -1.0
+    x = (x0 + (torch.rand(n, generator=g) * 2 - 1) * 0.05).clamp(-1, 1)
+    gr = torch.randn(n, generator=g)
+    gr[::7] = 0.0
+    e, a = 2 * 8 / 255, 2 * 2 / 255
+    ref = attack_ref.project_step(x, x0, gr, e, a)
+    xd = x.to(cuda)
+    ops.sign_project(xd, x0.to(cuda), gr.to(cuda), float(np.float32(a)), float(np.float32(e)))
+    u = torch.rand(n, generator=g) * 2 - 1
+    ref_rs = torch.clamp(x0 + float(np.float32(e)) * u, -1.0, 1.0)
+    rs = torch.empty(n, device=cuda)
+    ops.random_start(rs, x0.to(cuda), u.to(cuda), float(np.float32(e)))
+    torch.cuda.synchronize()
+    assert torch.equal(xd.cpu(), ref)
+    assert torch.equal(rs.cpu(), ref_rs)
+
+
+def test_gemm_and_demod(cuda):
+    g = torch.Generator().manual_seed(1)
+    A = torch.randn(37, 70, generator=g)
+    B = torch.randn(70, 45, generator=g)
+    bias = torch.randn(45, generator=g)
+    C = torch.randn(37, 45, generator=g)
+    Cd = C.clone().to(cuda)
+    ops.gemm(37, 45, 70, 0.5, A.to(cuda), 70, 1, B.to(cuda), 45, 1, 2.0, Cd, 45, 1, bias.to(cuda))
+    Bt = B.t().contiguous().to(cuda)  # strided access: B[k][n] = Bt[n][k]
+    C2 = torch.empty(37, 45, device=cuda)
+    ops.gemm(37, 45, 70, 1.0, A.to(cuda), 70, 1, Bt, 1, 70, 0.0, C2, 45, 1)
+    s = torch.randn(4, 64, generator=g)
+    wsq = torch.rand(96, 64, generator=g)
+    d = torch.empty(4, 96, device=cuda)
+    ops.style_demod(s.to(cuda), wsq.to(cuda), d, scale2=0.3)
+    torch.cuda.synchronize()
+    assert rel_err(Cd, 0.5 * A @ B + 2.0 * C + bias) < 1e-5
+    assert rel_err(C2, A @ B) < 1e-5
+    assert rel_err(d, torch.rsqrt(0.3 * (s ** 2) @ wsq.t() + 1e-8)) < 1e-5
+
+
+def test_adam_step(cuda):
+    g = torch.Generator().manual_seed(2)
+    p = torch.randn(1000, generator=g)
+    grads = [torch.randn(1000, generator=g) for _ in range(3)]
+    pr = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pr], lr=0.005)
+    pd, m, v = p.to(cuda), torch.zeros(1000, device=cuda), torch.zeros(1000, device=cuda)
+    for t, gr in enumerate(grads, 1):
+        opt.zero_grad()
+        pr.grad = gr.clone()
+        opt.step()
+        ops.adam_step(pd, gr.to(cuda), m, v, 0.005, 0.9, 0.999, 1e-8, t)
+    torch.cuda.synchronize()
+    assert rel_err(pd, pr.detach()) < 1e-6

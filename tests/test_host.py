@@ -1,0 +1,148 @@
+"""CPU tests of the host side: weight re-layouts, the C ABI surface, API validation, sharding."""
+import ctypes
+import math
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import ROOT
+from gfa_amd import layouts
+from gfa_amd.dist import shard_bounds
+from oracle import stylegan2_ref
+
+HEADER = os.path.join(ROOT, "include", "miattack.h")
+
+
+def _conv_via_matrix(x, m, cout, cin):
+    """Apply a [Cout][Kpad] kernel matrix the way the HIP kernel does (tap-major K)."""
+    N, _, H, W = x.shape
+    cols = F.unfold(x, 3, padding=1)  # (N, cin*9, HW) with ci-major, tap-minor
+    cols = cols.view(N, cin, 9, H * W).transpose(1, 2).reshape(N, 9 * cin, H * W)
+    y = m[:, :9 * cin] @ cols
+    return y.view(N, cout, H, W)
+
+
+def test_fwd_and_dgrad_matrices():
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(6, 5, 3, 3, generator=g, dtype=torch.float64)
+    x = torch.randn(2, 5, 7, 7, generator=g, dtype=torch.float64)
+    m = layouts.fwd_matrix(w, torch.float64)
+    assert torch.allclose(_conv_via_matrix(x, m, 6, 5), F.conv2d(x, w, padding=1))
+    gy = torch.randn(2, 6, 7, 7, generator=g, dtype=torch.float64)
+    xx = x.clone().requires_grad_(True)
+    (gx,) = torch.autograd.grad((F.conv2d(xx, w, padding=1) * gy).sum(), xx)
+    md = layouts.dgrad_matrix(w, torch.float64)
+    assert torch.allclose(_conv_via_matrix(gy, md, 5, 6), gx)
+
+
+def test_kpad():
+    assert layouts.kpad_for(8, torch.float16) == 96 and layouts.kpad_for(8, torch.float32) == 80
+    assert layouts.kpad_for(512, torch.float16) == 4608
+
+
+def test_upconv_phases_equal_convtranspose_plus_blur():
+    """conv_transpose2d(stride 2) + Blur(pad (1,1)) == 4 phase 3×3 convs, pixel-shuffled."""
+    g = torch.Generator().manual_seed(1)
+    cout, cin, R = 4, 3, 5
+    W = torch.randn(cout, cin, 3, 3, generator=g, dtype=torch.float64)
+    x = torch.randn(2, cin, R, R, generator=g, dtype=torch.float64)
+    t = F.conv_transpose2d(x, W.transpose(0, 1), stride=2)
+    ref = stylegan2_ref.upfirdn2d(t, stylegan2_ref.make_kernel([1, 3, 3, 1], torch.float64) * 4,
+                                  pad=(1, 1))
+    V = layouts.upconv_phases(W)
+    y = F.conv2d(x, V, padding=1)
+    out = torch.empty_like(ref)
+    for p in range(4):
+        out[:, :, p // 2::2, p % 2::2] = y[:, p * cout:(p + 1) * cout]
+    assert torch.allclose(out, ref, atol=1e-12)
+
+
+def _header_functions():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(mia_\w+)\(", txt, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    from gfa_amd import _lib
+    names = _header_functions()
+    assert len(names) >= 30
+    assert set(names) == set(_lib.SIGNATURES), set(names) ^ set(_lib.SIGNATURES)
+    assert os.path.exists(_lib.LIB_PATH), "run __graft_entry__.build() first"
+    lib = _lib.load()  # loads without a GPU; no compute call is made
+    for n in names:
+        assert hasattr(lib, n), n
+    assert lib.mia_version() == 1
+    assert lib.mia_conv_kpad(8, 1) == 96  # host-only helper
+
+
+def test_conv_args_struct_layout_matches_c(tmp_path):
+    """ctypes mirror of mia_conv_args has the C compiler's offsets."""
+    from gfa_amd._lib import ConvArgs
+    fields = [f for f, _ in ConvArgs._fields_]
+    src = tmp_path / "off.c"
+    body = "\n".join(f'printf("%s %zu\\n", "{f}", offsetof(mia_conv_args, {f}));' for f in fields)
+    src.write_text(f'#include <stdio.h>\n#include <stddef.h>\n#include "miattack.h"\n'
+                   f'int main(void){{ {body} printf("size %zu\\n", sizeof(mia_conv_args)); '
+                   f'return 0; }}\n')
+    exe = tmp_path / "off"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
+                   check=True)
+    out = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True,
+                                                         text=True, check=True).stdout.split("\n")
+               if line)
+    for f in fields:
+        assert int(out[f]) == getattr(ConvArgs, f).offset, f
+    assert int(out["size"]) == ctypes.sizeof(ConvArgs)
+
+
+def test_shard_bounds_cover_and_balance():
+    for n in (1, 7, 128, 1024, 1023):
+        for world in (1, 2, 3, 8):
+            spans = [shard_bounds(n, world, r) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+class _StubDecoder:
+    size = 32
+    device = torch.device("cpu")
+
+
+class _StubNet:
+    decoder = _StubDecoder()
+    vgg = object()
+
+
+def test_attack_argument_validation_before_any_device_work():
+    from gfa_amd import attack
+    x = torch.zeros(2, 3, 32, 32)
+    t = torch.zeros(1, 3, 32, 32)
+    net = _StubNet()
+    with pytest.raises(ValueError):
+        attack(net, torch.zeros(2, 3, 16, 16), 8 / 255, 2, target=t)   # wrong size
+    with pytest.raises(ValueError):
+        attack(net, x + 2.0, 8 / 255, 2, target=t)                     # out of [-1,1]
+    with pytest.raises(ValueError):
+        attack(net, x, 8 / 255, 2)                                     # no target
+    with pytest.raises(ValueError):
+        attack(net, x, -1.0, 2, target=t)                              # eps <= 0
+    with pytest.raises(ValueError):
+        attack(net, x, 8 / 255, 2, target=t, norm="l2")                # unsupported norm
+
+
+def test_no_cpu_fallback_in_product():
+    """The product package never imports the oracle and every op goes through the C ABI."""
+    pkg = os.path.join(ROOT, "adversarial-attacks-on-gan-based-image-fusion_amd")
+    for fn in os.listdir(pkg):
+        if fn.endswith(".py"):
+            src = open(os.path.join(pkg, fn)).read()
+            assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), fn
+            assert "torch.nn.functional" not in src, fn  # no torch compute fallback
+    assert math.isfinite(1.0) and sys.version_info >= (3, 8)

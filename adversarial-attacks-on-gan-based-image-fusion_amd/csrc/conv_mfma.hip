@@ -3,31 +3,45 @@
 // One kernel serves every dense contraction of the attack step:
 //   * VGG conv + bias + ReLU forward        (code/vgg.py:45-62)
 //   * VGG conv input-gradient                (flipped/transposed weights; tap-MSE + ReLU mask fused)
-//   * ModulatedConv2d forward [ext]          (modulation = per-(n,ci) A-operand scale, demodulation =
-//                                             per-(n,co) epilogue scale: one shared-weight GEMM,
-//                                             never N per-sample weight tensors)
+//   * ModulatedConv2d forward [ext]          (modulation = per-(n,ci) A-operand scale applied to the
+//                                             MFMA fragments, demodulation = per-(n,co) epilogue
+//                                             scale: one shared-weight GEMM, never N per-sample
+//                                             weight tensors)
 //   * up-sampling ModulatedConv2d [ext]      (conv_transpose2d(stride 2) ∘ Blur folded into four
 //                                             3x3 phase kernels on the low-res grid, pixel-shuffled
 //                                             in the epilogue)
 //   * ModulatedConv2d input/style gradient   (dgrad GEMM + Σ_p gx̃·x style reduction in the epilogue)
 //
 // GEMM view: M = N·H·W output pixels, N-dim = Cout, K = 9·Cin (tap-major, channel-minor).
-// Tile BM×BN×BK with 256 threads = 4 waves (WM×WN), wave tile of FM×FN MFMA 16×16 fragments.
-//   f16/bf16: v_mfma_f32_16x16x32_{f16,bf16}, BK = 32;  f32: v_mfma_f32_16x16x4_f32 ×4, BK = 16.
-// A and B tiles are staged global → registers → LDS (double buffered, one barrier per K-step) in
-// 16-byte chunks; each tile row is 64 B (4 chunks), XOR-swizzled so the ds_read_b128 fragment reads
-// are bank-conflict-free (chunk' = chunk ^ ((4 − (row>>2)) & 3), derived for the gfx950 b128 lane
-// groups {0–3,12–15,20–27},{4–11,16–19,28–31},…).
-// The fp32 path permutes K inside a chunk (lane group q holds k = 4q..4q+3 and step s uses k=4q+s
-// for both operands), so one ds_read_b128 feeds four 16x16x4 MFMAs.
+// Block tile BM×BN×BK, 256 threads = 4 waves (2×2), each wave FM×FN MFMA 16×16 fragments.
+//   f16/bf16: v_mfma_f32_16x16x32_{f16,bf16}, BK = 64;  f32: v_mfma_f32_16x16x4_f32, BK = 32.
+// Every tile row (one pixel's or one output channel's K-slice) is 128 B = 8 chunks of 16 B.
+//
+// Staging: both operands go global → LDS by LDS-DMA (global_load_lds_dwordx4), a 2-stage ring:
+// the loads of K-step k+1 are issued before the MFMAs of step k and retired by the barrier at its
+// end. The im2col gather is done by the per-lane SOURCE address (one pixel row + tap offset);
+// lanes whose tap falls outside the image (or whose row is beyond M / Cout) read a 16-byte zero
+// vector instead, so the loop has no branches. LDS-DMA writes lane-linearly, so the bank
+// swizzle (chunk' = chunk ^ ((row>>1)&7), conflict-free for the ds_read_b128 fragment lane groups
+// on 128-B rows) is applied by permuting which chunk each lane fetches (guide rule 21).
+// The modulation prologue x̃ = act(x)·s[n][ci] is applied to A fragments after ds_read, with s
+// held in an LDS table for the (≤ 9) images a tile spans.
+#include <algorithm>
+#include <type_traits>
+
 #include "mia_common.h"
 
 namespace mia {
 
 struct ConvK {
   mia_conv_args a;
-  int M, HW, cout_mod, ystride;
+  int M, HW, cout_mod, ystride, log2cin, n_first_max;
 };
+
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+__device__ __attribute__((aligned(16))) uint4 g_zero16[4];  // zero source for masked DMA lanes
 
 __device__ __forceinline__ int xcd_remap(int b, int nblk) {
   // Blocks are dealt round-robin over the 8 XCDs; give each XCD a contiguous run of logical tiles
@@ -38,7 +52,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
   return base + (b >> 3);
 }
 
-__device__ __forceinline__ int swz(int row) { return (4 - ((row >> 2) & 3)) & 3; }
+__device__ __forceinline__ int fsw(int row) { return (row >> 1) & 7; }
 
 template <typename T>
 __device__ __forceinline__ f32x4 mfma_chunk(const typename Vec<T>::type& a,
@@ -53,6 +67,7 @@ __device__ __forceinline__ f32x4 mfma_chunk<__bf16>(const bf16x8& a, const bf16x
 }
 template <>
 __device__ __forceinline__ f32x4 mfma_chunk<float>(const f32x4& a, const f32x4& b, f32x4 c) {
+  // fp32: lane group q holds k = 4q..4q+3 of the chunk; step s uses k = 4q+s for both operands
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
@@ -66,99 +81,124 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   return v;
 }
 
-template <typename T, int BM, int BN, int WM, int WN, bool PRO>
-__global__ __launch_bounds__(256) void conv3x3_kernel(const ConvK k) {
+// x̃ = act(x)·s on a 16-byte fragment; for LRELU the table already holds s·√2, and
+// leaky_relu(x, 0.2) = max(x, 0.2·x).
+template <typename T>
+__device__ __forceinline__ void modulate(typename Vec<T>::type& v, const typename Vec<T>::type& s,
+                                         bool lrelu) {
+  if constexpr (std::is_same<T, _Float16>::value) {
+    if (lrelu) v = __builtin_elementwise_max(v, v * (_Float16)0.2f);
+    v = v * s;
+  } else {
+#pragma unroll
+    for (int e = 0; e < Vec<T>::N; ++e) {
+      float f = (float)v[e];
+      if (lrelu) f = fmaxf(f, 0.2f * f);
+      v[e] = (T)(f * (float)s[e]);
+    }
+  }
+}
+
+constexpr int ROWB = 128;  // bytes per tile row (one K-step slice)
+
+template <typename T, int BM, int BN, bool PRO>
+__global__ __launch_bounds__(256, 2) void conv3x3_kernel(const ConvK k) {
   typedef typename Vec<T>::type VT;
   constexpr int VEC = Vec<T>::N;
-  constexpr int BK = 4 * VEC;
-  constexpr int FM = BM / (WM * 16), FN = BN / (WN * 16);
-  constexpr int A_CH = BM * 4 / 256, B_CH = BN * 4 / 256;
-  static_assert(WM * WN == 4, "4 waves");
-  static_assert(A_CH >= 1 && B_CH >= 1, "tile too small");
+  constexpr int BK = ROWB / (int)sizeof(T);
+  constexpr int FM = BM / 32, FN = BN / 32;         // 2×2 waves
+  constexpr int A_INS = BM / 32, B_INS = BN / 32;   // 1-KB DMA pieces per wave per K-step
+  constexpr int STAGE = (BM + BN) * ROWB;
 
-  __shared__ VT lds[2][(BM + BN) * 4];
+  extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const mia_conv_args& p = k.a;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WN, wn = wid % WN;
+  const int wm = wid >> 1, wn = wid & 1;
   const int nbn = (p.Cout + BN - 1) / BN;
   const int nbm = (k.M + BM - 1) / BM;
   const int b = xcd_remap(blockIdx.x, nbm * nbn);
   const int m0 = (b / nbn) * BM, n0 = (b % nbn) * BN;
   const int H = p.H, W = p.W, Cin = p.Cin;
+  const int lc = k.log2cin;
 
-  // ---- staging state -----------------------------------------------------------------------
   const T* __restrict__ X = (const T*)p.x;
   const T* __restrict__ Wt = (const T*)p.w;
-  const int kq = tid & 3;
-  int a_n[A_CH], a_y[A_CH], a_x[A_CH];
-  bool a_ok[A_CH];
-#pragma unroll
-  for (int j = 0; j < A_CH; ++j) {
-    const int m = m0 + (tid >> 2) + 64 * j;
-    a_ok[j] = m < k.M;
-    const int mm = a_ok[j] ? m : 0;
-    a_n[j] = mm / k.HW;
-    const int rem = mm - a_n[j] * k.HW;
-    a_y[j] = rem / W;
-    a_x[j] = rem - a_y[j] * W;
-  }
-  const T* b_ptr[B_CH];
-  bool b_ok[B_CH];
-#pragma unroll
-  for (int j = 0; j < B_CH; ++j) {
-    const int c = n0 + (tid >> 2) + 64 * j;
-    b_ok[j] = c < p.Cout;
-    b_ptr[j] = Wt + (size_t)(b_ok[j] ? c : 0) * p.Kpad + kq * VEC;
-  }
-  int tap = (kq * VEC) / Cin, ci = (kq * VEC) - tap * Cin;
-  VT ra[A_CH], rb[B_CH];
+  const T* zero = (const T*)g_zero16;
 
-  auto load_tile = [&](int kb) {
+  // ---- per-lane DMA source state -----------------------------------------------------------
+  int a_base[A_INS], a_koff[A_INS], a_mask[A_INS];
 #pragma unroll
-    for (int j = 0; j < A_CH; ++j) {
-      VT v = {};
-      if (a_ok[j] && tap < 9) {
-        const int ty = tap / 3;
-        const int yy = a_y[j] + ty - 1, xx = a_x[j] + (tap - 3 * ty) - 1;
-        if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
-          v = *(const VT*)(X + ((size_t)(a_n[j] * H + yy) * W + xx) * Cin + ci);
-          if constexpr (PRO) {
-            const float* sc = p.in_scale ? p.in_scale + (size_t)a_n[j] * Cin + ci : nullptr;
+  for (int j = 0; j < A_INS; ++j) {
+    const int row = (wid * A_INS + j) * 8 + (lane >> 3);
+    a_koff[j] = ((lane & 7) ^ fsw(row)) * VEC;
+    const int m = m0 + row;
+    int msk = 0, base = 0;
+    if (m < k.M) {
+      const int n = m / k.HW;
+      const int rem = m - n * k.HW;
+      const int y = rem / W, x = rem - (rem / W) * W;
+      base = ((n * H + y) * W + x) * Cin;
 #pragma unroll
-            for (int e = 0; e < VEC; ++e) {
-              float f = apply_act(to_f(v[e]), p.act_in);
-              if (sc) f *= sc[e];
-              v[e] = from_f<T>(f);
-            }
-          }
-        }
+      for (int t = 0; t < 9; ++t) {
+        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W) msk |= 1 << t;
       }
-      ra[j] = v;
+    }
+    a_base[j] = base;
+    a_mask[j] = msk;
+  }
+  const T* b_src[B_INS];
+#pragma unroll
+  for (int j = 0; j < B_INS; ++j) {
+    const int row = (wid * B_INS + j) * 8 + (lane >> 3);
+    const int c = n0 + row;
+    b_src[j] = c < p.Cout ? Wt + (size_t)c * p.Kpad + ((lane & 7) ^ fsw(row)) * VEC : nullptr;
+  }
+
+  auto issue = [&](int kb, int st) {
+    char* sa = smem + st * STAGE;
+    char* sb = sa + BM * ROWB;
+#pragma unroll
+    for (int j = 0; j < A_INS; ++j) {
+      const int kk = kb * BK + a_koff[j];
+      const int tap = kk >> lc;
+      const int ci = kk & (Cin - 1);
+      const int dy = (tap * 11) >> 5;  // tap / 3 for tap < 9
+      const int dx = tap - 3 * dy;
+      const T* src = ((a_mask[j] >> tap) & 1)
+                         ? X + (a_base[j] + ((dy - 1) * W + (dx - 1)) * Cin + ci)
+                         : zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(sa + (wid * A_INS + j) * 1024), 16,
+                                       0, 0);
     }
 #pragma unroll
-    for (int j = 0; j < B_CH; ++j) {
-      VT v = {};
-      if (b_ok[j]) v = *(const VT*)(b_ptr[j] + (size_t)kb * BK);
-      rb[j] = v;
+    for (int j = 0; j < B_INS; ++j) {
+      const T* src = b_src[j] ? b_src[j] + (size_t)kb * BK : zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(sb + (wid * B_INS + j) * 1024), 16,
+                                       0, 0);
     }
   };
-  auto advance = [&]() {
-    ci += BK;
-    while (ci >= Cin) { ci -= Cin; ++tap; }
-  };
-  auto store_tile = [&](int buf) {
+
+  // ---- modulation table (PRO): s[n][ci] (·√2 for lrelu inputs) for the images of this tile ----
+  const int n_first = m0 / k.HW;
+  T* stab = (T*)(smem + 2 * STAGE);
+  const bool lrelu_in = p.act_in == MIA_ACT_LRELU_S2;
+  int a_nl[FM];
+  if constexpr (PRO) {
+    const int n_last = (min(m0 + BM, k.M) - 1) / k.HW;
+    const int cnt = (n_last - n_first + 1) * Cin;
+    const float mul = lrelu_in ? SQRT2 : 1.f;
+    for (int i = tid; i < cnt; i += 256) {
+      const float sv = p.in_scale ? p.in_scale[(size_t)n_first * Cin + i] : 1.f;
+      stab[i] = from_f<T>(sv * mul);
+    }
 #pragma unroll
-    for (int j = 0; j < A_CH; ++j) {
-      const int r = (tid >> 2) + 64 * j;
-      lds[buf][r * 4 + (kq ^ swz(r))] = ra[j];
+    for (int i = 0; i < FM; ++i) {
+      const int m = min(m0 + wm * FM * 16 + 16 * i + (lane & 15), k.M - 1);
+      a_nl[i] = (m / k.HW - n_first) * Cin;
     }
-#pragma unroll
-    for (int j = 0; j < B_CH; ++j) {
-      const int r = (tid >> 2) + 64 * j;
-      lds[buf][(BM + r) * 4 + (kq ^ swz(r))] = rb[j];
-    }
-  };
+  }
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -167,28 +207,42 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(const ConvK k) {
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = p.Kpad / BK;
-  load_tile(0);
-  store_tile(0);
+  issue(0, 0);
   __syncthreads();
   const int frow = lane & 15, fq = lane >> 4;
-  const int fsw = fq ^ swz(frow);
   for (int kb = 0; kb < nk; ++kb) {
-    const int cur = kb & 1;
-    if (kb + 1 < nk) {
-      advance();
-      load_tile(kb + 1);
+    const int st = kb & 1;
+    if (kb + 1 < nk) issue(kb + 1, st ^ 1);
+    const char* sa = smem + st * STAGE;
+    const char* sb = sa + BM * ROWB;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = s * 4 + fq;
+      VT af[FM], bf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm * FM * 16 + 16 * i + frow;
+        af[i] = *(const VT*)(sa + row * ROWB + ((ch ^ fsw(row)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * FN * 16 + 16 * j + frow;
+        bf[j] = *(const VT*)(sb + row * ROWB + ((ch ^ fsw(row)) << 4));
+      }
+      if constexpr (PRO) {
+        const int ci = (kb * BK + ch * VEC) & (Cin - 1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const VT sv = *(const VT*)(stab + a_nl[i] + ci);
+          modulate<T>(af[i], sv, lrelu_in);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma_chunk<T>(af[i], bf[j], acc[i][j]);
     }
-    VT af[FM], bf[FN];
-#pragma unroll
-    for (int i = 0; i < FM; ++i) af[i] = lds[cur][(wm * FM * 16 + 16 * i + frow) * 4 + fsw];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) bf[j] = lds[cur][(BM + wn * FN * 16 + 16 * j + frow) * 4 + fsw];
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = mfma_chunk<T>(af[i], bf[j], acc[i][j]);
-    if (kb + 1 < nk) store_tile(cur ^ 1);
-    __syncthreads();
+    __syncthreads();  // retires the DMA of step kb+1 (vmcnt(0)) and frees stage st for kb+2
   }
 
   // ---- epilogue ---------------------------------------------------------------------------
@@ -265,26 +319,37 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(const ConvK k) {
     }
 }
 
-template <typename T, int BM, int BN, int WM, int WN>
+template <typename T, int BM, int BN, bool PRO>
 static int launch_tile(const ConvK& k, hipStream_t st) {
   const int nbm = (k.M + BM - 1) / BM, nbn = (k.a.Cout + BN - 1) / BN;
   const int nblk = nbm * nbn;
-  const bool pro = k.a.in_scale != nullptr || k.a.act_in != MIA_ACT_NONE;
-  if (pro)
-    hipLaunchKernelGGL((conv3x3_kernel<T, BM, BN, WM, WN, true>), dim3(nblk), dim3(256), 0, st, k);
-  else
-    hipLaunchKernelGGL((conv3x3_kernel<T, BM, BN, WM, WN, false>), dim3(nblk), dim3(256), 0, st, k);
+  size_t lds = 2 * (BM + BN) * ROWB;
+  if (PRO) lds += (size_t)k.n_first_max * k.a.Cin * sizeof(T);
+  auto fn = conv3x3_kernel<T, BM, BN, PRO>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
+      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(fn, dim3(nblk), dim3(256), lds, st, k);
   return check_launch("conv3x3");
+}
+
+template <typename T, bool PRO>
+static int launch_bn(const ConvK& k, hipStream_t st) {
+  if (k.a.Cout <= 64) return launch_tile<T, 128, 64, PRO>(k, st);
+  return launch_tile<T, 128, 128, PRO>(k, st);
 }
 
 template <typename T>
 static int launch_conv(const ConvK& k, hipStream_t st) {
-  if (k.a.Cout <= 64) return launch_tile<T, 128, 64, 2, 2>(k, st);
-  return launch_tile<T, 128, 128, 2, 2>(k, st);
+  const bool pro = k.a.in_scale != nullptr || k.a.act_in != MIA_ACT_NONE;
+  return pro ? launch_bn<T, true>(k, st) : launch_bn<T, false>(k, st);
 }
 
-static int bk_for(int dtype) { return dtype == MIA_F32 ? 16 : 32; }
-static int vec_for(int dtype) { return dtype == MIA_F32 ? 4 : 8; }
+static int bk_for(int dtype) { return dtype == MIA_F32 ? 32 : 64; }
 
 }  // namespace mia
 
@@ -301,19 +366,27 @@ extern "C" int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream) {
   MIA_CHECK_ARG(a.x && a.w, "x and w are required");
   MIA_CHECK_ARG(a.N > 0 && a.H > 0 && a.W > 0 && a.Cin > 0 && a.Cout > 0, "bad shape");
   MIA_CHECK_ARG(dtype == MIA_F32 || dtype == MIA_F16 || dtype == MIA_BF16, "bad dtype");
-  MIA_CHECK_ARG(a.Cin % vec_for(dtype) == 0, "Cin must be a multiple of the 16-byte vector");
-  MIA_CHECK_ARG(a.Kpad % bk_for(dtype) == 0 && a.Kpad >= 9 * a.Cin, "Kpad must be mia_conv_kpad()");
+  const int vec = dtype == MIA_F32 ? 4 : 8;
+  MIA_CHECK_ARG(a.Cin >= vec && (a.Cin & (a.Cin - 1)) == 0,
+                "Cin must be a power of two ≥ the 16-byte vector");
+  MIA_CHECK_ARG(a.Kpad == mia_conv_kpad(a.Cin, dtype), "Kpad must be mia_conv_kpad()");
   MIA_CHECK_ARG(!a.shuffle_out || a.Cout % 4 == 0, "shuffle_out needs Cout % 4 == 0");
   MIA_CHECK_ARG(!a.sdot || a.aux_x, "sdot needs aux_x");
   MIA_CHECK_ARG(!a.tap_a || a.tap_t, "tap_a needs tap_t");
-  MIA_CHECK_ARG(!a.shuffle_out || !(a.tap_a || a.mask_a || a.sdot), "aux inputs need un-shuffled output");
-  MIA_CHECK_ARG((int64_t)a.N * a.H * a.W < (1LL << 31), "too many pixels");
+  MIA_CHECK_ARG(!a.shuffle_out || !(a.tap_a || a.mask_a || a.sdot),
+                "aux inputs need un-shuffled output");
+  MIA_CHECK_ARG((int64_t)a.N * a.H * a.W * a.Cin < (1LL << 31), "input too large for 32-bit offsets");
+  MIA_CHECK_ARG(a.in_scale == nullptr || a.Cin <= 2048, "modulated Cin ≤ 2048");
   ConvK k;
   k.a = a;
   k.M = a.N * a.H * a.W;
   k.HW = a.H * a.W;
   k.cout_mod = a.shuffle_out ? a.Cout / 4 : a.Cout;
   k.ystride = a.y_cstride > 0 ? a.y_cstride : k.cout_mod;
+  int lc = 0;
+  while ((1 << lc) < a.Cin) ++lc;
+  k.log2cin = lc;
+  k.n_first_max = std::min(a.N, (128 + k.HW - 1) / k.HW + 1);
   MIA_CHECK_ARG(k.ystride >= k.cout_mod, "y_cstride < Cout");
   hipStream_t st = (hipStream_t)stream;
   MIA_DISPATCH_DTYPE(dtype, T, return launch_conv<T>(k, st));

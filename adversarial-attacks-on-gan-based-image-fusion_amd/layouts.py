@@ -20,7 +20,7 @@ BLUR_F = (0.25, 0.75, 0.75, 0.25)
 
 
 def kpad_for(cin, dtype):
-    bk = 16 if dtype == torch.float32 else 32
+    bk = 32 if dtype == torch.float32 else 64
     return (9 * cin + bk - 1) // bk * bk
 
 

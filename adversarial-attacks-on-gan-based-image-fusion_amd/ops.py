@@ -52,7 +52,7 @@ def _numel_ok(t, n, dtype=None, name="tensor"):
 
 
 def conv_kpad(cin, dtype):
-    bk = 16 if dtype == torch.float32 else 32
+    bk = 32 if dtype == torch.float32 else 64
     return (9 * cin + bk - 1) // bk * bk
 
 

@@ -41,7 +41,7 @@ def test_fwd_and_dgrad_matrices():
 
 
 def test_kpad():
-    assert layouts.kpad_for(8, torch.float16) == 96 and layouts.kpad_for(8, torch.float32) == 80
+    assert layouts.kpad_for(8, torch.float16) == 128 and layouts.kpad_for(8, torch.float32) == 96
     assert layouts.kpad_for(512, torch.float16) == 4608
 
 
@@ -77,7 +77,7 @@ def test_library_exports_every_header_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert lib.mia_version() == 1
-    assert lib.mia_conv_kpad(8, 1) == 96  # host-only helper
+    assert lib.mia_conv_kpad(8, 1) == 128  # host-only helper
 
 
 def test_conv_args_struct_layout_matches_c(tmp_path):

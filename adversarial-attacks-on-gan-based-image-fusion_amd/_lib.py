@@ -45,6 +45,12 @@ SIGNATURES = {
                                       P]),
     "mia_vgg_conv_dgrad": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P,
                                    c_float, P, c_int, P]),
+    "mia_upconv_kpad": (c_int, [c_int, c_int, c_int]),
+    "mia_upconv_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, P]),
+    "mia_upconv_blur_fwd": (c_int, [P, P, P, P, c_float, P, c_int, c_int, c_int, c_int, P]),
+    "mia_upconv_blur_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P]),
+    "mia_upconv_dgrad": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, c_int,
+                                 P]),
     "mia_bias_act_fwd": (c_int, [P, P, c_float, P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_bias_act_bwd": (c_int, [P, P, P, c_float, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
                                  c_int, P]),

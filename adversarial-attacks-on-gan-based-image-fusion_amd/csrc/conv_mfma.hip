@@ -1,4 +1,4 @@
-// Implicit-GEMM 3x3 convolution on CDNA4 MFMA (gfx950), NHWC.
+// Implicit-GEMM convolution on CDNA4 MFMA (gfx950), NHWC.
 //
 // One kernel serves every dense contraction of the attack step:
 //   * VGG conv + bias + ReLU forward        (code/vgg.py:45-62)
@@ -7,25 +7,30 @@
 //                                             MFMA fragments, demodulation = per-(n,co) epilogue
 //                                             scale: one shared-weight GEMM, never N per-sample
 //                                             weight tensors)
-//   * up-sampling ModulatedConv2d [ext]      (conv_transpose2d(stride 2) ∘ Blur folded into four
-//                                             3x3 phase kernels on the low-res grid, pixel-shuffled
-//                                             in the epilogue)
-//   * ModulatedConv2d input/style gradient   (dgrad GEMM + Σ_p gx̃·x style reduction in the epilogue)
+//   * up-sampling ModulatedConv2d [ext]      conv_transpose2d(stride 2) as four sub-pixel phase
+//                                             GEMMs (2×2, 2×1, 1×2, 1×1 taps) in ONE launch, or the
+//                                             blur-folded 4-phase 3×3 variant (shuffle_out)
+//   * ModulatedConv2d input/style gradient   (dgrad GEMM, stride 1 or the stride-2 transposed-conv
+//                                             adjoint, + Σ_p gx̃·x style reduction in the epilogue)
 //
-// GEMM view: M = N·H·W output pixels, N-dim = Cout, K = 9·Cin (tap-major, channel-minor).
+// GEMM view per problem ("group"): M = N·Ho·Wo output pixels, N-dim = Cout,
+// K = KH·KW·Cin (tap-major, channel-minor). Input pixel of tap (ty,tx) for output (y,x) is
+// (s·y + ty − pad_y, s·x + tx − pad_x); the result lands at (ay·y + by, ax·x + bx).
 // Block tile BM×BN×BK, 256 threads = 4 waves (2×2), each wave FM×FN MFMA 16×16 fragments.
 //   f16/bf16: v_mfma_f32_16x16x32_{f16,bf16}, BK = 64;  f32: v_mfma_f32_16x16x4_f32, BK = 32.
-// Every tile row (one pixel's or one output channel's K-slice) is 128 B = 8 chunks of 16 B.
+// Every tile row (a pixel's or an output channel's K-slice) is 128 B = 8 chunks of 16 B.
 //
 // Staging: both operands go global → LDS by LDS-DMA (global_load_lds_dwordx4), a 2-stage ring:
 // the loads of K-step k+1 are issued before the MFMAs of step k and retired by the barrier at its
-// end. The im2col gather is done by the per-lane SOURCE address (one pixel row + tap offset);
-// lanes whose tap falls outside the image (or whose row is beyond M / Cout) read a 16-byte zero
-// vector instead, so the loop has no branches. LDS-DMA writes lane-linearly, so the bank
-// swizzle (chunk' = chunk ^ ((row>>1)&7), conflict-free for the ds_read_b128 fragment lane groups
-// on 128-B rows) is applied by permuting which chunk each lane fetches (guide rule 21).
-// The modulation prologue x̃ = act(x)·s[n][ci] is applied to A fragments after ds_read, with s
-// held in an LDS table for the (≤ 9) images a tile spans.
+// end. The im2col gather is the per-lane SOURCE address (one pixel row + tap offset); lanes whose
+// tap falls outside the input (or whose row is past M / Cout) read a 16-byte zero vector, so the
+// loop has no branches. For Cin ≥ BK the tap is uniform per K-step and each DMA costs one 64-bit
+// add. LDS-DMA writes lane-linearly, so the bank swizzle (chunk' = chunk ^ ((row>>1)&7),
+// conflict-free for the ds_read_b128 fragment lane groups on 128-B rows) is applied by permuting
+// which chunk each lane fetches (guide rule 21). The modulation prologue x̃ = act(x)·s[n][ci] is
+// applied to A fragments after ds_read, with s held in an LDS table for the (≤ 9) images a tile
+// spans. The epilogue stages the fp32 tile through LDS and then works on 8-channel vectors
+// (16-byte loads of every aux operand, 16-byte stores).
 #include <algorithm>
 #include <type_traits>
 
@@ -33,9 +38,15 @@
 
 namespace mia {
 
+struct ConvGroup {
+  const void* w;
+  int kpad, kh, kw, pad_y, pad_x, ho, wo, ay, by, ax, bx, blk0, nbm, m;
+};
+
 struct ConvK {
-  mia_conv_args a;
-  int M, HW, cout_mod, ystride, log2cin, n_first_max;
+  mia_conv_args a;  // x, y, N, H/W = INPUT dims, Cin, Cout and the epilogue fields
+  int stride, HT, WT, ystride, cout_mod, log2cin, n_first_max, ng, nblk, nbn;
+  ConvGroup g[4];
 };
 
 typedef const __attribute__((address_space(1))) void* gptr_t;
@@ -53,6 +64,10 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
 }
 
 __device__ __forceinline__ int fsw(int row) { return (row >> 1) & 7; }
+
+__device__ __forceinline__ int div_kw(int t, int kw) {
+  return kw == 3 ? (t * 11) >> 5 : (kw == 2 ? t >> 1 : t);  // exact for t < 9
+}
 
 template <typename T>
 __device__ __forceinline__ f32x4 mfma_chunk(const typename Vec<T>::type& a,
@@ -99,34 +114,75 @@ __device__ __forceinline__ void modulate(typename Vec<T>::type& v, const typenam
   }
 }
 
+// 8 consecutive elements of T as fp32
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const typename Vec<T>::type t = *(const typename Vec<T>::type*)p;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (float)t[e];
+  } else {
+    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[e + 4] = b[e]; }
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store8(T* p, const float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    typename Vec<T>::type t;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[e] = (T)v[e];
+    *(typename Vec<T>::type*)p = t;
+  } else {
+    *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+    *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+}
+__device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[e + 4] = b[e]; }
+}
+
 constexpr int ROWB = 128;  // bytes per tile row (one K-step slice)
 
-template <typename T, int BM, int BN, bool PRO>
-__global__ __launch_bounds__(256, 2) void conv3x3_kernel(const ConvK k) {
+template <int BM, int BN>
+constexpr int epi_stride() { return BN + 4; }  // fp32 words per staged row (bank-conflict pad)
+
+template <typename T, int BM, int BN, bool PRO, bool SMALLC>
+__global__ __launch_bounds__(256, 2) void conv_kernel(const ConvK k) {
   typedef typename Vec<T>::type VT;
   constexpr int VEC = Vec<T>::N;
   constexpr int BK = ROWB / (int)sizeof(T);
   constexpr int FM = BM / 32, FN = BN / 32;         // 2×2 waves
   constexpr int A_INS = BM / 32, B_INS = BN / 32;   // 1-KB DMA pieces per wave per K-step
   constexpr int STAGE = (BM + BN) * ROWB;
+  constexpr int ES = epi_stride<BM, BN>();
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const mia_conv_args& p = k.a;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int nbn = (p.Cout + BN - 1) / BN;
-  const int nbm = (k.M + BM - 1) / BM;
-  const int b = xcd_remap(blockIdx.x, nbm * nbn);
-  const int m0 = (b / nbn) * BM, n0 = (b % nbn) * BN;
-  const int H = p.H, W = p.W, Cin = p.Cin;
-  const int lc = k.log2cin;
+  const int bl = xcd_remap(blockIdx.x, k.nblk);
+  int gi = 0;
+#pragma unroll
+  for (int g = 1; g < 4; ++g)
+    if (g < k.ng && bl >= k.g[g].blk0) gi = g;
+  const ConvGroup& G = k.g[gi];
+  const int b = bl - G.blk0;
+  const int m0 = (b / k.nbn) * BM, n0 = (b % k.nbn) * BN;
+  const int Hin = p.H, Win = p.W, Cin = p.Cin;
+  const int HWo = G.ho * G.wo;
+  const int ntap = G.kh * G.kw;
 
   const T* __restrict__ X = (const T*)p.x;
-  const T* __restrict__ Wt = (const T*)p.w;
+  const T* __restrict__ Wt = (const T*)G.w;
   const T* zero = (const T*)g_zero16;
 
   // ---- per-lane DMA source state -----------------------------------------------------------
+  const T* a_ptr[A_INS];
   int a_base[A_INS], a_koff[A_INS], a_mask[A_INS];
 #pragma unroll
   for (int j = 0; j < A_INS; ++j) {
@@ -134,59 +190,77 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(const ConvK k) {
     a_koff[j] = ((lane & 7) ^ fsw(row)) * VEC;
     const int m = m0 + row;
     int msk = 0, base = 0;
-    if (m < k.M) {
-      const int n = m / k.HW;
-      const int rem = m - n * k.HW;
-      const int y = rem / W, x = rem - (rem / W) * W;
-      base = ((n * H + y) * W + x) * Cin;
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-        if (yy >= 0 && yy < H && xx >= 0 && xx < W) msk |= 1 << t;
+    if (m < G.m) {
+      const int n = m / HWo;
+      const int rem = m - n * HWo;
+      const int y = rem / G.wo, x = rem - (rem / G.wo) * G.wo;
+      const int iy0 = k.stride * y - G.pad_y, ix0 = k.stride * x - G.pad_x;
+      base = ((n * Hin + iy0) * Win + ix0) * Cin;
+      for (int t = 0; t < ntap; ++t) {
+        const int ty = div_kw(t, G.kw), tx = t - ty * G.kw;
+        const int yy = iy0 + ty, xx = ix0 + tx;
+        if (yy >= 0 && yy < Hin && xx >= 0 && xx < Win) msk |= 1 << t;
       }
     }
     a_base[j] = base;
     a_mask[j] = msk;
+    a_ptr[j] = X + base + a_koff[j];
   }
-  const T* b_src[B_INS];
+  const T* b_ptr[B_INS];
 #pragma unroll
   for (int j = 0; j < B_INS; ++j) {
     const int row = (wid * B_INS + j) * 8 + (lane >> 3);
     const int c = n0 + row;
-    b_src[j] = c < p.Cout ? Wt + (size_t)c * p.Kpad + ((lane & 7) ^ fsw(row)) * VEC : nullptr;
+    b_ptr[j] = c < p.Cout ? Wt + (size_t)c * G.kpad + ((lane & 7) ^ fsw(row)) * VEC : zero;
   }
+  const int b_inc = b_ptr[0] == zero ? 0 : BK;  // per-lane below (rows past Cout stay on zero)
+
+  // K-step state for the DMA issue (uniform across the block)
+  int is_tap = 0, is_cb = 0;
+  const int ncb = SMALLC ? 1 : Cin / BK;
 
   auto issue = [&](int kb, int st) {
     char* sa = smem + st * STAGE;
     char* sb = sa + BM * ROWB;
+    if constexpr (SMALLC) {
 #pragma unroll
-    for (int j = 0; j < A_INS; ++j) {
-      const int kk = kb * BK + a_koff[j];
-      const int tap = kk >> lc;
-      const int ci = kk & (Cin - 1);
-      const int dy = (tap * 11) >> 5;  // tap / 3 for tap < 9
-      const int dx = tap - 3 * dy;
-      const T* src = ((a_mask[j] >> tap) & 1)
-                         ? X + (a_base[j] + ((dy - 1) * W + (dx - 1)) * Cin + ci)
-                         : zero;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(sa + (wid * A_INS + j) * 1024), 16,
-                                       0, 0);
+      for (int j = 0; j < A_INS; ++j) {
+        const int kk = kb * BK + a_koff[j];
+        const int tap = kk >> k.log2cin;
+        const int ci = kk & (Cin - 1);
+        const int ty = div_kw(tap, G.kw), tx = tap - ty * G.kw;
+        const T* src = ((a_mask[j] >> tap) & 1) ? X + (a_base[j] + (ty * Win + tx) * Cin + ci)
+                                                 : zero;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(sa + (wid * A_INS + j) * 1024), 16,
+                                         0, 0);
+      }
+    } else {
+      const int ty = div_kw(is_tap, G.kw), tx = is_tap - ty * G.kw;
+      const int off = (ty * Win + tx) * Cin + is_cb * BK;  // uniform
+#pragma unroll
+      for (int j = 0; j < A_INS; ++j) {
+        const T* src = ((a_mask[j] >> is_tap) & 1) ? a_ptr[j] + off : zero;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(sa + (wid * A_INS + j) * 1024), 16,
+                                         0, 0);
+      }
+      if (++is_cb == ncb) { is_cb = 0; ++is_tap; }
     }
 #pragma unroll
     for (int j = 0; j < B_INS; ++j) {
-      const T* src = b_src[j] ? b_src[j] + (size_t)kb * BK : zero;
+      const T* src = b_ptr[j] == zero ? zero : b_ptr[j] + (size_t)kb * BK;
       __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(sb + (wid * B_INS + j) * 1024), 16,
                                        0, 0);
     }
   };
+  (void)b_inc;
 
   // ---- modulation table (PRO): s[n][ci] (·√2 for lrelu inputs) for the images of this tile ----
-  const int n_first = m0 / k.HW;
+  const int n_first = m0 / HWo;
   T* stab = (T*)(smem + 2 * STAGE);
   const bool lrelu_in = p.act_in == MIA_ACT_LRELU_S2;
   int a_nl[FM];
   if constexpr (PRO) {
-    const int n_last = (min(m0 + BM, k.M) - 1) / k.HW;
+    const int n_last = (min(m0 + BM, G.m) - 1) / HWo;
     const int cnt = (n_last - n_first + 1) * Cin;
     const float mul = lrelu_in ? SQRT2 : 1.f;
     for (int i = tid; i < cnt; i += 256) {
@@ -195,8 +269,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(const ConvK k) {
     }
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const int m = min(m0 + wm * FM * 16 + 16 * i + (lane & 15), k.M - 1);
-      a_nl[i] = (m / k.HW - n_first) * Cin;
+      const int m = min(m0 + wm * FM * 16 + 16 * i + (lane & 15), G.m - 1);
+      a_nl[i] = (m / HWo - n_first) * Cin;
     }
   }
 
@@ -206,7 +280,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(const ConvK k) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = p.Kpad / BK;
+  const int nk = G.kpad / BK;
   issue(0, 0);
   __syncthreads();
   const int frow = lane & 15, fq = lane >> 4;
@@ -245,87 +319,142 @@ __global__ __launch_bounds__(256, 2) void conv3x3_kernel(const ConvK k) {
     __syncthreads();  // retires the DMA of step kb+1 (vmcnt(0)) and frees stage st for kb+2
   }
 
-  // ---- epilogue ---------------------------------------------------------------------------
-  const int Cout = p.Cout;
-  const int row_base = m0 + wm * FM * 16 + fq * 4;
-  const int col_base = n0 + wn * FN * 16 + frow;
-
-  if (p.sdot) {
-    const T* AX = (const T*)p.aux_x;
-    const int last = min(m0 + BM, k.M) - 1;
-    const bool single = (m0 / k.HW) == (last / k.HW);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int col = col_base + 16 * j;
-      float part = 0.f;
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = row_base + 16 * i + r;
-          if (row < k.M && col < Cout) {
-            const float xv = apply_act(to_f(AX[(size_t)row * Cout + col]), p.act_aux);
-            const float c = acc[i][j][r] * xv;
-            if (single) part += c;
-            else atomicAdd(&p.sdot[(size_t)(row / k.HW) * Cout + col], c);
-          }
-        }
-      if (single) {
-        part += __shfl_xor(part, 16, 64);
-        part += __shfl_xor(part, 32, 64);
-        if (fq == 0 && col < Cout) atomicAdd(&p.sdot[(size_t)(m0 / k.HW) * Cout + col], part);
-      }
-    }
-  }
-  if (!p.y) return;
-
-  T* __restrict__ Y = (T*)p.y;
-  const T* TA = (const T*)p.tap_a;
-  const T* TT = (const T*)p.tap_t;
-  const T* MA = (const T*)p.mask_a;
-  const int Ho = p.shuffle_out ? 2 * H : H, Wo = p.shuffle_out ? 2 * W : W;
+  // ---- epilogue: stage the fp32 tile in LDS, then 8-channel vectors -------------------------
+  float* tile = (float*)smem;
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = row_base + 16 * i + r;
-      if (row >= k.M) continue;
-      const int n = row / k.HW;
-      const int pix = row - n * k.HW;
-      const int y = pix / W, x = pix - (pix / W) * W;
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int col = col_base + 16 * j;
-        if (col >= Cout) continue;
-        int cm = col, yo = y, xo = x;
-        if (p.shuffle_out) {
-          const int ph = col / k.cout_mod;
-          cm = col - ph * k.cout_mod;
-          yo = 2 * y + (ph >> 1);
-          xo = 2 * x + (ph & 1);
-        }
-        const size_t off = ((size_t)(n * Ho + yo) * Wo + xo) * k.ystride + cm;
-        const size_t aoff = (size_t)row * Cout + col;
-        float v = acc[i][j][r];
-        if (p.out_scale) v *= p.out_scale[(size_t)n * k.cout_mod + cm];
-        if (p.noise) v += p.noise_w * p.noise[yo * Wo + xo];
-        if (p.bias) v += p.bias[cm];
-        if (TA) v += p.tap_coef * (to_f(TA[aoff]) - to_f(TT[aoff]));
-        if (MA && !(to_f(MA[aoff]) > 0.f)) v = 0.f;
-        v = apply_act(v, p.act_out);
-        if (p.accumulate) v += to_f(Y[off]);
-        Y[off] = from_f<T>(v);
+      for (int r = 0; r < 4; ++r)
+        tile[(wm * FM * 16 + 16 * i + fq * 4 + r) * ES + wn * FN * 16 + 16 * j + frow] =
+            acc[i][j][r];
+  __syncthreads();
+
+  const int Cout = p.Cout;
+  constexpr int CPR = BN / 8;          // 8-channel chunks per row
+  constexpr int RPP = 256 / CPR;       // rows per pass
+  const int cc = tid % CPR, r0 = tid / CPR;
+  const int col = n0 + cc * 8;
+  const bool col_ok = col < Cout;      // Cout % 8 == 0 (host check)
+  const T* AX = (const T*)p.aux_x;
+  const T* TA = (const T*)p.tap_a;
+  const T* TT = (const T*)p.tap_t;
+  const T* MA = (const T*)p.mask_a;
+  T* __restrict__ Y = (T*)p.y;
+  const int last = min(m0 + BM, G.m) - 1;
+  const bool single = (m0 / HWo) == (last / HWo);
+  float part[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[e] = 0.f;
+
+  for (int rr = r0; rr < BM; rr += RPP) {
+    const int row = m0 + rr;
+    if (row >= G.m || !col_ok) continue;
+    float v[8];
+    load8f(tile + rr * ES + cc * 8, v);
+    const size_t aoff = (size_t)row * Cout + col;
+    if (p.sdot) {
+      float xv[8];
+      load8<T>(AX + aoff, xv);
+      const int n = row / HWo;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float c = v[e] * apply_act(xv[e], p.act_aux);
+        if (single) part[e] += c;
+        else atomicAdd(&p.sdot[(size_t)n * Cout + col + e], c);
       }
     }
+    if (!Y) continue;
+    const int n = row / HWo;
+    const int pix = row - n * HWo;
+    const int y = pix / G.wo, x = pix - (pix / G.wo) * G.wo;
+    int cm = col, yo, xo;
+    if (p.shuffle_out) {
+      const int ph = col / k.cout_mod;
+      cm = col - ph * k.cout_mod;
+      yo = 2 * y + (ph >> 1);
+      xo = 2 * x + (ph & 1);
+    } else {
+      yo = G.ay * y + G.by;
+      xo = G.ax * x + G.bx;
+    }
+    const size_t off = ((size_t)(n * k.HT + yo) * k.WT + xo) * k.ystride + cm;
+    if (p.out_scale) {
+      float s[8];
+      load8f(p.out_scale + (size_t)n * k.cout_mod + cm, s);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= s[e];
+    }
+    if (p.noise) {
+      const float nz = p.noise_w * p.noise[yo * k.WT + xo];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += nz;
+    }
+    if (p.bias) {
+      float bb[8];
+      load8f(p.bias + cm, bb);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += bb[e];
+    }
+    if (TA) {
+      float ta[8], tt[8];
+      load8<T>(TA + aoff, ta);
+      load8<T>(TT + aoff, tt);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += p.tap_coef * (ta[e] - tt[e]);
+    }
+    if (MA) {
+      float ma[8];
+      load8<T>(MA + aoff, ma);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = ma[e] > 0.f ? v[e] : 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], p.act_out);
+    if (p.accumulate) {
+      float yo8[8];
+      load8<T>(Y + off, yo8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += yo8[e];
+    }
+    store8<T>(Y + off, v);
+  }
+
+  if (p.sdot && single) {
+    // reduce the per-thread partial sums of equal channel chunks: lanes cc, cc+CPR, … of a wave
+    // by shuffles, then the waves through LDS, one atomic per channel per block
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      for (int o = CPR; o < 64; o <<= 1) part[e] += __shfl_xor(part[e], o, 64);
+    __syncthreads();
+    float* red = (float*)smem;  // [4 waves][BN]
+    if (lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[wid * BN + lane * 8 + e] = part[e];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < Cout) {
+      const float s = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
+      atomicAdd(&p.sdot[(size_t)(m0 / HWo) * Cout + n0 + tid], s);
+    }
+  }
 }
 
-template <typename T, int BM, int BN, bool PRO>
-static int launch_tile(const ConvK& k, hipStream_t st) {
-  const int nbm = (k.M + BM - 1) / BM, nbn = (k.a.Cout + BN - 1) / BN;
-  const int nblk = nbm * nbn;
+template <typename T, int BM, int BN, bool PRO, bool SMALLC>
+static int launch_tile(ConvK& k, hipStream_t st) {
+  k.nbn = (k.a.Cout + BN - 1) / BN;
+  int blk = 0;
+  for (int g = 0; g < k.ng; ++g) {
+    k.g[g].nbm = (k.g[g].m + BM - 1) / BM;
+    k.g[g].blk0 = blk;
+    blk += k.g[g].nbm * k.nbn;
+  }
+  k.nblk = blk;
   size_t lds = 2 * (BM + BN) * ROWB;
   if (PRO) lds += (size_t)k.n_first_max * k.a.Cin * sizeof(T);
-  auto fn = conv3x3_kernel<T, BM, BN, PRO>;
+  lds = std::max(lds, (size_t)BM * epi_stride<BM, BN>() * 4);
+  auto fn = conv_kernel<T, BM, BN, PRO, SMALLC>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -333,64 +462,159 @@ static int launch_tile(const ConvK& k, hipStream_t st) {
       return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     attr_set = true;
   }
-  hipLaunchKernelGGL(fn, dim3(nblk), dim3(256), lds, st, k);
-  return check_launch("conv3x3");
+  hipLaunchKernelGGL(fn, dim3(blk), dim3(256), lds, st, k);
+  return check_launch("conv");
 }
 
-template <typename T, bool PRO>
-static int launch_bn(const ConvK& k, hipStream_t st) {
-  if (k.a.Cout <= 64) return launch_tile<T, 128, 64, PRO>(k, st);
-  return launch_tile<T, 128, 128, PRO>(k, st);
+template <typename T, bool PRO, bool SMALLC>
+static int launch_bn(ConvK& k, hipStream_t st) {
+  if (k.a.Cout <= 64) return launch_tile<T, 128, 64, PRO, SMALLC>(k, st);
+  return launch_tile<T, 128, 128, PRO, SMALLC>(k, st);
 }
 
 template <typename T>
-static int launch_conv(const ConvK& k, hipStream_t st) {
+static int launch_conv(ConvK& k, hipStream_t st) {
   const bool pro = k.a.in_scale != nullptr || k.a.act_in != MIA_ACT_NONE;
-  return pro ? launch_bn<T, true>(k, st) : launch_bn<T, false>(k, st);
+  const bool small = k.a.Cin < ROWB / (int)sizeof(T);
+  if (pro) return small ? launch_bn<T, true, true>(k, st) : launch_bn<T, true, false>(k, st);
+  return small ? launch_bn<T, false, true>(k, st) : launch_bn<T, false, false>(k, st);
 }
 
 static int bk_for(int dtype) { return dtype == MIA_F32 ? 32 : 64; }
 
-}  // namespace mia
-
-using namespace mia;
-
-extern "C" int mia_conv_kpad(int cin, int dtype) {
+static int kpad_for(int k, int dtype) {
   const int bk = bk_for(dtype);
-  return (9 * cin + bk - 1) / bk * bk;
+  return (k + bk - 1) / bk * bk;
 }
 
-extern "C" int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream) {
-  MIA_CHECK_ARG(args != nullptr, "null args");
-  const mia_conv_args& a = *args;
-  MIA_CHECK_ARG(a.x && a.w, "x and w are required");
+// Shared validation + dispatch for a filled ConvK (groups set up by the caller).
+static int run_conv(ConvK& k, int dtype, hipStream_t st) {
+  const mia_conv_args& a = k.a;
+  MIA_CHECK_ARG(a.x, "x is required");
   MIA_CHECK_ARG(a.N > 0 && a.H > 0 && a.W > 0 && a.Cin > 0 && a.Cout > 0, "bad shape");
   MIA_CHECK_ARG(dtype == MIA_F32 || dtype == MIA_F16 || dtype == MIA_BF16, "bad dtype");
   const int vec = dtype == MIA_F32 ? 4 : 8;
   MIA_CHECK_ARG(a.Cin >= vec && (a.Cin & (a.Cin - 1)) == 0,
                 "Cin must be a power of two ≥ the 16-byte vector");
-  MIA_CHECK_ARG(a.Kpad == mia_conv_kpad(a.Cin, dtype), "Kpad must be mia_conv_kpad()");
-  MIA_CHECK_ARG(!a.shuffle_out || a.Cout % 4 == 0, "shuffle_out needs Cout % 4 == 0");
+  MIA_CHECK_ARG(a.Cout % 8 == 0, "Cout must be a multiple of 8");
+  MIA_CHECK_ARG(!a.shuffle_out || (a.Cout % 32 == 0 && k.ng == 1), "shuffle_out: Cout % 32, 1 group");
   MIA_CHECK_ARG(!a.sdot || a.aux_x, "sdot needs aux_x");
   MIA_CHECK_ARG(!a.tap_a || a.tap_t, "tap_a needs tap_t");
   MIA_CHECK_ARG(!a.shuffle_out || !(a.tap_a || a.mask_a || a.sdot),
                 "aux inputs need un-shuffled output");
   MIA_CHECK_ARG((int64_t)a.N * a.H * a.W * a.Cin < (1LL << 31), "input too large for 32-bit offsets");
   MIA_CHECK_ARG(a.in_scale == nullptr || a.Cin <= 2048, "modulated Cin ≤ 2048");
-  ConvK k;
-  k.a = a;
-  k.M = a.N * a.H * a.W;
-  k.HW = a.H * a.W;
-  k.cout_mod = a.shuffle_out ? a.Cout / 4 : a.Cout;
-  k.ystride = a.y_cstride > 0 ? a.y_cstride : k.cout_mod;
+  MIA_CHECK_ARG(k.ng >= 1 && k.ng <= 4, "1..4 groups");
+  for (int g = 0; g < k.ng; ++g) {
+    const ConvGroup& G = k.g[g];
+    MIA_CHECK_ARG(G.w, "w is required");
+    MIA_CHECK_ARG(G.kh >= 1 && G.kh <= 3 && G.kw >= 1 && G.kw <= 3, "taps 1..3");
+    MIA_CHECK_ARG(G.kpad == kpad_for(G.kh * G.kw * a.Cin, dtype), "Kpad must be mia_conv_kpad()");
+    MIA_CHECK_ARG(G.ho > 0 && G.wo > 0, "empty output grid");
+    MIA_CHECK_ARG((int64_t)a.N * G.ho * G.wo < (1LL << 31), "too many pixels");
+    MIA_CHECK_ARG(!(a.sdot || a.tap_a || a.mask_a) || (k.ng == 1 && G.ho * G.wo == k.HT * k.WT),
+                  "aux operands need one group with an identity output placement");
+  }
   int lc = 0;
   while ((1 << lc) < a.Cin) ++lc;
   k.log2cin = lc;
-  k.n_first_max = std::min(a.N, (128 + k.HW - 1) / k.HW + 1);
-  MIA_CHECK_ARG(k.ystride >= k.cout_mod, "y_cstride < Cout");
-  hipStream_t st = (hipStream_t)stream;
+  int hw_min = 1 << 30;
+  for (int g = 0; g < k.ng; ++g) hw_min = std::min(hw_min, k.g[g].ho * k.g[g].wo);
+  k.n_first_max = std::min(a.N, (128 + hw_min - 1) / hw_min + 1);
   MIA_DISPATCH_DTYPE(dtype, T, return launch_conv<T>(k, st));
   return MIA_OK;
+}
+
+}  // namespace mia
+
+using namespace mia;
+
+extern "C" int mia_conv_kpad(int cin, int dtype) { return kpad_for(9 * cin, dtype); }
+
+extern "C" int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream) {
+  MIA_CHECK_ARG(args != nullptr, "null args");
+  const mia_conv_args& a = *args;
+  ConvK k = {};
+  k.a = a;
+  k.stride = 1;
+  k.ng = 1;
+  ConvGroup& G = k.g[0];
+  G.w = a.w;
+  G.kpad = a.Kpad;
+  G.kh = G.kw = 3;
+  G.pad_y = G.pad_x = 1;
+  G.ho = a.H;
+  G.wo = a.W;
+  G.ay = G.ax = 1;
+  G.m = a.N * a.H * a.W;
+  k.HT = a.shuffle_out ? 2 * a.H : a.H;
+  k.WT = a.shuffle_out ? 2 * a.W : a.W;
+  k.cout_mod = a.shuffle_out ? a.Cout / 4 : a.Cout;
+  k.ystride = a.y_cstride > 0 ? a.y_cstride : k.cout_mod;
+  MIA_CHECK_ARG(k.ystride >= k.cout_mod, "y_cstride < Cout");
+  return run_conv(k, dtype, (hipStream_t)stream);
+}
+
+extern "C" int mia_upconv_kpad(int cin, int phase, int dtype) {
+  const int kh = 2 - (phase >> 1), kw = 2 - (phase & 1);
+  return kpad_for(kh * kw * cin, dtype);
+}
+
+extern "C" int mia_upconv_fwd(const void* x, const void* const* w_phase, void* t_out, int N,
+                              int R, int Cin, int Cout, int act_in, const float* style, int dtype,
+                              void* stream) {
+  MIA_CHECK_ARG(w_phase && t_out, "bad args");
+  mia_conv_args a = {};
+  a.x = x; a.y = t_out; a.N = N; a.H = R; a.W = R; a.Cin = Cin; a.Cout = Cout;
+  a.act_in = act_in; a.in_scale = style;
+  ConvK k = {};
+  k.a = a;
+  k.stride = 1;
+  k.ng = 4;
+  k.HT = k.WT = 2 * R + 1;
+  k.cout_mod = Cout;
+  k.ystride = Cout;
+  for (int ph = 0; ph < 4; ++ph) {
+    const int py = ph >> 1, px = ph & 1;
+    ConvGroup& G = k.g[ph];
+    G.w = w_phase[ph];
+    G.kh = 2 - py;
+    G.kw = 2 - px;
+    G.kpad = kpad_for(G.kh * G.kw * Cin, dtype);
+    G.pad_y = G.kh - 1;
+    G.pad_x = G.kw - 1;
+    G.ho = R + 1 - py;
+    G.wo = R + 1 - px;
+    G.ay = G.ax = 2;
+    G.by = py;
+    G.bx = px;
+    G.m = N * G.ho * G.wo;
+  }
+  return run_conv(k, dtype, (hipStream_t)stream);
+}
+
+extern "C" int mia_upconv_dgrad(const void* g_t, const void* w_t, void* gx, int N, int R, int Cout,
+                                int Cin, const void* x_fwd, int act_x, const float* style,
+                                float* sdot, int dtype, void* stream) {
+  mia_conv_args a = {};
+  a.x = g_t; a.y = gx; a.N = N; a.H = 2 * R + 1; a.W = 2 * R + 1; a.Cin = Cout; a.Cout = Cin;
+  a.out_scale = style; a.aux_x = x_fwd; a.act_aux = act_x; a.sdot = sdot;
+  ConvK k = {};
+  k.a = a;
+  k.stride = 2;
+  k.ng = 1;
+  ConvGroup& G = k.g[0];
+  G.w = w_t;
+  G.kh = G.kw = 3;
+  G.kpad = kpad_for(9 * Cout, dtype);
+  G.pad_y = G.pad_x = 0;
+  G.ho = G.wo = R;
+  G.ay = G.ax = 1;
+  G.m = N * R * R;
+  k.HT = k.WT = R;
+  k.cout_mod = Cin;
+  k.ystride = Cin;
+  return run_conv(k, dtype, (hipStream_t)stream);
 }
 
 extern "C" int mia_modconv_fwd(const void* x, const void* w, void* pre, int N, int H, int W,

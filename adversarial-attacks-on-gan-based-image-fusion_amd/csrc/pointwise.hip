@@ -101,6 +101,93 @@ __global__ void bias_act_bwd_kernel(const T* __restrict__ g_a, const T* __restri
 }
 
 // ---------------------------------------------------------------------------------------------
+// Blur of the up-sampling StyledConv (rosinality Blur: upfirdn2d, k = [1,3,3,1]⊗[1,3,3,1]/64·4,
+// pad (1,1)) applied to the transposed-conv output T (N, 2R+1, 2R+1, C), fused with the
+// demodulation scale, noise injection and bias: pre = demod·blur(T) + nw·noise + b.
+__constant__ float kBlur4[4] = {0.25f, 0.75f, 0.75f, 0.25f};
+
+template <typename T>
+__global__ void upconv_blur_fwd_kernel(const T* __restrict__ t, T* __restrict__ pre,
+                                       const float* __restrict__ demod,
+                                       const float* __restrict__ noise, float nw,
+                                       const float* __restrict__ bias, int N, int R, int C) {
+  typedef typename Vec<T>::type VT;
+  constexpr int V = Vec<T>::N;
+  const int S = 2 * R, TS = 2 * R + 1, nc = C / V;
+  const int64_t total = (int64_t)N * S * S * nc;
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
+    const int cv = (int)(i % nc);
+    const int64_t pix = i / nc;
+    const int ox = (int)(pix % S);
+    const int oy = (int)((pix / S) % S);
+    const int n = (int)(pix / ((int64_t)S * S));
+    float acc[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int jy = 0; jy < 4; ++jy) {
+      const int ty = oy + jy - 1;
+      if (ty < 0 || ty >= TS) continue;
+#pragma unroll
+      for (int jx = 0; jx < 4; ++jx) {
+        const int tx = ox + jx - 1;
+        if (tx < 0 || tx >= TS) continue;
+        const VT v = *(const VT*)(t + (((size_t)n * TS + ty) * TS + tx) * C + cv * V);
+        const float w = kBlur4[jy] * kBlur4[jx];
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] += w * to_f(v[e]);
+      }
+    }
+    const float nz = noise ? nw * noise[oy * S + ox] : 0.f;
+    VT o;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int c = cv * V + e;
+      o[e] = from_f<T>(acc[e] * demod[(size_t)n * C + c] + nz + (bias ? bias[c] : 0.f));
+    }
+    *(VT*)(pre + pix * C + cv * V) = o;
+  }
+}
+
+// Adjoint of the blur: gT[t] = Σ_j f[j]·gy[t − j + 1] per axis (gy = demod-scaled ∂L/∂pre).
+template <typename T>
+__global__ void upconv_blur_bwd_kernel(const T* __restrict__ gy, T* __restrict__ gt, int N, int R,
+                                       int C) {
+  typedef typename Vec<T>::type VT;
+  constexpr int V = Vec<T>::N;
+  const int S = 2 * R, TS = 2 * R + 1, nc = C / V;
+  const int64_t total = (int64_t)N * TS * TS * nc;
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
+    const int cv = (int)(i % nc);
+    const int64_t pix = i / nc;
+    const int tx = (int)(pix % TS);
+    const int ty = (int)((pix / TS) % TS);
+    const int n = (int)(pix / ((int64_t)TS * TS));
+    float acc[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int jy = 0; jy < 4; ++jy) {
+      const int oy = ty - jy + 1;
+      if (oy < 0 || oy >= S) continue;
+#pragma unroll
+      for (int jx = 0; jx < 4; ++jx) {
+        const int ox = tx - jx + 1;
+        if (ox < 0 || ox >= S) continue;
+        const VT v = *(const VT*)(gy + (((size_t)n * S + oy) * S + ox) * C + cv * V);
+        const float w = kBlur4[jy] * kBlur4[jx];
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] += w * to_f(v[e]);
+      }
+    }
+    VT o;
+#pragma unroll
+    for (int e = 0; e < V; ++e) o[e] = from_f<T>(acc[e]);
+    *(VT*)(gt + pix * C + cv * V) = o;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // upfirdn2d on fp32 NCHW planes with a separable kernel (rosinality op/upfirdn2d semantics).
 __device__ __forceinline__ float upfir_at(const float* __restrict__ x, int H, int W, int oy, int ox,
                                           const float* kf, int kt, int up, int down, int pad0) {
@@ -611,6 +698,31 @@ extern "C" int mia_bias_act_bwd(const void* g_a, const void* pre, const float* n
   MIA_DISPATCH_DTYPE(dtype, T,
       MIA_LAUNCH(bias_act_bwd_kernel<T>, grid, dim3(TPB), 0, (const T*)g_a, (const T*)pre, noise,
                  noise_w, bias, demod, (T*)gy, q, H, W, C, unshuffle, ppb));
+  return MIA_OK;
+}
+
+extern "C" int mia_upconv_blur_fwd(const void* t, void* pre, const float* demod,
+                                   const float* noise, float noise_w, const float* bias, int N,
+                                   int R, int C, int dtype, void* stream) {
+  MIA_CHECK_ARG(t && pre && demod && N > 0 && R > 0, "bad args");
+  const int V = dtype == MIA_F32 ? 4 : 8;
+  MIA_CHECK_ARG(C % V == 0, "C must be a multiple of the vector width");
+  const int64_t total = (int64_t)N * 4 * R * R * (C / V);
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH(upconv_blur_fwd_kernel<T>, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0,
+                 (const T*)t, (T*)pre, demod, noise, noise_w, bias, N, R, C));
+  return MIA_OK;
+}
+
+extern "C" int mia_upconv_blur_bwd(const void* gy, void* gt, int N, int R, int C, int dtype,
+                                   void* stream) {
+  MIA_CHECK_ARG(gy && gt && N > 0 && R > 0, "bad args");
+  const int V = dtype == MIA_F32 ? 4 : 8;
+  MIA_CHECK_ARG(C % V == 0, "C must be a multiple of the vector width");
+  const int64_t total = (int64_t)N * (2 * R + 1) * (2 * R + 1) * (C / V);
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH(upconv_blur_bwd_kernel<T>, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0,
+                 (const T*)gy, (T*)gt, N, R, C));
   return MIA_OK;
 }
 

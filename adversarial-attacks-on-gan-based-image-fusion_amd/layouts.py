@@ -45,6 +45,34 @@ def dgrad_matrix(w, dtype, cin_pad=None):
     return fwd_matrix(wt, dtype)
 
 
+def upconv_subpixel_matrices(w, dtype):
+    """conv_transpose2d(stride 2) as four sub-pixel phase GEMMs: T[2m+p] = Σ_j x[m−j]·W[p+2j].
+    Phase (py,px) has kh = 2−py, kw = 2−px taps; as a window conv with input m + ty − (kh−1),
+    tap (ty,tx) ↔ W[py + 2(kh−1−ty)][px + 2(kw−1−tx)]. Returns 4 [Cout][Kpad] matrices."""
+    cout, cin = w.shape[:2]
+    w = w.double()
+    out = []
+    for ph in range(4):
+        py, px = ph >> 1, ph & 1
+        kh, kw = 2 - py, 2 - px
+        m = torch.zeros(cout, kh, kw, cin, dtype=torch.float64)
+        for ty in range(kh):
+            for tx in range(kw):
+                m[:, ty, tx, :] = w[:, :, py + 2 * (kh - 1 - ty), px + 2 * (kw - 1 - tx)]
+        bk = 32 if dtype == torch.float32 else 64
+        kp = (kh * kw * cin + bk - 1) // bk * bk
+        full = torch.zeros(cout, kp, dtype=torch.float64)
+        full[:, :kh * kw * cin] = m.reshape(cout, -1)
+        out.append(full.to(dtype))
+    return out
+
+
+def upconv_dgrad_matrix(w, dtype):
+    """Input gradient of conv_transpose2d(stride 2): gx[i] = Σ_k gT[2i+k]·W[k] — a stride-2 3×3
+    conv with Wd[ci][(ky·3+kx)·Cout + co] = W[co][ci][ky][kx] (no flip)."""
+    return fwd_matrix(w.double().transpose(0, 1), dtype)
+
+
 def upconv_phases(w):
     """(Cout, Cin, 3, 3) → (4·Cout, Cin, 3, 3) phase kernels, row index = (2·py+px)·Cout + co."""
     cout, cin = w.shape[:2]

@@ -114,6 +114,80 @@ def conv3x3(x, w, y, *, cout, act_in=ACT_NONE, in_scale=None, out_scale=None, bi
     return y
 
 
+def _prof_call(name, flops, *args):
+    prof = PROFILE
+    if prof is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    call(name, *args)
+    if prof is not None:
+        e1.record()
+        prof.append((e0, e1, flops))
+
+
+def upconv_kpad(cin, phase, dtype):
+    kh, kw = 2 - (phase >> 1), 2 - (phase & 1)
+    bk = 32 if dtype == torch.float32 else 64
+    return (kh * kw * cin + bk - 1) // bk * bk
+
+
+def upconv_fwd(x, w_phases, t_out, cout, act_in=ACT_NONE, style=None, flops=None):
+    """conv_transpose2d(stride 2) as 4 sub-pixel phase GEMMs (one launch). x: (N,R,R,Cin) →
+    T: (N, 2R+1, 2R+1, Cout)."""
+    N, R, R2, Cin = x.shape
+    T = x.dtype
+    if R != R2:
+        raise ValueError("square inputs only")
+    if len(w_phases) != 4:
+        raise ValueError("4 phase weight matrices required")
+    for ph, w in enumerate(w_phases):
+        _need(w, (cout, upconv_kpad(Cin, ph, T)), T, f"w_phase[{ph}]")
+    _need(t_out, (N, 2 * R + 1, 2 * R + 1, cout), T, "t_out")
+    _numel_ok(style, N * Cin, torch.float32, "style")
+    wp = (ctypes.c_void_p * 4)(*[w.data_ptr() for w in w_phases])
+    for w in w_phases:
+        ptr(w)
+    _prof_call("mia_upconv_fwd", flops if flops is not None else 2 * N * R * R * 9 * Cin * cout,
+               ptr(x), wp, ptr(t_out), N, R, Cin, cout, act_in, ptr(style), dt(T), stream())
+    return t_out
+
+
+def upconv_blur_fwd(t, pre, demod, noise, noise_w, bias):
+    N, TS, _, C = t.shape
+    R = (TS - 1) // 2
+    _need(pre, (N, 2 * R, 2 * R, C), t.dtype, "pre")
+    _numel_ok(demod, N * C, torch.float32, "demod")
+    _numel_ok(noise, 4 * R * R, torch.float32, "noise")
+    _numel_ok(bias, C, torch.float32, "bias")
+    call("mia_upconv_blur_fwd", ptr(t), ptr(pre), ptr(demod), ptr(noise), float(noise_w),
+         ptr(bias), N, R, C, dt(t), stream())
+    return pre
+
+
+def upconv_blur_bwd(gy, gt):
+    N, S, _, C = gy.shape
+    R = S // 2
+    _need(gt, (N, 2 * R + 1, 2 * R + 1, C), gy.dtype, "gt")
+    call("mia_upconv_blur_bwd", ptr(gy), ptr(gt), N, R, C, dt(gy), stream())
+    return gt
+
+
+def upconv_dgrad(g_t, w_t, gx, cin, x_fwd, act_x, style, sdot, flops=None):
+    N, TS, _, Cout = g_t.shape
+    R = (TS - 1) // 2
+    T = g_t.dtype
+    _need(w_t, (cin, conv_kpad(Cout, T)), T, "w_t")
+    if gx is not None:
+        _need(gx, (N, R, R, cin), T, "gx")
+    _need(x_fwd, (N, R, R, cin), T, "x_fwd")
+    _numel_ok(style, N * cin, torch.float32, "style")
+    _numel_ok(sdot, N * cin, torch.float32, "sdot")
+    _prof_call("mia_upconv_dgrad", flops if flops is not None else 2 * N * R * R * 9 * Cout * cin,
+               ptr(g_t), ptr(w_t), ptr(gx), N, R, Cout, cin, ptr(x_fwd), act_x, ptr(style),
+               ptr(sdot), dt(T), stream())
+    return gx
+
+
 def bias_act_fwd(x, noise, noise_w, bias, y):
     N, H, W, C = x.shape
     _need(y, x.shape, x.dtype, "y")

@@ -28,7 +28,11 @@ UP_K = list(layouts.BLUR_F)  # separable ToRGB skip up-sampler (Upsample(blur_ke
 
 
 class SynthesisNet:
-    def __init__(self, params, size, dtype=torch.float32, device="cuda", channel_multiplier=2):
+    def __init__(self, params, size, dtype=torch.float32, device="cuda", channel_multiplier=2,
+                 up_mode="subpixel"):
+        if up_mode not in ("subpixel", "fused"):
+            raise ValueError("up_mode: 'subpixel' (convT phases + blur) or 'fused' (4-phase 3×3)")
+        self.up_mode = up_mode
         self.size = int(size)
         self.n_latent = n_latent_for(self.size)
         self.dtype = dtype
@@ -49,7 +53,11 @@ class SynthesisNet:
             scale = 1.0 / math.sqrt(cin * 9)
             ws = w * scale
             L = dict(c)
-            if c["up"]:
+            if c["up"] and up_mode == "subpixel":
+                L["wph"] = [m.contiguous().to(dev)
+                            for m in layouts.upconv_subpixel_matrices(ws, dtype)]
+                L["wd"] = layouts.upconv_dgrad_matrix(ws, dtype).contiguous().to(dev)
+            elif c["up"]:
                 ph = layouts.upconv_phases(ws)
                 L["wf"] = layouts.fwd_matrix(ph, dtype).contiguous().to(dev)
                 L["wd"] = layouts.dgrad_matrix(ph, dtype).contiguous().to(dev)
@@ -115,10 +123,16 @@ class SynthesisNet:
         for i, L in enumerate(self.convs):
             r, cout = L["res"], L["cout"]
             pre = ws.get(f"g.pre{i}", (N, r, r, cout), T)
-            ops.conv3x3(x, L["wf"], pre, cout=4 * cout if L["up"] else cout, act_in=act,
-                        in_scale=L["_s"], out_scale=L["_d"], noise=L["noise"],
-                        noise_w=L["noise_w"], bias=L["bias"], shuffle_out=L["up"],
-                        flops=self._alg_flops(L, N))
+            if L["up"] and self.up_mode == "subpixel":
+                t = ws.get(f"g.t{i}", (N, r + 1, r + 1, cout), T)
+                ops.upconv_fwd(x, L["wph"], t, cout, act_in=act, style=L["_s"],
+                               flops=self._alg_flops(L, N))
+                ops.upconv_blur_fwd(t, pre, L["_d"], L["noise"], L["noise_w"], L["bias"])
+            else:
+                ops.conv3x3(x, L["wf"], pre, cout=4 * cout if L["up"] else cout, act_in=act,
+                            in_scale=L["_s"], out_scale=L["_d"], noise=L["noise"],
+                            noise_w=L["noise_w"], bias=L["bias"], shuffle_out=L["up"],
+                            flops=self._alg_flops(L, N))
             L["_x"], L["_xact"], L["_pre"] = x, act, pre
             x, act = pre, ACT_LRELU_S2
             if not L["up"]:  # every non-up conv closes a resolution → ToRGB
@@ -163,12 +177,13 @@ class SynthesisNet:
             # StyledConv backward front: g_pre, q, gy
             q = ws.get(f"g.q{i}", (N, cout), torch.float32)
             ops.zero_(q)
-            if L["up"]:
+            sub = L["up"] and self.up_mode == "subpixel"
+            if L["up"] and not sub:
                 gy = ws.get(f"g.gy{i}", (N, r // 2, r // 2, 4 * cout), T)
             else:
                 gy = ws.get(f"g.gy{i}", (N, r, r, cout), T)
             ops.bias_act_bwd(g_a_next, pre, L["noise"], L["noise_w"], L["bias"], L["_d"], gy, q,
-                             unshuffle=L["up"])
+                             unshuffle=L["up"] and not sub)
             # dgrad + style sdot
             gs = ws.get(f"g.gs{i}", (N, cin), torch.float32)
             ops.zero_(gs)
@@ -177,8 +192,14 @@ class SynthesisNet:
                 gx = ws.get(f"g.ga{i - 1}", (N, rin, rin, cin), T)
             else:
                 gx = None
-            ops.conv3x3(gy, L["wd"], gx, cout=cin, out_scale=L["_s"], aux_x=L["_x"],
-                        act_aux=L["_xact"], sdot=gs, flops=self._alg_flops(L, N))
+            if sub:
+                gt = ws.get(f"g.gt{i}", (N, r + 1, r + 1, cout), T)
+                ops.upconv_blur_bwd(gy, gt)
+                ops.upconv_dgrad(gt, L["wd"], gx, cin, L["_x"], L["_xact"], L["_s"], gs,
+                                 flops=self._alg_flops(L, N))
+            else:
+                ops.conv3x3(gy, L["wd"], gx, cout=cin, out_scale=L["_s"], aux_x=L["_x"],
+                            act_aux=L["_xact"], sdot=gs, flops=self._alg_flops(L, N))
             ops.demod_bwd(q, L["_d"], L["wsq"], L["_s"], gs)
             L["_gs"] = gs
             g_a_next = gx

@@ -107,6 +107,27 @@ int mia_vgg_conv_dgrad(const void* g, const void* w_t, void* gx, int N, int H, i
                        int Cout_g, int Kpad, const void* tap_a, const void* tap_t,
                        float tap_coef, const void* mask_a, int dtype, void* stream);
 
+/* Up-sampling StyledConv [ext] as conv_transpose2d(stride 2, pad 0) → Blur (algorithmic FLOPs:
+ * 9·Cin·Cout MACs per INPUT pixel). The transposed conv runs as four sub-pixel phase GEMMs in one
+ * launch: phase (py,px) has (2−py)×(2−px) taps, w_phase[ph] = [Cout][mia_upconv_kpad(Cin, ph)]
+ * with tap (ty,tx) ↔ W[py + 2(kh−1−ty)][px + 2(kw−1−tx)]. Output T: (N, 2R+1, 2R+1, Cout), no
+ * demod (applied after the blur, with which it commutes). x: (N,R,R,Cin). */
+int mia_upconv_kpad(int cin, int phase, int dtype);
+int mia_upconv_fwd(const void* x, const void* const* w_phase, void* t_out, int N, int R, int Cin,
+                   int Cout, int act_in, const float* style, int dtype, void* stream);
+/* pre = demod·Blur(T) + noise_w·noise + bias, (N, 2R, 2R, C) (rosinality Blur pad (1,1)). */
+int mia_upconv_blur_fwd(const void* t, void* pre, const float* demod, const float* noise,
+                        float noise_w, const float* bias, int N, int R, int C, int dtype,
+                        void* stream);
+/* Adjoint of the blur: gT (N, 2R+1, 2R+1, C) from gy = demod·∂L/∂pre (N, 2R, 2R, C). */
+int mia_upconv_blur_bwd(const void* gy, void* gt, int N, int R, int C, int dtype, void* stream);
+/* Input gradient of the transposed conv = stride-2, pad-0 3×3 conv over gT with w_t =
+ * [Cin][9·Cout] (W[co][ci][ky][kx] at (ky·3+kx)·Cout + co, no flip); epilogue gx = acc·style and
+ * sdot[n][ci] += Σ_p acc·act(x_fwd). gx: (N,R,R,Cin). */
+int mia_upconv_dgrad(const void* g_t, const void* w_t, void* gx, int N, int R, int Cout, int Cin,
+                     const void* x_fwd, int act_x, const float* style, float* sdot, int dtype,
+                     void* stream);
+
 /* ---- elementwise / reduction kernels ----------------------------------------------------- */
 /* FusedLeakyReLU + NoiseInjection forward, standalone (K4): y = lrelu(x + nw·noise + b)·√2 (NHWC). */
 int mia_bias_act_fwd(const void* x, const float* noise, float noise_w, const float* bias,

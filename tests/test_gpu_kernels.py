@@ -312,3 +312,58 @@ def test_adam_step(cuda):
         ops.adam_step(pd, gr.to(cuda), m, v, 0.005, 0.9, 0.999, 1e-8, t)
     torch.cuda.synchronize()
     assert rel_err(pd, pr.detach()) < 1e-6
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,cin,cout,R", [(3, 64, 128, 8), (2, 512, 512, 4), (1, 128, 64, 16)])
+def test_upconv_subpixel_fwd_bwd(cuda, dtype, N, cin, cout, R):
+    """Sub-pixel transposed conv (4 phase GEMMs, one launch) + fused blur/demod/noise/bias, and the
+    backward (bias_act_bwd → blur adjoint → stride-2 dgrad with style sdot → demod_bwd) against
+    autograd through the oracle's per-sample conv_transpose2d + upfirdn2d formulation."""
+    p, wlat, x, noise, bias = _modconv_setup(21 + cin, N, cin, cout, R)
+    g = torch.Generator().manual_seed(5)
+    g_a = torch.randn(N, cout, 2 * R, 2 * R, generator=g)
+    pd = {k: v.double() for k, v in p.items()}
+    scale = 1.0 / math.sqrt(cin * 9)
+    s_in = F.linear(wlat.double(), pd["m.modulation.weight"] / math.sqrt(512),
+                    pd["m.modulation.bias"]).requires_grad_(True)
+    xa = (F.leaky_relu(x.double(), 0.2) * math.sqrt(2)).requires_grad_(True)
+    wt = scale * pd["m.weight"] * s_in.view(N, 1, cin, 1, 1)
+    dm = torch.rsqrt(wt.pow(2).sum([2, 3, 4]) + 1e-8)
+    wt = wt * dm.view(N, cout, 1, 1, 1)
+    wt2 = wt.transpose(1, 2).reshape(N * cin, cout, 3, 3)
+    o = F.conv_transpose2d(xa.reshape(1, N * cin, R, R), wt2, stride=2, groups=N)
+    o = o.view(N, cout, o.shape[2], o.shape[3])
+    o = stylegan2_ref.upfirdn2d(o, stylegan2_ref.make_kernel([1, 3, 3, 1], torch.float64) * 4,
+                                pad=(1, 1))
+    pre_ref = o + 0.1 * noise.double() + bias.double().view(1, -1, 1, 1)
+    act = F.leaky_relu(pre_ref, 0.2) * math.sqrt(2)
+    gx_ref, gs_ref = torch.autograd.grad((act * g_a.double()).sum(), [xa, s_in])
+    # device path
+    ws_ = pd["m.weight"][0] * scale
+    s = s_in.detach().float().to(cuda)
+    wsq = (ws_ ** 2).sum((2, 3)).float().to(cuda)
+    demod = torch.empty(N, cout, device=cuda)
+    ops.style_demod(s, wsq, demod)
+    xd = nhwc(x, dtype).to(cuda)
+    wph = [m.to(cuda) for m in layouts.upconv_subpixel_matrices(ws_, dtype)]
+    t = torch.empty(N, 2 * R + 1, 2 * R + 1, cout, dtype=dtype, device=cuda)
+    ops.upconv_fwd(xd, wph, t, cout, act_in=ops.ACT_LRELU_S2, style=s)
+    nz, bz = noise.reshape(-1).to(cuda), bias.to(cuda)
+    pre = torch.empty(N, 2 * R, 2 * R, cout, dtype=dtype, device=cuda)
+    ops.upconv_blur_fwd(t, pre, demod, nz, 0.1, bz)
+    q = torch.zeros(N, cout, device=cuda)
+    gy = torch.empty_like(pre)
+    ops.bias_act_bwd(nhwc(g_a, dtype).to(cuda), pre, nz, 0.1, bz, demod, gy, q)
+    gt = torch.empty_like(t)
+    ops.upconv_blur_bwd(gy, gt)
+    gs = torch.zeros(N, cin, device=cuda)
+    gx = torch.empty(N, R, R, cin, dtype=dtype, device=cuda)
+    ops.upconv_dgrad(gt, layouts.upconv_dgrad_matrix(ws_, dtype).to(cuda), gx, cin, xd,
+                     ops.ACT_LRELU_S2, s, gs)
+    ops.demod_bwd(q, demod, wsq, s, gs)
+    torch.cuda.synchronize()
+    tol = {torch.float32: 1e-4, torch.float16: 6e-2, torch.bfloat16: 1.2e-1}[dtype]
+    assert rel_err(nchw(pre), pre_ref.detach()) < tol
+    assert rel_err(nchw(gx), gx_ref) < tol
+    assert rel_err(gs, gs_ref) < 2 * tol

@@ -146,3 +146,31 @@ def test_no_cpu_fallback_in_product():
             assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), fn
             assert "torch.nn.functional" not in src, fn  # no torch compute fallback
     assert math.isfinite(1.0) and sys.version_info >= (3, 8)
+
+
+def test_upconv_subpixel_matrices_equal_conv_transpose():
+    """The four sub-pixel phase GEMMs reproduce conv_transpose2d(stride 2, pad 0) exactly."""
+    g = torch.Generator().manual_seed(2)
+    cout, cin, R = 3, 4, 5
+    W = torch.randn(cout, cin, 3, 3, generator=g, dtype=torch.float64)
+    x = torch.randn(2, cin, R, R, generator=g, dtype=torch.float64)
+    T = F.conv_transpose2d(x, W.transpose(0, 1), stride=2)  # (2, cout, 2R+1, 2R+1)
+    mats = layouts.upconv_subpixel_matrices(W, torch.float64)
+    for ph, m in enumerate(mats):
+        py, px = ph >> 1, ph & 1
+        kh, kw = 2 - py, 2 - px
+        ho, wo = R + 1 - py, R + 1 - px
+        xp = F.pad(x, [kw - 1, 1, kh - 1, 1])  # input m + t − (k−1), zero outside
+        out = torch.zeros(2, cout, ho, wo, dtype=torch.float64)
+        for ty in range(kh):
+            for tx in range(kw):
+                blk = m[:, (ty * kw + tx) * cin:(ty * kw + tx + 1) * cin]  # (cout, cin)
+                out += torch.einsum("oc,nchw->nohw", blk, xp[:, :, ty:ty + ho, tx:tx + wo])
+        assert torch.allclose(out, T[:, :, py::2, px::2], atol=1e-12), ph
+    # the adjoint (stride-2 conv with the un-flipped kernel) is the input gradient
+    xx = x.clone().requires_grad_(True)
+    gT = torch.randn(T.shape, generator=g, dtype=torch.float64)
+    (gx,) = torch.autograd.grad((F.conv_transpose2d(xx, W.transpose(0, 1), stride=2) * gT).sum(), xx)
+    md = layouts.upconv_dgrad_matrix(W, torch.float64)
+    cols = F.unfold(gT, 3, stride=2).view(2, cout, 9, R * R).transpose(1, 2).reshape(2, 9 * cout, -1)
+    assert torch.allclose((md[:, :9 * cout] @ cols).view(2, cin, R, R), gx, atol=1e-12)

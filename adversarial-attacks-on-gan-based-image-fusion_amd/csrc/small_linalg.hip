@@ -35,14 +35,19 @@ __global__ __launch_bounds__(256) void sgemm_kernel(int M, int Nn, int K, float 
   __shared__ float Bs[GK][GT + 1];
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
+  const bool a_kfast = sak == 1, b_kfast = sbk == 1;
   float acc[4][4] = {};
   for (int k0 = 0; k0 < K; k0 += GK) {
+    // consecutive threads walk the operand's contiguous dimension (coalesced loads)
     for (int i = threadIdx.x; i < GK * GT; i += 256) {
-      const int kk = i / GT, mm = i % GT;
+      const int kk = a_kfast ? i % GK : i / GT, mm = a_kfast ? i / GK : i % GT;
       const int gm = m0 + mm, gk = k0 + kk;
       As[kk][mm] = (gm < M && gk < K) ? A[gm * sam + gk * sak] : 0.f;
-      const int gn = n0 + mm;
-      Bs[kk][mm] = (gn < Nn && gk < K) ? B[gk * sbk + gn * sbn] : 0.f;
+    }
+    for (int i = threadIdx.x; i < GK * GT; i += 256) {
+      const int kk = b_kfast ? i % GK : i / GT, nn = b_kfast ? i / GK : i % GT;
+      const int gn = n0 + nn, gk = k0 + kk;
+      Bs[kk][nn] = (gn < Nn && gk < K) ? B[gk * sbk + gn * sbn] : 0.f;
     }
     __syncthreads();
 #pragma unroll

@@ -47,19 +47,20 @@ SIGNATURES = {
                                    c_float, P, c_int, P]),
     "mia_upconv_kpad": (c_int, [c_int, c_int, c_int]),
     "mia_upconv_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, P]),
-    "mia_upconv_blur_fwd": (c_int, [P, P, P, P, c_float, P, c_int, c_int, c_int, c_int, P]),
+    "mia_upconv_blur_fwd": (c_int, [P, P, P, P, c_float, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_upconv_blur_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     "mia_upconv_dgrad": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, c_int,
                                  P]),
     "mia_bias_act_fwd": (c_int, [P, P, c_float, P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_bias_act_bwd": (c_int, [P, P, P, c_float, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
-                                 c_int, P]),
+                                 c_int, c_int, P]),
     "mia_upfirdn2d_fwd": (c_int, [P, P, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, c_int,
                                   P]),
     "mia_upfirdn2d_bwd": (c_int, [P, P, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, c_int,
                                   P]),
-    "mia_torgb_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
-    "mia_torgb_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    "mia_torgb_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
+    "mia_torgb_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                              P]),
     "mia_maxpool2_fwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_maxpool2_bwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_float, c_int,
                                  c_int, P]),

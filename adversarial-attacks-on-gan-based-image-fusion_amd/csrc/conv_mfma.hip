@@ -32,6 +32,7 @@
 // spans. The epilogue stages the fp32 tile through LDS and then works on 8-channel vectors
 // (16-byte loads of every aux operand, 16-byte stores).
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "mia_common.h"
@@ -147,30 +148,43 @@ __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
 
 constexpr int ROWB = 128;  // bytes per tile row (one K-step slice)
 
-template <int BM, int BN>
-constexpr int epi_stride() { return BN + 4; }  // fp32 words per staged row (bank-conflict pad)
+// Tile configurations: WM×WN waves, each wave FM×FN 16×16 fragments; STAGES-deep DMA ring.
+//   128×64  / 128×128 : 4 waves, 2 stages, 2 blocks per CU (small M, Cout ≤ 64)
+//   256×128           : 8 waves, 3 stages, 1 block per CU (large M: 85 FLOP per staged byte,
+//                       two K-steps of DMA in flight behind a counted vmcnt)
+template <int WM_, int WN_, int FM_, int FN_, int STAGES_>
+struct Tile {
+  static constexpr int WM = WM_, WN = WN_, FM = FM_, FN = FN_, STAGES = STAGES_;
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+  static constexpr int A_INS = BM / (8 * NW), B_INS = BN / (8 * NW);  // 1-KB DMA pieces/wave/step
+  static constexpr int STAGE = (BM + BN) * ROWB;
+  static constexpr int EROWS = BM < 128 ? BM : 128;  // rows staged per epilogue pass
+  static constexpr int ES = BN + 4;                  // fp32 words per staged row (bank pad)
+  static_assert(A_INS >= 1 && B_INS >= 1 && A_INS * 8 * NW == BM && B_INS * 8 * NW == BN, "");
+};
 
-template <typename T, int BM, int BN, bool PRO, bool SMALLC>
-__global__ __launch_bounds__(256, 2) void conv_kernel(const ConvK k) {
+template <typename T, typename TL, bool PRO, bool SMALLC>
+__global__ __launch_bounds__(TL::NT, TL::NW == 4 ? 2 : 1) void conv_kernel(const ConvK k) {
   typedef typename Vec<T>::type VT;
   constexpr int VEC = Vec<T>::N;
   constexpr int BK = ROWB / (int)sizeof(T);
-  constexpr int FM = BM / 32, FN = BN / 32;         // 2×2 waves
-  constexpr int A_INS = BM / 32, B_INS = BN / 32;   // 1-KB DMA pieces per wave per K-step
-  constexpr int STAGE = (BM + BN) * ROWB;
-  constexpr int ES = epi_stride<BM, BN>();
+  constexpr int WN = TL::WN, FM = TL::FM, FN = TL::FN, NT = TL::NT, NW = TL::NW;
+  constexpr int BM = TL::BM, BN = TL::BN, A_INS = TL::A_INS, B_INS = TL::B_INS;
+  constexpr int STAGE = TL::STAGE, STAGES = TL::STAGES, ES = TL::ES, EROWS = TL::EROWS;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const mia_conv_args& p = k.a;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform → scalar LDS bases
+  const int wm = wid / WN, wn = wid % WN;
   const int bl = xcd_remap(blockIdx.x, k.nblk);
   int gi = 0;
 #pragma unroll
   for (int g = 1; g < 4; ++g)
     if (g < k.ng && bl >= k.g[g].blk0) gi = g;
-  const ConvGroup& G = k.g[gi];
+  const ConvGroup G = k.g[gi];  // by value: scalar registers for the whole kernel
   const int b = bl - G.blk0;
   const int m0 = (b / k.nbn) * BM, n0 = (b % k.nbn) * BN;
   const int Hin = p.H, Win = p.W, Cin = p.Cin;
@@ -213,7 +227,6 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(const ConvK k) {
     const int c = n0 + row;
     b_ptr[j] = c < p.Cout ? Wt + (size_t)c * G.kpad + ((lane & 7) ^ fsw(row)) * VEC : zero;
   }
-  const int b_inc = b_ptr[0] == zero ? 0 : BK;  // per-lane below (rows past Cout stay on zero)
 
   // K-step state for the DMA issue (uniform across the block)
   int is_tap = 0, is_cb = 0;
@@ -252,18 +265,17 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(const ConvK k) {
                                        0, 0);
     }
   };
-  (void)b_inc;
 
   // ---- modulation table (PRO): s[n][ci] (·√2 for lrelu inputs) for the images of this tile ----
   const int n_first = m0 / HWo;
-  T* stab = (T*)(smem + 2 * STAGE);
+  T* stab = (T*)(smem + STAGES * STAGE);
   const bool lrelu_in = p.act_in == MIA_ACT_LRELU_S2;
   int a_nl[FM];
   if constexpr (PRO) {
     const int n_last = (min(m0 + BM, G.m) - 1) / HWo;
     const int cnt = (n_last - n_first + 1) * Cin;
     const float mul = lrelu_in ? SQRT2 : 1.f;
-    for (int i = tid; i < cnt; i += 256) {
+    for (int i = tid; i < cnt; i += NT) {
       const float sv = p.in_scale ? p.in_scale[(size_t)n_first * Cin + i] : 1.f;
       stab[i] = from_f<T>(sv * mul);
     }
@@ -281,12 +293,23 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(const ConvK k) {
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = G.kpad / BK;
-  issue(0, 0);
-  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s, s);
+  if constexpr (STAGES == 2) {
+    __syncthreads();
+  } else {
+    // retire step 0 (step 1 may stay in flight), then make every wave's DMA visible
+    if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_INS + B_INS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   const int frow = lane & 15, fq = lane >> 4;
+  int st = 0;
   for (int kb = 0; kb < nk; ++kb) {
-    const int st = kb & 1;
-    if (kb + 1 < nk) issue(kb + 1, st ^ 1);
+    const int ahead = kb + STAGES - 1;
+    const int st_ahead = st == 0 ? STAGES - 1 : st - 1;  // (kb + STAGES - 1) % STAGES
+    if (ahead < nk) issue(ahead, st_ahead);
     const char* sa = smem + st * STAGE;
     const char* sb = sa + BM * ROWB;
 #pragma unroll
@@ -316,24 +339,25 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(const ConvK k) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = mfma_chunk<T>(af[i], bf[j], acc[i][j]);
     }
-    __syncthreads();  // retires the DMA of step kb+1 (vmcnt(0)) and frees stage st for kb+2
+    if constexpr (STAGES == 2) {
+      __syncthreads();  // retires the DMA of step kb+1 (vmcnt(0)) and frees stage st
+    } else {
+      // step kb+1 must have landed; step kb+2 (issued this iteration) may stay in flight
+      if (ahead < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_INS + B_INS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS reads of stage st done
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    st = st + 1 == STAGES ? 0 : st + 1;
   }
+  if constexpr (STAGES != 2) __syncthreads();
 
-  // ---- epilogue: stage the fp32 tile in LDS, then 8-channel vectors -------------------------
+  // ---- epilogue: stage the fp32 tile in LDS (EROWS rows per pass), then 8-channel vectors ---
   float* tile = (float*)smem;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        tile[(wm * FM * 16 + 16 * i + fq * 4 + r) * ES + wn * FN * 16 + 16 * j + frow] =
-            acc[i][j][r];
-  __syncthreads();
-
   const int Cout = p.Cout;
   constexpr int CPR = BN / 8;          // 8-channel chunks per row
-  constexpr int RPP = 256 / CPR;       // rows per pass
+  constexpr int RPP = NT / CPR;        // rows per pass
   const int cc = tid % CPR, r0 = tid / CPR;
   const int col = n0 + cc * 8;
   const bool col_ok = col < Cout;      // Cout % 8 == 0 (host check)
@@ -348,77 +372,100 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(const ConvK k) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) part[e] = 0.f;
 
-  for (int rr = r0; rr < BM; rr += RPP) {
-    const int row = m0 + rr;
-    if (row >= G.m || !col_ok) continue;
-    float v[8];
-    load8f(tile + rr * ES + cc * 8, v);
-    const size_t aoff = (size_t)row * Cout + col;
-    if (p.sdot) {
-      float xv[8];
-      load8<T>(AX + aoff, xv);
-      const int n = row / HWo;
+  // per-column epilogue constants, loaded once (single-image tiles: out_scale too)
+  float bias8[8], osc8[8];
+  const int cm0 = p.shuffle_out ? col % k.cout_mod : col;
+  if (p.bias && col_ok) load8f(p.bias + cm0, bias8);
+  if (p.out_scale && single && col_ok) load8f(p.out_scale + (size_t)(m0 / HWo) * k.cout_mod + cm0, osc8);
+  constexpr int ITERS = EROWS / RPP;
+  static_assert(ITERS * RPP == EROWS, "");
+
+  for (int h = 0; h < BM / EROWS; ++h) {
+    const int wrow0 = wm * FM * 16;
+    if (wrow0 >= h * EROWS && wrow0 < (h + 1) * EROWS) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float c = v[e] * apply_act(xv[e], p.act_aux);
-        if (single) part[e] += c;
-        else atomicAdd(&p.sdot[(size_t)n * Cout + col + e], c);
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            tile[(wrow0 - h * EROWS + 16 * i + fq * 4 + r) * ES + wn * FN * 16 + 16 * j + frow] =
+                acc[i][j][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      const int rr = r0 + it * RPP;
+      const int row = m0 + h * EROWS + rr;
+      if (row < G.m && col_ok) {
+        float v[8];
+        load8f(tile + rr * ES + cc * 8, v);
+        const size_t aoff = (size_t)row * Cout + col;
+        const int n = single ? m0 / HWo : row / HWo;
+        if (p.sdot) {
+          float xv[8];
+          load8<T>(AX + aoff, xv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float c = v[e] * apply_act(xv[e], p.act_aux);
+            if (single) part[e] += c;
+            else atomicAdd(&p.sdot[(size_t)n * Cout + col + e], c);
+          }
+        }
+        if (Y) {
+          const int pix = row - n * HWo;
+          const int y = pix / G.wo, x = pix - (pix / G.wo) * G.wo;
+          int cm = col, yo, xo;
+          if (p.shuffle_out) {
+            const int ph = col / k.cout_mod;
+            cm = col - ph * k.cout_mod;
+            yo = 2 * y + (ph >> 1);
+            xo = 2 * x + (ph & 1);
+          } else {
+            yo = G.ay * y + G.by;
+            xo = G.ax * x + G.bx;
+          }
+          const size_t off = ((size_t)(n * k.HT + yo) * k.WT + xo) * k.ystride + cm;
+          if (p.out_scale) {
+            if (!single) load8f(p.out_scale + (size_t)n * k.cout_mod + cm, osc8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= osc8[e];
+          }
+          if (p.noise) {
+            const float nz = p.noise_w * p.noise[yo * k.WT + xo];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += nz;
+          }
+          if (p.bias) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += bias8[e];
+          }
+          if (TA) {
+            float ta[8], tt[8];
+            load8<T>(TA + aoff, ta);
+            load8<T>(TT + aoff, tt);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += p.tap_coef * (ta[e] - tt[e]);
+          }
+          if (MA) {
+            float ma[8];
+            load8<T>(MA + aoff, ma);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = ma[e] > 0.f ? v[e] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], p.act_out);
+          if (p.accumulate) {
+            float yo8[8];
+            load8<T>(Y + off, yo8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += yo8[e];
+          }
+          store8<T>(Y + off, v);
+        }
       }
     }
-    if (!Y) continue;
-    const int n = row / HWo;
-    const int pix = row - n * HWo;
-    const int y = pix / G.wo, x = pix - (pix / G.wo) * G.wo;
-    int cm = col, yo, xo;
-    if (p.shuffle_out) {
-      const int ph = col / k.cout_mod;
-      cm = col - ph * k.cout_mod;
-      yo = 2 * y + (ph >> 1);
-      xo = 2 * x + (ph & 1);
-    } else {
-      yo = G.ay * y + G.by;
-      xo = G.ax * x + G.bx;
-    }
-    const size_t off = ((size_t)(n * k.HT + yo) * k.WT + xo) * k.ystride + cm;
-    if (p.out_scale) {
-      float s[8];
-      load8f(p.out_scale + (size_t)n * k.cout_mod + cm, s);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= s[e];
-    }
-    if (p.noise) {
-      const float nz = p.noise_w * p.noise[yo * k.WT + xo];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += nz;
-    }
-    if (p.bias) {
-      float bb[8];
-      load8f(p.bias + cm, bb);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += bb[e];
-    }
-    if (TA) {
-      float ta[8], tt[8];
-      load8<T>(TA + aoff, ta);
-      load8<T>(TT + aoff, tt);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += p.tap_coef * (ta[e] - tt[e]);
-    }
-    if (MA) {
-      float ma[8];
-      load8<T>(MA + aoff, ma);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = ma[e] > 0.f ? v[e] : 0.f;
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], p.act_out);
-    if (p.accumulate) {
-      float yo8[8];
-      load8<T>(Y + off, yo8);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += yo8[e];
-    }
-    store8<T>(Y + off, v);
+    __syncthreads();
   }
 
   if (p.sdot && single) {
@@ -427,34 +474,37 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(const ConvK k) {
 #pragma unroll
     for (int e = 0; e < 8; ++e)
       for (int o = CPR; o < 64; o <<= 1) part[e] += __shfl_xor(part[e], o, 64);
-    __syncthreads();
-    float* red = (float*)smem;  // [4 waves][BN]
+    float* red = (float*)smem;  // [NW waves][BN]
     if (lane < CPR) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) red[wid * BN + lane * 8 + e] = part[e];
     }
     __syncthreads();
     if (tid < BN && n0 + tid < Cout) {
-      const float s = red[tid] + red[BN + tid] + red[2 * BN + tid] + red[3 * BN + tid];
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s += red[w * BN + tid];
       atomicAdd(&p.sdot[(size_t)(m0 / HWo) * Cout + n0 + tid], s);
     }
   }
 }
 
-template <typename T, int BM, int BN, bool PRO, bool SMALLC>
+template <typename T, typename TL, bool PRO, bool SMALLC>
 static int launch_tile(ConvK& k, hipStream_t st) {
-  k.nbn = (k.a.Cout + BN - 1) / BN;
+  k.nbn = (k.a.Cout + TL::BN - 1) / TL::BN;
   int blk = 0;
   for (int g = 0; g < k.ng; ++g) {
-    k.g[g].nbm = (k.g[g].m + BM - 1) / BM;
+    k.g[g].nbm = (k.g[g].m + TL::BM - 1) / TL::BM;
     k.g[g].blk0 = blk;
     blk += k.g[g].nbm * k.nbn;
   }
   k.nblk = blk;
-  size_t lds = 2 * (BM + BN) * ROWB;
+  size_t lds = (size_t)TL::STAGES * TL::STAGE;
   if (PRO) lds += (size_t)k.n_first_max * k.a.Cin * sizeof(T);
-  lds = std::max(lds, (size_t)BM * epi_stride<BM, BN>() * 4);
-  auto fn = conv_kernel<T, BM, BN, PRO, SMALLC>;
+  lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
+  lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
+  if (lds > 160 * 1024) return set_error("conv: LDS budget exceeded");
+  auto fn = conv_kernel<T, TL, PRO, SMALLC>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -462,14 +512,27 @@ static int launch_tile(ConvK& k, hipStream_t st) {
       return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     attr_set = true;
   }
-  hipLaunchKernelGGL(fn, dim3(blk), dim3(256), lds, st, k);
+  hipLaunchKernelGGL(fn, dim3(blk), dim3(TL::NT), lds, st, k);
   return check_launch("conv");
 }
 
+typedef Tile<2, 2, 4, 2, 2> Tile128x64;
+typedef Tile<2, 2, 4, 4, 2> Tile128x128;
+typedef Tile<4, 2, 4, 4, 3> Tile256x128;
+
 template <typename T, bool PRO, bool SMALLC>
 static int launch_bn(ConvK& k, hipStream_t st) {
-  if (k.a.Cout <= 64) return launch_tile<T, 128, 64, PRO, SMALLC>(k, st);
-  return launch_tile<T, 128, 128, PRO, SMALLC>(k, st);
+  int64_t m = 0;
+  for (int g = 0; g < k.ng; ++g) m += k.g[g].m;
+  // Tuning override MIA_CONV_TILE (read per launch): 2 = 256x128 3-stage tile where the launch
+  // has ≥ 2 waves of them. Default 128x128: measured faster on every StyleGAN2/VGG shape of the
+  // 256² attack step (2 blocks/CU hide each other's DMA waits better than 1 deeper ring).
+  const char* e = getenv("MIA_CONV_TILE");
+  const int force = e ? atoi(e) : 0;
+  if (k.a.Cout <= 64) return launch_tile<T, Tile128x64, PRO, SMALLC>(k, st);
+  const int64_t big_blocks = (m / 256) * ((k.a.Cout + 127) / 128);
+  if (force == 2 && big_blocks >= 512) return launch_tile<T, Tile256x128, PRO, SMALLC>(k, st);
+  return launch_tile<T, Tile128x128, PRO, SMALLC>(k, st);
 }
 
 template <typename T>
@@ -520,7 +583,8 @@ static int run_conv(ConvK& k, int dtype, hipStream_t st) {
   k.log2cin = lc;
   int hw_min = 1 << 30;
   for (int g = 0; g < k.ng; ++g) hw_min = std::min(hw_min, k.g[g].ho * k.g[g].wo);
-  k.n_first_max = std::min(a.N, (128 + hw_min - 1) / hw_min + 1);
+  k.n_first_max = std::min(a.N, (256 + hw_min - 1) / hw_min + 1);
+
   MIA_DISPATCH_DTYPE(dtype, T, return launch_conv<T>(k, st));
   return MIA_OK;
 }

@@ -41,7 +41,7 @@ __global__ void bias_act_bwd_kernel(const T* __restrict__ g_a, const T* __restri
                                     const float* __restrict__ noise, float nw,
                                     const float* __restrict__ bias, const float* __restrict__ demod,
                                     T* __restrict__ gy, float* __restrict__ q, int H, int W, int C,
-                                    int unshuffle, int pix_per_block) {
+                                    int unshuffle, int from_act, int pix_per_block) {
   typedef typename Vec<T>::type VT;
   constexpr int V = Vec<T>::N;
   __shared__ float red[TPB * 8];
@@ -72,8 +72,10 @@ __global__ void bias_act_bwd_kernel(const T* __restrict__ g_a, const T* __restri
       VT o;
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        const float pv = to_f(pr[e]);
-        const float gp = to_f(ga[e]) * lrelu_s2_grad(pv);
+        const float pin = to_f(pr[e]);
+        const float gr = lrelu_s2_grad(pin);  // same sign for pre and act = lrelu(pre)·√2
+        const float pv = from_act ? pin / gr : pin;
+        const float gp = to_f(ga[e]) * gr;
         qa[e] += gp * (pv - nz - bs[e]);
         o[e] = from_f<T>(gp * dm[e]);
       }
@@ -115,7 +117,8 @@ __constant__ float kBlur4[4] = {0.25f, 0.75f, 0.75f, 0.25f};
 template <typename T, bool FWD>
 __global__ void blur4_quad_kernel(const T* __restrict__ in, T* __restrict__ out,
                                   const float* __restrict__ demod, const float* __restrict__ noise,
-                                  float nw, const float* __restrict__ bias, int N, int R, int C) {
+                                  float nw, const float* __restrict__ bias, int N, int R, int C,
+                                  int act_out) {
   typedef typename Vec<T>::type VT;
   constexpr int V = Vec<T>::N;
   const int Hin = FWD ? 2 * R + 1 : 2 * R;
@@ -191,7 +194,9 @@ __global__ void blur4_quad_kernel(const T* __restrict__ in, T* __restrict__ out,
         const float nz = (FWD && noise) ? nw * noise[oy * Hout + ox] : 0.f;
 #pragma unroll
         for (int e = 0; e < V; ++e)
-          o[e] = from_f<T>(FWD ? acc[a][b][e] * dm[e] + nz + bs[e] : acc[a][b][e]);
+          o[e] = from_f<T>(FWD ? (act_out ? lrelu_s2(acc[a][b][e] * dm[e] + nz + bs[e])
+                                          : acc[a][b][e] * dm[e] + nz + bs[e])
+                               : acc[a][b][e]);
         *(VT*)(out + (((size_t)n * Hout + oy) * Hout + ox) * C + cv * V) = o;
       }
     }
@@ -269,7 +274,7 @@ template <typename T>
 __global__ void torgb_fwd_kernel(const T* __restrict__ pre, const float* __restrict__ s,
                                  const float* __restrict__ wr, const float* __restrict__ bias,
                                  const float* __restrict__ skip, float* __restrict__ rgb, int H,
-                                 int W, int Cin, int tpp, int cpt, int pix_per_block) {
+                                 int W, int Cin, int tpp, int cpt, int pix_per_block, int act_in) {
   typedef typename Vec<T>::type VT;
   constexpr int V = Vec<T>::N;
   extern __shared__ float wm[];  // [3][Cin]
@@ -291,7 +296,7 @@ __global__ void torgb_fwd_kernel(const T* __restrict__ pre, const float* __restr
         const VT v = *(const VT*)(row + c0);
 #pragma unroll
         for (int e = 0; e < V; ++e) {
-          const float a = lrelu_s2(to_f(v[e]));
+          const float a = act_in ? lrelu_s2(to_f(v[e])) : to_f(v[e]);
           a0 += a * wm[c0 + e];
           a1 += a * wm[Cin + c0 + e];
           a2 += a * wm[2 * Cin + c0 + e];
@@ -320,7 +325,7 @@ template <typename T>
 __global__ void torgb_bwd_kernel(const float* __restrict__ grgb, const T* __restrict__ pre,
                                  const float* __restrict__ s, const float* __restrict__ wr,
                                  T* __restrict__ g_a, float* __restrict__ gs, int H, int W, int Cin,
-                                 int accumulate, int pix_per_block) {
+                                 int accumulate, int pix_per_block, int act_in) {
   typedef typename Vec<T>::type VT;
   constexpr int V = Vec<T>::N;
   extern __shared__ float sh[];  // wr [3][Cin], s [Cin], partials [TPB/tpp][Cin]
@@ -356,7 +361,7 @@ __global__ void torgb_bwd_kernel(const float* __restrict__ grgb, const T* __rest
       for (int e = 0; e < V; ++e) {
         const int c = c0 + e;
         const float u = g0 * w3[c] + g1 * w3[Cin + c] + g2 * w3[2 * Cin + c];
-        acc[e] += lrelu_s2(to_f(pr[e])) * u;
+        acc[e] += (act_in ? lrelu_s2(to_f(pr[e])) : to_f(pr[e])) * u;
         const float gv = sn[c] * u + (accumulate ? to_f(ga[e]) : 0.f);
         ga[e] = from_f<T>(gv);
       }
@@ -696,8 +701,8 @@ extern "C" int mia_bias_act_fwd(const void* x, const float* noise, float noise_w
 
 extern "C" int mia_bias_act_bwd(const void* g_a, const void* pre, const float* noise,
                                 float noise_w, const float* bias, const float* demod, void* gy,
-                                float* q, int N, int H, int W, int C, int unshuffle, int dtype,
-                                void* stream) {
+                                float* q, int N, int H, int W, int C, int unshuffle, int from_act,
+                                int dtype, void* stream) {
   MIA_CHECK_ARG(g_a && pre && demod && gy && q, "bad args");
   const int V = dtype == MIA_F32 ? 4 : 8;
   MIA_CHECK_ARG(C % V == 0 && C / V <= TPB && (TPB % (C / V)) == 0, "C/V must divide 256");
@@ -708,20 +713,20 @@ extern "C" int mia_bias_act_bwd(const void* g_a, const void* pre, const float* n
   dim3 grid((HW + ppb - 1) / ppb, N);
   MIA_DISPATCH_DTYPE(dtype, T,
       MIA_LAUNCH(bias_act_bwd_kernel<T>, grid, dim3(TPB), 0, (const T*)g_a, (const T*)pre, noise,
-                 noise_w, bias, demod, (T*)gy, q, H, W, C, unshuffle, ppb));
+                 noise_w, bias, demod, (T*)gy, q, H, W, C, unshuffle, from_act, ppb));
   return MIA_OK;
 }
 
 extern "C" int mia_upconv_blur_fwd(const void* t, void* pre, const float* demod,
                                    const float* noise, float noise_w, const float* bias, int N,
-                                   int R, int C, int dtype, void* stream) {
+                                   int R, int C, int act_out, int dtype, void* stream) {
   MIA_CHECK_ARG(t && pre && demod && N > 0 && R > 0, "bad args");
   const int V = dtype == MIA_F32 ? 4 : 8;
   MIA_CHECK_ARG(C % V == 0, "C must be a multiple of the vector width");
   const int64_t total = (int64_t)N * R * R * (C / V);
   MIA_DISPATCH_DTYPE(dtype, T,
       MIA_LAUNCH((blur4_quad_kernel<T, true>), dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0,
-                 (const T*)t, (T*)pre, demod, noise, noise_w, bias, N, R, C));
+                 (const T*)t, (T*)pre, demod, noise, noise_w, bias, N, R, C, act_out));
   return MIA_OK;
 }
 
@@ -733,7 +738,7 @@ extern "C" int mia_upconv_blur_bwd(const void* gy, void* gt, int N, int R, int C
   const int64_t total = (int64_t)N * (R + 1) * (R + 1) * (C / V);
   MIA_DISPATCH_DTYPE(dtype, T,
       MIA_LAUNCH((blur4_quad_kernel<T, false>), dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0,
-                 (const T*)gy, (T*)gt, nullptr, nullptr, 0.f, nullptr, N, R, C));
+                 (const T*)gy, (T*)gt, nullptr, nullptr, 0.f, nullptr, N, R, C, 0));
   return MIA_OK;
 }
 
@@ -774,7 +779,7 @@ extern "C" int mia_upfirdn2d_bwd(const float* gy, float* gx, int planes, int H, 
 
 extern "C" int mia_torgb_fwd(const void* pre, const float* style, const float* wr,
                              const float* bias, const float* skip, float* rgb, int N, int H, int W,
-                             int Cin, int dtype, void* stream) {
+                             int Cin, int act_in, int dtype, void* stream) {
   MIA_CHECK_ARG(pre && style && wr && bias && rgb, "bad args");
   const int V = dtype == MIA_F32 ? 4 : 8;
   MIA_CHECK_ARG(Cin % V == 0, "Cin must be a multiple of the vector width");
@@ -788,13 +793,13 @@ extern "C" int mia_torgb_fwd(const void* pre, const float* style, const float* w
   const size_t sh = 3 * Cin * sizeof(float);
   MIA_DISPATCH_DTYPE(dtype, T,
       MIA_LAUNCH(torgb_fwd_kernel<T>, grid, dim3(TPB), sh, (const T*)pre, style, wr, bias, skip,
-                 rgb, H, W, Cin, tpp, cpt, ppb));
+                 rgb, H, W, Cin, tpp, cpt, ppb, act_in));
   return MIA_OK;
 }
 
 extern "C" int mia_torgb_bwd(const float* g_rgb, const void* pre, const float* style,
                              const float* wr, void* g_a, float* gs, int N, int H, int W, int Cin,
-                             int accumulate, int dtype, void* stream) {
+                             int accumulate, int act_in, int dtype, void* stream) {
   MIA_CHECK_ARG(g_rgb && pre && style && wr && g_a && gs, "bad args");
   const int V = dtype == MIA_F32 ? 4 : 8;
   MIA_CHECK_ARG(Cin % V == 0 && Cin / V <= TPB && TPB % (Cin / V) == 0, "Cin/V must divide 256");
@@ -805,7 +810,7 @@ extern "C" int mia_torgb_bwd(const float* g_rgb, const void* pre, const float* s
   MIA_CHECK_ARG(sh <= 64 * 1024, "LDS budget");
   MIA_DISPATCH_DTYPE(dtype, T,
       MIA_LAUNCH(torgb_bwd_kernel<T>, grid, dim3(TPB), sh, g_rgb, (const T*)pre, style, wr, (T*)g_a,
-                 gs, H, W, Cin, accumulate, ppb));
+                 gs, H, W, Cin, accumulate, ppb, act_in));
   return MIA_OK;
 }
 

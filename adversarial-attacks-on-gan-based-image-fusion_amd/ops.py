@@ -152,7 +152,7 @@ def upconv_fwd(x, w_phases, t_out, cout, act_in=ACT_NONE, style=None, flops=None
     return t_out
 
 
-def upconv_blur_fwd(t, pre, demod, noise, noise_w, bias):
+def upconv_blur_fwd(t, pre, demod, noise, noise_w, bias, act_out=ACT_NONE):
     N, TS, _, C = t.shape
     R = (TS - 1) // 2
     _need(pre, (N, 2 * R, 2 * R, C), t.dtype, "pre")
@@ -160,7 +160,7 @@ def upconv_blur_fwd(t, pre, demod, noise, noise_w, bias):
     _numel_ok(noise, 4 * R * R, torch.float32, "noise")
     _numel_ok(bias, C, torch.float32, "bias")
     call("mia_upconv_blur_fwd", ptr(t), ptr(pre), ptr(demod), ptr(noise), float(noise_w),
-         ptr(bias), N, R, C, dt(t), stream())
+         ptr(bias), N, R, C, int(act_out), dt(t), stream())
     return pre
 
 
@@ -198,7 +198,7 @@ def bias_act_fwd(x, noise, noise_w, bias, y):
     return y
 
 
-def bias_act_bwd(g_a, pre, noise, noise_w, bias, demod, gy, q, unshuffle=False):
+def bias_act_bwd(g_a, pre, noise, noise_w, bias, demod, gy, q, unshuffle=False, from_act=False):
     N, H, W, C = pre.shape
     _need(g_a, pre.shape, pre.dtype, "g_a")
     _numel_ok(noise, H * W, torch.float32, "noise")
@@ -210,7 +210,7 @@ def bias_act_bwd(g_a, pre, noise, noise_w, bias, demod, gy, q, unshuffle=False):
     else:
         _need(gy, pre.shape, pre.dtype, "gy")
     call("mia_bias_act_bwd", ptr(g_a), ptr(pre), ptr(noise), float(noise_w), ptr(bias), ptr(demod),
-         ptr(gy), ptr(q), N, H, W, C, int(bool(unshuffle)), dt(pre), stream())
+         ptr(gy), ptr(q), N, H, W, C, int(bool(unshuffle)), int(bool(from_act)), dt(pre), stream())
     return gy
 
 
@@ -243,7 +243,7 @@ def upfirdn2d_bwd(gy, gx, k1d, up=1, down=1, pad=(0, 0)):
     return gx
 
 
-def torgb_fwd(pre, style, wr, bias, skip, rgb):
+def torgb_fwd(pre, style, wr, bias, skip, rgb, act_in=ACT_LRELU_S2):
     N, H, W, Cin = pre.shape
     _numel_ok(style, N * Cin, torch.float32, "style")
     _need(wr, (3, Cin), torch.float32, "wr")
@@ -252,11 +252,11 @@ def torgb_fwd(pre, style, wr, bias, skip, rgb):
         _need(skip, (N, 3, H // 2, W // 2), torch.float32, "skip")
     _need(rgb, (N, 3, H, W), torch.float32, "rgb")
     call("mia_torgb_fwd", ptr(pre), ptr(style), ptr(wr), ptr(bias), ptr(skip), ptr(rgb), N, H, W,
-         Cin, dt(pre), stream())
+         Cin, int(act_in), dt(pre), stream())
     return rgb
 
 
-def torgb_bwd(g_rgb, pre, style, wr, g_a, gs, accumulate):
+def torgb_bwd(g_rgb, pre, style, wr, g_a, gs, accumulate, act_in=ACT_LRELU_S2):
     N, H, W, Cin = pre.shape
     _need(g_rgb, (N, 3, H, W), torch.float32, "g_rgb")
     _numel_ok(style, N * Cin, torch.float32, "style")
@@ -264,7 +264,7 @@ def torgb_bwd(g_rgb, pre, style, wr, g_a, gs, accumulate):
     _need(g_a, pre.shape, pre.dtype, "g_a")
     _numel_ok(gs, N * Cin, torch.float32, "gs")
     call("mia_torgb_bwd", ptr(g_rgb), ptr(pre), ptr(style), ptr(wr), ptr(g_a), ptr(gs), N, H, W,
-         Cin, int(bool(accumulate)), dt(pre), stream())
+         Cin, int(bool(accumulate)), int(act_in), dt(pre), stream())
 
 
 def pool_out(H, ceil_mode):

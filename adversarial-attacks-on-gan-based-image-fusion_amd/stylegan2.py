@@ -7,9 +7,11 @@ rosinality generator (un-vendored dependency, see oracle/stylegan2_ref.py) with 
 omitted (the attack always passes W+ latents).
 
 Layout in HBM: every feature map is NHWC in the compute dtype. Each StyledConv stores only its
-pre-activation ``pre = demod·conv(x̃) + noise_w·noise + bias`` (one tensor per layer); consumers
-apply lrelu·√2 on load (next conv's A-operand prologue, ToRGB, backward masks). The image/skip path
-(3 channels) is fp32 NCHW. Styles, demod coefficients and their gradients are fp32 [N][C].
+activation ``a = lrelu(pre)·√2`` with ``pre = demod·conv(x̃) + noise_w·noise + bias`` (one tensor
+per layer, written by the producing epilogue), so the next conv's A-operand prologue is a single
+multiply by the style. The backward recovers ``pre = a / lrelu'(a)`` (same sign) where it needs it.
+The image/skip path (3 channels) is fp32 NCHW. Styles, demod coefficients and their gradients are
+fp32 [N][C].
 
 Backward computes ∂L/∂w+ only (no weight gradients: the pixel gradient does not need them,
 SURVEY.md §2.1 note). Per StyledConv, with g_pre = ∂L/∂pre:
@@ -117,7 +119,7 @@ class SynthesisNet:
         self.styles(lat, ws)
         x0 = ws.get("g.const", (N, 4, 4, self.const.shape[-1]), T)
         ops.repeat(self.const, x0, N)
-        x, act = x0, ACT_NONE
+        x = x0
         rgb = None
         ti = 0
         for i, L in enumerate(self.convs):
@@ -125,20 +127,20 @@ class SynthesisNet:
             pre = ws.get(f"g.pre{i}", (N, r, r, cout), T)
             if L["up"] and self.up_mode == "subpixel":
                 t = ws.get(f"g.t{i}", (N, r + 1, r + 1, cout), T)
-                ops.upconv_fwd(x, L["wph"], t, cout, act_in=act, style=L["_s"],
-                               flops=self._alg_flops(L, N))
-                ops.upconv_blur_fwd(t, pre, L["_d"], L["noise"], L["noise_w"], L["bias"])
+                ops.upconv_fwd(x, L["wph"], t, cout, style=L["_s"], flops=self._alg_flops(L, N))
+                ops.upconv_blur_fwd(t, pre, L["_d"], L["noise"], L["noise_w"], L["bias"],
+                                    act_out=ACT_LRELU_S2)
             else:
-                ops.conv3x3(x, L["wf"], pre, cout=4 * cout if L["up"] else cout, act_in=act,
+                ops.conv3x3(x, L["wf"], pre, cout=4 * cout if L["up"] else cout,
                             in_scale=L["_s"], out_scale=L["_d"], noise=L["noise"],
-                            noise_w=L["noise_w"], bias=L["bias"], shuffle_out=L["up"],
-                            flops=self._alg_flops(L, N))
-            L["_x"], L["_xact"], L["_pre"] = x, act, pre
-            x, act = pre, ACT_LRELU_S2
+                            noise_w=L["noise_w"], bias=L["bias"], act_out=ACT_LRELU_S2,
+                            shuffle_out=L["up"], flops=self._alg_flops(L, N))
+            L["_x"], L["_pre"] = x, pre  # _pre holds the activation a = lrelu(pre)·√2
+            x = pre
             if not L["up"]:  # every non-up conv closes a resolution → ToRGB
                 t = self.torgbs[ti]
                 out = ws.get(f"g.rgb{ti}", (N, 3, r, r), torch.float32)
-                ops.torgb_fwd(pre, t["_s"], t["wr"], t["bias"], rgb, out)
+                ops.torgb_fwd(pre, t["_s"], t["wr"], t["bias"], rgb, out, act_in=ACT_NONE)
                 t["_pre"], t["_skip"] = pre, rgb
                 rgb = out
                 ti += 1
@@ -167,7 +169,8 @@ class SynthesisNet:
                     acc = False
                 else:
                     acc = True
-                ops.torgb_bwd(g_rgb, pre, t["_s"], t["wr"], g_a_next, gs_t, accumulate=acc)
+                ops.torgb_bwd(g_rgb, pre, t["_s"], t["wr"], g_a_next, gs_t, accumulate=acc,
+                              act_in=ACT_NONE)
                 t["_gs"] = gs_t
                 if t["_skip"] is not None:
                     g_skip = ws.get(f"g.gskip{ti}", (N, 3, r // 2, r // 2), torch.float32)
@@ -183,7 +186,7 @@ class SynthesisNet:
             else:
                 gy = ws.get(f"g.gy{i}", (N, r, r, cout), T)
             ops.bias_act_bwd(g_a_next, pre, L["noise"], L["noise_w"], L["bias"], L["_d"], gy, q,
-                             unshuffle=L["up"] and not sub)
+                             unshuffle=L["up"] and not sub, from_act=True)
             # dgrad + style sdot
             gs = ws.get(f"g.gs{i}", (N, cin), torch.float32)
             ops.zero_(gs)
@@ -195,11 +198,11 @@ class SynthesisNet:
             if sub:
                 gt = ws.get(f"g.gt{i}", (N, r + 1, r + 1, cout), T)
                 ops.upconv_blur_bwd(gy, gt)
-                ops.upconv_dgrad(gt, L["wd"], gx, cin, L["_x"], L["_xact"], L["_s"], gs,
+                ops.upconv_dgrad(gt, L["wd"], gx, cin, L["_x"], ACT_NONE, L["_s"], gs,
                                  flops=self._alg_flops(L, N))
             else:
                 ops.conv3x3(gy, L["wd"], gx, cout=cin, out_scale=L["_s"], aux_x=L["_x"],
-                            act_aux=L["_xact"], sdot=gs, flops=self._alg_flops(L, N))
+                            act_aux=ACT_NONE, sdot=gs, flops=self._alg_flops(L, N))
             ops.demod_bwd(q, L["_d"], L["wsq"], L["_s"], gs)
             L["_gs"] = gs
             g_a_next = gx

@@ -115,10 +115,11 @@ int mia_vgg_conv_dgrad(const void* g, const void* w_t, void* gx, int N, int H, i
 int mia_upconv_kpad(int cin, int phase, int dtype);
 int mia_upconv_fwd(const void* x, const void* const* w_phase, void* t_out, int N, int R, int Cin,
                    int Cout, int act_in, const float* style, int dtype, void* stream);
-/* pre = demod·Blur(T) + noise_w·noise + bias, (N, 2R, 2R, C) (rosinality Blur pad (1,1)). */
+/* pre = demod·Blur(T) + noise_w·noise + bias, (N, 2R, 2R, C) (rosinality Blur pad (1,1));
+ * act_out = MIA_ACT_LRELU_S2 stores the StyledConv activation lrelu(pre)·√2 instead. */
 int mia_upconv_blur_fwd(const void* t, void* pre, const float* demod, const float* noise,
-                        float noise_w, const float* bias, int N, int R, int C, int dtype,
-                        void* stream);
+                        float noise_w, const float* bias, int N, int R, int C, int act_out,
+                        int dtype, void* stream);
 /* Adjoint of the blur: gT (N, 2R+1, 2R+1, C) from gy = demod·∂L/∂pre (N, 2R, 2R, C). */
 int mia_upconv_blur_bwd(const void* gy, void* gt, int N, int R, int C, int dtype, void* stream);
 /* Input gradient of the transposed conv = stride-2, pad-0 3×3 conv over gT with w_t =
@@ -134,25 +135,27 @@ int mia_bias_act_fwd(const void* x, const float* noise, float noise_w, const flo
                      void* y, int N, int H, int W, int C, int dtype, void* stream);
 /* StyledConv backward front (K4 bwd + demod): from g_a = ∂L/∂a and pre:
  *   g_pre = g_a·lrelu_s2'(pre); q[n][c] += Σ_p g_pre·(pre − nw·noise − b); gy = g_pre·demod[n][c]
- * gy is written un-shuffled (N,H/2,W/2,4C) when unshuffle=1 (up-conv dgrad input). */
+ * gy is written un-shuffled (N,H/2,W/2,4C) when unshuffle=1 (up-conv dgrad input).
+ * from_act=1: the stored tensor is the activation a = lrelu(pre)·√2 (pre is recovered as
+ * a / lrelu'(a), the sign of a and pre being equal). */
 int mia_bias_act_bwd(const void* g_a, const void* pre, const float* noise, float noise_w,
                      const float* bias, const float* demod, void* gy, float* q, int N, int H,
-                     int W, int C, int unshuffle, int dtype, void* stream);
+                     int W, int C, int unshuffle, int from_act, int dtype, void* stream);
 /* upfirdn2d (K3) on fp32 NCHW planes, separable 1-D kernel (taps ≤ 8):
  * zero-insert `up`, pad (pad0,pad1), correlate with the flipped kernel, keep every `down`-th. */
 int mia_upfirdn2d_fwd(const float* x, float* y, int planes, int H, int W, const float* k1d,
                       int ktaps, int up, int down, int pad0, int pad1, void* stream);
 int mia_upfirdn2d_bwd(const float* gy, float* gx, int planes, int H, int W, const float* k1d,
                       int ktaps, int up, int down, int pad0, int pad1, void* stream);
-/* ToRGB (K5): rgb = Σ_ci act(pre)·wr[c][ci]·s[n][ci] + bias[c] (+ upfirdn2d(skip, up 2, pad (2,1)))
+/* ToRGB (K5): rgb = Σ_ci act_in(x)·wr[c][ci]·s[n][ci] + bias[c] (+ upfirdn2d(skip, up 2, pad (2,1)))
  * pre NHWC (dtype), rgb/skip fp32 NCHW (N,3,H,W)/(N,3,H/2,W/2). */
 int mia_torgb_fwd(const void* pre, const float* style, const float* wr, const float* bias,
-                  const float* skip, float* rgb, int N, int H, int W, int Cin, int dtype,
-                  void* stream);
+                  const float* skip, float* rgb, int N, int H, int W, int Cin, int act_in,
+                  int dtype, void* stream);
 /* ToRGB backward: u = Σ_c g[c]·wr[c][ci]; g_a (+)= s·u; gs[n][ci] += Σ_p act(pre)·u. */
 int mia_torgb_bwd(const float* g_rgb, const void* pre, const float* style, const float* wr,
-                  void* g_a, float* gs, int N, int H, int W, int Cin, int accumulate, int dtype,
-                  void* stream);
+                  void* g_a, float* gs, int N, int H, int W, int Cin, int accumulate, int act_in,
+                  int dtype, void* stream);
 /* MaxPool 2x2/2 (K8) NHWC, ceil_mode for odd sizes (code/vgg.py:14,18,24). */
 int mia_maxpool2_fwd(const void* x, void* y, int N, int H, int W, int C, int ceil_mode,
                      int dtype, void* stream);

@@ -113,8 +113,11 @@ def test_modconv_fwd(cuda, dtype, up):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("up", [False, True])
-def test_modconv_bwd_input_and_style(cuda, dtype, up):
-    """bias_act_bwd + dgrad(sdot) + demod_bwd reproduce autograd's ∂x and ∂s of a StyledConv."""
+@pytest.mark.parametrize("store_act", [False, True])
+def test_modconv_bwd_input_and_style(cuda, dtype, up, store_act):
+    """bias_act_bwd + dgrad(sdot) + demod_bwd reproduce autograd's ∂x and ∂s of a StyledConv.
+    store_act: the layout SynthesisNet uses — the producing epilogue stores a = lrelu(pre)·√2 and
+    the backward recovers pre from it (from_act)."""
     N, cin, cout, R = 2, 32, 64, 8
     p, wlat, x, noise, bias = _modconv_setup(5, N, cin, cout, R)
     Ro = 2 * R if up else R
@@ -159,10 +162,11 @@ def test_modconv_bwd_input_and_style(cuda, dtype, up):
     bz = bias.to(cuda)
     ops.conv3x3(xd, layouts.fwd_matrix(wm, dtype).to(cuda), pre_d, cout=4 * cout if up else cout,
                 act_in=ops.ACT_LRELU_S2, in_scale=s, out_scale=demod, noise=nz, noise_w=0.1,
-                bias=bz, shuffle_out=up)
+                bias=bz, shuffle_out=up, act_out=ops.ACT_LRELU_S2 if store_act else ops.ACT_NONE)
     q = torch.zeros(N, cout, device=cuda)
     gy = torch.empty((N, R, R, 4 * cout) if up else (N, R, R, cout), dtype=dtype, device=cuda)
-    ops.bias_act_bwd(nhwc(g_a, dtype).to(cuda), pre_d, nz, 0.1, bz, demod, gy, q, unshuffle=up)
+    ops.bias_act_bwd(nhwc(g_a, dtype).to(cuda), pre_d, nz, 0.1, bz, demod, gy, q, unshuffle=up,
+                     from_act=store_act)
     gs = torch.zeros(N, cin, device=cuda)
     gx = torch.empty(N, R, R, cin, dtype=dtype, device=cuda)
     ops.conv3x3(gy, layouts.dgrad_matrix(wm, dtype).to(cuda), gx, cout=cin, out_scale=s, aux_x=xd,
@@ -170,6 +174,7 @@ def test_modconv_bwd_input_and_style(cuda, dtype, up):
     ops.demod_bwd(q, demod, wsq, s, gs)
     torch.cuda.synchronize()
     tol = 1e-4 if dtype == torch.float32 else 5e-2
+    assert rel_err(nchw(pre_d), (act if store_act else pre).detach()) < tol
     assert rel_err(nchw(gx), gx_ref) < tol
     assert rel_err(gs, gs_ref) < tol
 
@@ -222,7 +227,8 @@ def test_upfirdn2d(cuda, up, down, pad):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("cin", [32, 128, 512])
-def test_torgb_fwd_bwd(cuda, dtype, cin):
+@pytest.mark.parametrize("stored", ["pre", "act"])
+def test_torgb_fwd_bwd(cuda, dtype, cin, stored):
     g = torch.Generator().manual_seed(cin)
     N, R = 2, 8
     pre = torch.randn(N, cin, R, R, generator=g)
@@ -239,14 +245,15 @@ def test_torgb_fwd_bwd(cuda, dtype, cin):
     out = out + stylegan2_ref.upfirdn2d(skip, up, up=2, pad=(2, 1))
     grgb = torch.randn(out.shape, generator=g, dtype=torch.float64)
     gpre, gsr = torch.autograd.grad((out * grgb).sum(), [a, s])  # ∂L/∂activation, ∂L/∂s
-    pd = nhwc(pre, dtype).to(cuda)
+    act_in = ops.ACT_NONE if stored == "act" else ops.ACT_LRELU_S2
+    pd = nhwc(a.detach() if stored == "act" else pre, dtype).to(cuda)
     rgb = torch.empty(N, 3, R, R, device=cuda)
     sd = s.detach().float().to(cuda)
     wrd = wr.float().to(cuda)
-    ops.torgb_fwd(pd, sd, wrd, b.float().to(cuda), skip.float().to(cuda), rgb)
+    ops.torgb_fwd(pd, sd, wrd, b.float().to(cuda), skip.float().to(cuda), rgb, act_in=act_in)
     ga = torch.full((N, R, R, cin), 0.25, dtype=dtype, device=cuda)
     gs = torch.zeros(N, cin, device=cuda)
-    ops.torgb_bwd(grgb.float().to(cuda), pd, sd, wrd, ga, gs, accumulate=True)
+    ops.torgb_bwd(grgb.float().to(cuda), pd, sd, wrd, ga, gs, accumulate=True, act_in=act_in)
     torch.cuda.synchronize()
     tol = 1e-5 if dtype == torch.float32 else 2e-2
     assert rel_err(rgb, out.detach()) < tol
@@ -316,7 +323,8 @@ def test_adam_step(cuda):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("N,cin,cout,R", [(3, 64, 128, 8), (2, 512, 512, 4), (1, 128, 64, 16)])
-def test_upconv_subpixel_fwd_bwd(cuda, dtype, N, cin, cout, R):
+@pytest.mark.parametrize("store_act", [False, True])
+def test_upconv_subpixel_fwd_bwd(cuda, dtype, N, cin, cout, R, store_act):
     """Sub-pixel transposed conv (4 phase GEMMs, one launch) + fused blur/demod/noise/bias, and the
     backward (bias_act_bwd → blur adjoint → stride-2 dgrad with style sdot → demod_bwd) against
     autograd through the oracle's per-sample conv_transpose2d + upfirdn2d formulation."""
@@ -348,22 +356,71 @@ def test_upconv_subpixel_fwd_bwd(cuda, dtype, N, cin, cout, R):
     xd = nhwc(x, dtype).to(cuda)
     wph = [m.to(cuda) for m in layouts.upconv_subpixel_matrices(ws_, dtype)]
     t = torch.empty(N, 2 * R + 1, 2 * R + 1, cout, dtype=dtype, device=cuda)
-    ops.upconv_fwd(xd, wph, t, cout, act_in=ops.ACT_LRELU_S2, style=s)
+    # store_act: the input arrives activated (SynthesisNet layout) and the output is stored as
+    # a = lrelu(pre)·√2
+    act_x = ops.ACT_NONE if store_act else ops.ACT_LRELU_S2
+    if store_act:
+        xd = nhwc(xa.detach(), dtype).to(cuda)
+    ops.upconv_fwd(xd, wph, t, cout, act_in=act_x, style=s)
     nz, bz = noise.reshape(-1).to(cuda), bias.to(cuda)
     pre = torch.empty(N, 2 * R, 2 * R, cout, dtype=dtype, device=cuda)
-    ops.upconv_blur_fwd(t, pre, demod, nz, 0.1, bz)
+    ops.upconv_blur_fwd(t, pre, demod, nz, 0.1, bz,
+                        act_out=ops.ACT_LRELU_S2 if store_act else ops.ACT_NONE)
     q = torch.zeros(N, cout, device=cuda)
     gy = torch.empty_like(pre)
-    ops.bias_act_bwd(nhwc(g_a, dtype).to(cuda), pre, nz, 0.1, bz, demod, gy, q)
+    ops.bias_act_bwd(nhwc(g_a, dtype).to(cuda), pre, nz, 0.1, bz, demod, gy, q,
+                     from_act=store_act)
     gt = torch.empty_like(t)
     ops.upconv_blur_bwd(gy, gt)
     gs = torch.zeros(N, cin, device=cuda)
     gx = torch.empty(N, R, R, cin, dtype=dtype, device=cuda)
     ops.upconv_dgrad(gt, layouts.upconv_dgrad_matrix(ws_, dtype).to(cuda), gx, cin, xd,
-                     ops.ACT_LRELU_S2, s, gs)
+                     act_x, s, gs)
     ops.demod_bwd(q, demod, wsq, s, gs)
     torch.cuda.synchronize()
     tol = {torch.float32: 1e-4, torch.float16: 6e-2, torch.bfloat16: 1.2e-1}[dtype]
-    assert rel_err(nchw(pre), pre_ref.detach()) < tol
+    assert rel_err(nchw(pre), (act if store_act else pre_ref).detach()) < tol
     assert rel_err(nchw(gx), gx_ref) < tol
     assert rel_err(gs, gs_ref) < 2 * tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("kind", ["plain", "modconv", "dgrad_sdot"])
+@pytest.mark.parametrize("tile", ["1", "2"])
+def test_conv_large_m_tiles(cuda, dtype, kind, tile, monkeypatch):
+    """Large-M launches on the default 128×128 tile and on the 256×128 3-stage DMA-ring tile
+    (MIA_CONV_TILE=2), checked against torch's conv."""
+    monkeypatch.setenv("MIA_CONV_TILE", tile)
+    g = torch.Generator().manual_seed(17)
+    N, H, Cin, Cout = 8, 128, 64, 128
+    x = torch.randn(N, Cin, H, H, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)
+    xd = nhwc(x, dtype).to(cuda)
+    xq = x.to(dtype).float().to(cuda)
+    wq = w.to(dtype).float().to(cuda)
+    y = torch.empty(N, H, H, Cout, dtype=dtype, device=cuda)
+    if kind == "plain":
+        b = torch.randn(Cout, generator=g).to(cuda)
+        ref = torch.relu(F.conv2d(xq, wq, b, padding=1))
+        ops.conv3x3(xd, layouts.fwd_matrix(w, dtype).to(cuda), y, cout=Cout, bias=b,
+                    act_out=ops.ACT_RELU)
+    elif kind == "modconv":
+        s = (torch.rand(N, Cin, generator=g) + 0.5).to(cuda)
+        d = (torch.rand(N, Cout, generator=g) + 0.5).to(cuda)
+        xa = F.leaky_relu(xq, 0.2) * math.sqrt(2) * s.view(N, Cin, 1, 1)
+        ref = F.conv2d(xa, wq, padding=1) * d.view(N, Cout, 1, 1)
+        ops.conv3x3(xd, layouts.fwd_matrix(w, dtype).to(cuda), y, cout=Cout,
+                    act_in=ops.ACT_LRELU_S2, in_scale=s, out_scale=d)
+    else:
+        # input-gradient conv (Cin_g = 64 → Cout_g = 128 roles) with style sdot vs aux tensor
+        aux = torch.randn(N, Cout, H, H, generator=g)
+        ref = F.conv2d(xq, wq, padding=1)
+        sdot_ref = (ref * (F.leaky_relu(aux.to(dtype).float(), 0.2) * math.sqrt(2)).to(cuda)).sum((2, 3))
+        sd = torch.zeros(N, Cout, device=cuda)
+        ops.conv3x3(xd, layouts.fwd_matrix(w, dtype).to(cuda), y, cout=Cout,
+                    aux_x=nhwc(aux, dtype).to(cuda), act_aux=ops.ACT_LRELU_S2, sdot=sd)
+    torch.cuda.synchronize()
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    assert rel_err(nchw(y), ref) < tol
+    if kind == "dgrad_sdot":
+        assert rel_err(sd, sdot_ref) < tol

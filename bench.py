@@ -9,6 +9,7 @@ region. Rank 0 prints ONE JSON line.
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -44,7 +45,7 @@ def parse():
     ap.add_argument("--pgd-steps", type=int, default=20)
     ap.add_argument("--dtype", default="fp16", choices=list(DT))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-steps", type=int, default=1)
+    ap.add_argument("--cpu-sample-steps", type=int, default=10)
     ap.add_argument("--no-roofline", action="store_true")
     return ap.parse_args()
 
@@ -76,6 +77,23 @@ def cpu_baseline(size, pgd_steps, sample_steps):
             "sample": f"oracle fp32 CPU, 1 image @{size}², {sample_steps} PGD step(s) timed "
                       f"({dt:.2f} s/step) extrapolated to PGD-{pgd_steps}; "
                       f"torch.set_num_threads({cores})"}
+
+
+def pmc_traffic(dtype, batch, size, pgd_steps):
+    """HBM bytes per conv_kernel launch from the newest committed PMC profile of this exact
+    workload (profiles/rNN_bench_<dtype>_b<batch>.json, written by profiles/summarize_rocprof.py
+    from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench; FETCH_SIZE ×2 per the
+    gfx950 correction). PMC counters cannot be read from inside the timed process, hence a file."""
+    if size != 256 or pgd_steps != 20:
+        return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_bench_{dtype}_b{batch}.json")))
+    for f in reversed(files):
+        with open(f) as fh:
+            d = json.load(fh)
+        v = d.get("conv_kernel", {}).get("hbm_bytes_per_launch")
+        if v:
+            return v, os.path.relpath(f, ROOT)
+    return None, None
 
 
 def main():
@@ -148,7 +166,8 @@ def main():
                    "pgd_steps": args.pgd_steps, "parallelism": f"dp{world}",
                    "algorithmic_gflop_per_image_step": flops_img_step / 1e9,
                    "effective_tflops": flops_img_step * B * args.pgd_steps * world
-                   / (elapsed / args.steps) / 1e12},
+                   / (elapsed / args.steps) / 1e12,
+                   "peak_hbm_gb_per_gpu": torch.cuda.max_memory_allocated(dev) / 1e9},
     }
     if prof:
         durs = [a.elapsed_time(b) for a, b, _ in prof]  # ms
@@ -157,10 +176,13 @@ def main():
         n = len(prof)
         ach = tot_fl / (tot_ms * 1e-3) / 1e12
         peak = PEAK_TFLOPS[args.dtype]
+        traffic, src = pmc_traffic(args.dtype, B, S, args.pgd_steps)
         out["roofline"] = {
-            "kernel": "mia::conv3x3_kernel (all launches: StyledConv fwd/dgrad, VGG fwd/dgrad)",
+            "kernel": "mia::conv_kernel<...> (every instantiation and launch: StyledConv fwd, "
+                      "sub-pixel up-conv, dgrads, VGG fwd/dgrad)",
             "bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
-            "traffic": None, "launches": n, "avg_launch_us": tot_ms / n * 1e3,
+            "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": src,
+            "launches": n, "avg_launch_us": tot_ms / n * 1e3,
             "algorithmic_gflop_per_launch": tot_fl / n / 1e9,
             "share_of_step_time": tot_ms / (elapsed * 1e3)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

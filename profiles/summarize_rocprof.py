@@ -1,0 +1,110 @@
+"""Summarize a rocprofv3 run of bench.py into the committed per-round profile files.
+
+    python profiles/summarize_rocprof.py <kernel_stats.csv> [--fetch counter_collection.csv]
+        [--write counter_collection.csv] [--steps S] --out profiles/rNN_<name>
+
+Writes <out>.md (per-kernel table, time per bench step) and <out>.json (the dominant kernel's
+aggregate: every conv_kernel<...> instantiation is the same implicit-GEMM conv, so the launch
+average is Σ duration / Σ calls over them — the figure bench.py's live HIP-event roofline must
+agree with). HBM traffic per launch follows /opt/skills/guides/MI355X_MICROARCH.md §HBM:
+FETCH_SIZE and WRITE_SIZE come from separate --pmc passes, are in KiB, and FETCH_SIZE is doubled
+on gfx950 (it tallies 128-B requests at 64 B).
+"""
+import argparse
+import csv
+import json
+import re
+from collections import defaultdict
+
+CONV = re.compile(r"conv_kernel")
+
+
+def short(name):
+    m = re.match(r"_ZN3mia\d+(\w+?)I", name)
+    if m:
+        base = re.sub(r"^\d+", "", m.group(1))
+        tile = re.search(r"TileILi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)", name)
+        flags = re.findall(r"ELb([01])", name)
+        extra = ""
+        if tile:
+            wm, wn, fm, fn, st = map(int, tile.groups())
+            extra = f"<{wm * fm * 16}x{wn * fn * 16},{st}st,pro={flags[0]},smallc={flags[1]}>"
+        elif "Lb1" in name or "Lb0" in name:
+            extra = "<fwd>" if "Lb1" in name else "<bwd>"
+        return base + extra
+    return name.split("(")[0]
+
+
+def read_stats(path):
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            rows.append((r["Name"], int(r["Calls"]), int(r["TotalDurationNs"])))
+    return rows
+
+
+def read_pmc(path, counter):
+    per = defaultdict(lambda: [0, 0.0])
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] != counter:
+                continue
+            k = r["Kernel_Name"]
+            per[k][0] += 1
+            per[k][1] += float(r["Counter_Value"]) * 1024.0  # KiB → bytes
+    return per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("stats")
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--steps", type=int, default=3, help="bench steps in the trace (warmup+timed)")
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--title", default="")
+    a = ap.parse_args()
+    rows = read_stats(a.stats)
+    tot = sum(r[2] for r in rows)
+    conv_calls = sum(c for n, c, t in rows if CONV.search(n))
+    conv_ns = sum(t for n, c, t in rows if CONV.search(n))
+    out = {"source": a.stats, "bench_steps_in_trace": a.steps,
+           "kernel_ms_per_step": tot / 1e6 / a.steps,
+           "conv_kernel": {"launches": conv_calls, "total_ms": conv_ns / 1e6,
+                           "avg_launch_us": conv_ns / conv_calls / 1e3 if conv_calls else None,
+                           "share_of_kernel_time": conv_ns / tot}}
+    lines = [f"# {a.title}", "", f"rocprofv3 --kernel-trace --stats; {a.steps} bench steps in the "
+             f"trace; kernel time per step {tot / 1e6 / a.steps:.1f} ms", "",
+             "| kernel | calls/step | ms/step | avg µs | share |", "|---|---|---|---|---|"]
+    for n, c, t in sorted(rows, key=lambda r: -r[2]):
+        lines.append(f"| `{short(n)}` | {c / a.steps:.0f} | {t / 1e6 / a.steps:.2f} | "
+                     f"{t / c / 1e3:.1f} | {100 * t / tot:.2f}% |")
+    lines += ["", f"conv_kernel (all instantiations): {conv_calls} launches, average "
+              f"{out['conv_kernel']['avg_launch_us']:.1f} µs, {100 * conv_ns / tot:.1f}% of kernel time"]
+    if a.fetch and a.write:
+        fe, wr = read_pmc(a.fetch, "FETCH_SIZE"), read_pmc(a.write, "WRITE_SIZE")
+        fb = sum(v[1] for k, v in fe.items() if CONV.search(k))
+        fl = sum(v[0] for k, v in fe.items() if CONV.search(k))
+        wb = sum(v[1] for k, v in wr.items() if CONV.search(k))
+        wl = sum(v[0] for k, v in wr.items() if CONV.search(k))
+        per = 2.0 * fb / fl + wb / wl
+        out["conv_kernel"]["hbm_bytes_per_launch"] = per
+        out["conv_kernel"]["fetch_bytes_per_launch_x2"] = 2.0 * fb / fl
+        out["conv_kernel"]["write_bytes_per_launch"] = wb / wl
+        out["conv_kernel"]["pmc_launches"] = [fl, wl]
+        lines += ["", "PMC (separate passes, FETCH_SIZE×2 per the gfx950 correction):",
+                  f"conv_kernel HBM bytes per launch = {per / 1e6:.1f} MB "
+                  f"(fetch {2 * fb / fl / 1e6:.1f} MB, write {wb / wl / 1e6:.1f} MB, "
+                  f"{fl} launches)", "", "| kernel | fetch MB/launch (×2) | write MB/launch |",
+                  "|---|---|---|"]
+        for k in sorted(fe, key=lambda k: -fe[k][1]):
+            w = wr.get(k, [1, 0.0])
+            lines.append(f"| `{short(k)}` | {2 * fe[k][1] / fe[k][0] / 1e6:.2f} | "
+                         f"{w[1] / max(w[0], 1) / 1e6:.2f} |")
+    open(a.out + ".md", "w").write("\n".join(lines) + "\n")
+    json.dump(out, open(a.out + ".json", "w"), indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

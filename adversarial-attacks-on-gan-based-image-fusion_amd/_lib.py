@@ -31,6 +31,19 @@ class ConvArgs(ctypes.Structure):
     ]
 
 
+class GemmSeg(ctypes.Structure):
+    """Mirror of ``mia_gemm_seg``."""
+    _fields_ = [("A", P), ("B", P), ("sam", c_int64), ("sak", c_int64), ("sbk", c_int64),
+                ("sbn", c_int64), ("K", c_int)]
+
+
+class GemmGroup(ctypes.Structure):
+    """Mirror of ``mia_gemm_group``."""
+    _fields_ = [("C", P), ("bias", P), ("scm", c_int64), ("scn", c_int64), ("M", c_int),
+                ("N", c_int), ("alpha", c_float), ("beta", c_float), ("nseg", c_int),
+                ("seg", GemmSeg * 2)]
+
+
 # name -> (restype, argtypes); every function declared in include/miattack.h
 SIGNATURES = {
     "mia_version": (c_int, []),
@@ -78,6 +91,7 @@ SIGNATURES = {
     "mia_adam_step": (c_int, [P, P, P, P, c_int64, c_float, c_float, c_float, c_float, c_int, P]),
     "mia_gemm_f32": (c_int, [c_int, c_int, c_int, c_float, P, c_int64, c_int64, P, c_int64,
                              c_int64, c_float, P, c_int64, c_int64, P, P]),
+    "mia_gemm_f32_grouped": (c_int, [ctypes.POINTER(GemmGroup), c_int, P]),
     "mia_style_demod": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
     "mia_demod_bwd": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
     "mia_repeat": (c_int, [P, P, c_int64, c_int, P]),

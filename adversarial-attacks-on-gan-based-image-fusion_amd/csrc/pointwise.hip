@@ -108,96 +108,147 @@ __global__ void bias_act_bwd_kernel(const T* __restrict__ g_a, const T* __restri
 // demodulation scale, noise injection and bias: pre = demod·blur(T) + nw·noise + b.
 __constant__ float kBlur4[4] = {0.25f, 0.75f, 0.75f, 0.25f};
 
-// Both directions are the same separable 4-tap FIR evaluated on 2×2 output quads: a thread loads
-// the 5×5 input neighbourhood of its quad once (6.25 vector loads per output instead of 16),
-// filters rows then columns, for one 8-channel (16-byte) vector.
-//   forward : out = pre (N,2R,2R,C),    in = T  (N,2R+1,2R+1,C), input row of quad row 2q is 2q−1
-//   backward: out = gT (N,2R+1,2R+1,C), in = gy (N,2R,2R,C),     input row of quad row 2q is 2q−2
+// Both directions are the same separable 4-tap FIR (factor-2 up-sampling phases). A thread owns a
+// 2-wide × 2·KQ-tall output strip of one 8-channel (16-byte) vector and streams down the 2·KQ+3
+// input rows it needs: each row is loaded once (5 vectors), filtered horizontally into the strip's
+// 2 columns, and accumulated into the ≤ 4 output rows it feeds; an output row is stored as soon as
+// its 4th input row has been added (≈ 3.4 loads per output instead of 16 for a direct 4×4 FIR).
+//   forward : out = pre (N,2R,2R,C),    in = T  (N,2R+1,2R+1,C), input row of output row 0 is −1
+//   backward: out = gT (N,2R+1,2R+1,C), in = gy (N,2R,2R,C),     input row of output row 0 is −2
 // (the adjoint flips the taps; the kernel is symmetric so the weights are the same).
-template <typename T, bool FWD>
-__global__ void blur4_quad_kernel(const T* __restrict__ in, T* __restrict__ out,
-                                  const float* __restrict__ demod, const float* __restrict__ noise,
-                                  float nw, const float* __restrict__ bias, int N, int R, int C,
-                                  int act_out) {
+constexpr int kBlurKQ = 4;
+
+// V consecutive fp32 values (V = 8 or 4) with 16-byte loads
+template <int V>
+__device__ __forceinline__ void load8f_or_4(const float* p, float (&v)[V]) {
+#pragma unroll
+  for (int q = 0; q < V / 4; ++q) {
+    const f32x4 t = *(const f32x4*)(p + 4 * q);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[4 * q + e] = t[e];
+  }
+}
+
+template <typename T, bool FWD, bool NOISE>
+__global__ __launch_bounds__(256) void blur4_strip_kernel(
+    const T* __restrict__ in, T* __restrict__ out, const float* __restrict__ demod,
+    const float* __restrict__ noise, float nw, const float* __restrict__ bias, int N, int R, int C,
+    int act_out) {
   typedef typename Vec<T>::type VT;
   constexpr int V = Vec<T>::N;
+  constexpr int KQ = kBlurKQ, OR = 2 * KQ, IR = 2 * KQ + 3;
   const int Hin = FWD ? 2 * R + 1 : 2 * R;
   const int Hout = FWD ? 2 * R : 2 * R + 1;
-  const int Q = (Hout + 1) / 2;  // quads per side
+  const int Q = (Hout + 1) / 2;     // 2-wide columns per row
+  const int SY = (Hout + OR - 1) / OR;  // strips per column
   const int off0 = FWD ? -1 : -2;
   const int nc = C / V;
-  const int64_t total = (int64_t)N * Q * Q * nc;
+  const int64_t total = (int64_t)N * SY * Q * nc;
   for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
     const int cv = (int)(i % nc);
-    const int64_t qp = i / nc;
-    const int qx = (int)(qp % Q);
-    const int qy = (int)((qp / Q) % Q);
-    const int n = (int)(qp / ((int64_t)Q * Q));
-    float acc[2][2][V];
+    const int64_t r1 = i / nc;
+    const int qx = (int)(r1 % Q);
+    const int64_t r2 = r1 / Q;
+    const int sy = (int)(r2 % SY);
+    const int n = (int)(r2 / SY);
+    const int x0 = 2 * qx + off0, y0 = sy * OR + off0;
+    const int oy0 = sy * OR, ox0 = 2 * qx;
+    float dm[V], bs[V];
+    if (FWD) {
+      load8f_or_4(demod + (size_t)n * C + cv * V, dm);
+      if (bias) {
+        load8f_or_4(bias + cv * V, bs);
+      } else {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+        for (int e = 0; e < V; ++e) bs[e] = 0.f;
+      }
+    }
+    const T* base = in + (size_t)n * Hin * Hin * C + cv * V;
+    T* obase = out + (size_t)n * Hout * Hout * C + cv * V;
+    // noise of the whole strip up front: a global load issued between the pipelined row loads
+    // would force a vmcnt(0) drain (the counter retires in order)
+    // (NOISE is a template flag so that no branch separates these loads from the row loads)
+    float nzs[OR][2];
+#pragma unroll
+    for (int a = 0; a < OR; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b)
+        nzs[a][b] = NOISE ? noise[min(oy0 + a, Hout - 1) * Hout + min(ox0 + b, Hout - 1)] : 0.f;
+    float acc[OR][2][V];
+    // software pipeline: rows rl+1, rl+2 are in flight while row rl is filtered. Loads are unconditional
+    // (clamped addresses) and out-of-range taps are zeroed afterwards, so nothing serialises them.
+    int xc[5];
+    bool xv[5];
 #pragma unroll
-        for (int e = 0; e < V; ++e) acc[a][b][e] = 0.f;
-    const int y0 = 2 * qy + off0, x0 = 2 * qx + off0;
+    for (int lc = 0; lc < 5; ++lc) {
+      const int xx = x0 + lc;
+      xv[lc] = xx >= 0 && xx < Hin;
+      xc[lc] = min(max(xx, 0), Hin - 1);
+    }
+    VT nx1[5], nx2[5];
 #pragma unroll
-    for (int lr = 0; lr < 5; ++lr) {
-      const int yy = y0 + lr;
-      if (yy < 0 || yy >= Hin) continue;
+    for (int lc = 0; lc < 5; ++lc) {
+      nx1[lc] = *(const VT*)(base + ((size_t)min(max(y0, 0), Hin - 1) * Hin + xc[lc]) * C);
+      nx2[lc] = *(const VT*)(base + ((size_t)min(max(y0 + 1, 0), Hin - 1) * Hin + xc[lc]) * C);
+    }
+#pragma unroll
+    for (int rl = 0; rl < IR; ++rl) {
+      const int yy = y0 + rl;
+      const bool rv = yy >= 0 && yy < Hin;
+      VT v[5];
+#pragma unroll
+      for (int lc = 0; lc < 5; ++lc) {
+        v[lc] = nx1[lc];
+        nx1[lc] = nx2[lc];
+      }
+      if (rl + 2 < IR) {
+        const int yc = min(max(yy + 2, 0), Hin - 1);
+#pragma unroll
+        for (int lc = 0; lc < 5; ++lc)
+          nx2[lc] = *(const VT*)(base + ((size_t)yc * Hin + xc[lc]) * C);
+      }
+#pragma unroll
+      for (int lc = 0; lc < 5; ++lc)
+        if (!(rv && xv[lc]))
+#pragma unroll
+          for (int e = 0; e < V; ++e) v[lc][e] = (T)0.f;
       float h[2][V];
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int e = 0; e < V; ++e) h[b][e] = 0.f;
-      const T* rowp = in + (((size_t)n * Hin + yy) * Hin) * C + cv * V;
+        for (int e = 0; e < V; ++e)
+          h[b][e] = kBlur4[0] * to_f(v[b][e]) + kBlur4[1] * to_f(v[b + 1][e]) +
+                    kBlur4[2] * to_f(v[b + 2][e]) + kBlur4[3] * to_f(v[b + 3][e]);
 #pragma unroll
-      for (int lc = 0; lc < 5; ++lc) {
-        const int xx = x0 + lc;
-        if (xx < 0 || xx >= Hin) continue;
-        const VT v = *(const VT*)(rowp + (size_t)xx * C);
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const int j = lc - b;
-          if (j < 0 || j > 3) continue;
-#pragma unroll
-          for (int e = 0; e < V; ++e) h[b][e] += kBlur4[j] * to_f(v[e]);
-        }
-      }
-#pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        const int j = lr - a;
+      for (int a = 0; a < OR; ++a) {
+        const int j = rl - a;
         if (j < 0 || j > 3) continue;
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
-          for (int e = 0; e < V; ++e) acc[a][b][e] += kBlur4[j] * h[b][e];
-      }
-    }
-    float dm[V], bs[V];
-    if (FWD) {
+          for (int e = 0; e < V; ++e)
+            acc[a][b][e] = (j == 0 ? 0.f : acc[a][b][e]) + kBlur4[j] * h[b][e];
+        if (j != 3) continue;
+        // output row a is complete
+        const int oy = oy0 + a;
+        if (oy >= Hout) continue;
 #pragma unroll
-      for (int e = 0; e < V; ++e) {
-        dm[e] = demod[(size_t)n * C + cv * V + e];
-        bs[e] = bias ? bias[cv * V + e] : 0.f;
-      }
-    }
+        for (int b = 0; b < 2; ++b) {
+          const int ox = ox0 + b;
+          if (ox >= Hout) continue;
+          VT o;
+          const float nz = nw * nzs[a][b];
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      const int oy = 2 * qy + a;
-      if (oy >= Hout) continue;
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int ox = 2 * qx + b;
-        if (ox >= Hout) continue;
-        VT o;
-        const float nz = (FWD && noise) ? nw * noise[oy * Hout + ox] : 0.f;
-#pragma unroll
-        for (int e = 0; e < V; ++e)
-          o[e] = from_f<T>(FWD ? (act_out ? lrelu_s2(acc[a][b][e] * dm[e] + nz + bs[e])
-                                          : acc[a][b][e] * dm[e] + nz + bs[e])
-                               : acc[a][b][e]);
-        *(VT*)(out + (((size_t)n * Hout + oy) * Hout + ox) * C + cv * V) = o;
+          for (int e = 0; e < V; ++e) {
+            float r = acc[a][b][e];
+            if (FWD) {
+              r = r * dm[e] + nz + bs[e];
+              if (act_out) r = lrelu_s2(r);
+            }
+            o[e] = from_f<T>(r);
+          }
+          *(VT*)(obase + ((size_t)oy * Hout + ox) * C) = o;
+        }
       }
     }
   }
@@ -277,6 +328,7 @@ __global__ void torgb_fwd_kernel(const T* __restrict__ pre, const float* __restr
                                  int W, int Cin, int tpp, int cpt, int pix_per_block, int act_in) {
   typedef typename Vec<T>::type VT;
   constexpr int V = Vec<T>::N;
+  constexpr int U = 4;  // pixels in flight per lane group (U independent 16-B loads per lane)
   extern __shared__ float wm[];  // [3][Cin]
   const int n = blockIdx.y;
   for (int i = threadIdx.x; i < 3 * Cin; i += TPB) wm[i] = wr[i] * s[(size_t)n * Cin + (i % Cin)];
@@ -286,37 +338,59 @@ __global__ void torgb_fwd_kernel(const T* __restrict__ pre, const float* __restr
   const int g = t % tpp, sub = t / tpp, ppp = TPB / tpp;
   const int p_begin = blockIdx.x * pix_per_block;
   const int p_end = min(p_begin + pix_per_block, HW);
-  for (int pb = p_begin; pb < p_end; pb += ppp) {
-    const int p = pb + sub;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    if (p < p_end) {
-      const T* row = pre + ((size_t)n * HW + p) * Cin;
-      for (int cc = 0; cc < cpt; ++cc) {
-        const int c0 = (g + cc * tpp) * V;
-        const VT v = *(const VT*)(row + c0);
+  const T* img = pre + (size_t)n * HW * Cin;
+  for (int pb = p_begin; pb < p_end; pb += ppp * U) {
+    float a[U][3];
 #pragma unroll
-        for (int e = 0; e < V; ++e) {
-          const float a = act_in ? lrelu_s2(to_f(v[e])) : to_f(v[e]);
-          a0 += a * wm[c0 + e];
-          a1 += a * wm[Cin + c0 + e];
-          a2 += a * wm[2 * Cin + c0 + e];
+    for (int u = 0; u < U; ++u) a[u][0] = a[u][1] = a[u][2] = 0.f;
+    for (int cc = 0; cc < cpt; ++cc) {
+      const int c0 = (g + cc * tpp) * V;
+      VT v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int p = pb + u * ppp + sub;
+        if (p < p_end) {
+          v[u] = *(const VT*)(img + (size_t)p * Cin + c0);
+        } else {
+#pragma unroll
+          for (int e = 0; e < V; ++e) v[u][e] = (T)0.f;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float w0 = wm[c0 + e], w1 = wm[Cin + c0 + e], w2 = wm[2 * Cin + c0 + e];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float x = act_in ? lrelu_s2(to_f(v[u][e])) : to_f(v[u][e]);
+          a[u][0] += x * w0;
+          a[u][1] += x * w1;
+          a[u][2] += x * w2;
         }
       }
     }
-    for (int o = 1; o < tpp; o <<= 1) {
-      a0 += __shfl_xor(a0, o, 64);
-      a1 += __shfl_xor(a1, o, 64);
-      a2 += __shfl_xor(a2, o, 64);
-    }
-    if (g == 0 && p < p_end) {
-      const int y = p / W, x = p - (p / W) * W;
-      float r[3] = {a0 + bias[0], a1 + bias[1], a2 + bias[2]};
+    // butterfly: every lane of the group ends with the full sums
+    for (int o = 1; o < tpp; o <<= 1)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) a[u][c] += __shfl_xor(a[u][c], o, 64);
+    // lanes g = 3u + c (g < 3U ≤ tpp) each finish one (pixel, channel); tpp < 12 loops
+    for (int k = g; k < 3 * U; k += tpp) {
+      const int u = k / 3, c = k - 3 * (k / 3);
+      const int p = pb + u * ppp + sub;
+      if (p >= p_end) continue;
+      float r = bias[c];
+#pragma unroll
+      for (int uu = 0; uu < U; ++uu)
+#pragma unroll
+        for (int cc2 = 0; cc2 < 3; ++cc2)
+          if (uu == u && cc2 == c) r += a[uu][cc2];
       if (skip) {
+        const int y = p / W, x = p - (p / W) * W;
         const int Hs = H / 2, Ws = W / 2;
-        for (int c = 0; c < 3; ++c)
-          r[c] += upfir_at(skip + ((size_t)n * 3 + c) * Hs * Ws, Hs, Ws, y, x, kUp4, 4, 2, 1, 2);
+        r += upfir_at(skip + ((size_t)n * 3 + c) * Hs * Ws, Hs, Ws, y, x, kUp4, 4, 2, 1, 2);
       }
-      for (int c = 0; c < 3; ++c) rgb[((size_t)n * 3 + c) * HW + p] = r[c];
+      rgb[((size_t)n * 3 + c) * HW + p] = r;
     }
   }
 }
@@ -723,10 +797,18 @@ extern "C" int mia_upconv_blur_fwd(const void* t, void* pre, const float* demod,
   MIA_CHECK_ARG(t && pre && demod && N > 0 && R > 0, "bad args");
   const int V = dtype == MIA_F32 ? 4 : 8;
   MIA_CHECK_ARG(C % V == 0, "C must be a multiple of the vector width");
-  const int64_t total = (int64_t)N * R * R * (C / V);
+  const int SY = (2 * R + 2 * kBlurKQ - 1) / (2 * kBlurKQ);
+  const int64_t total = (int64_t)N * SY * R * (C / V);
   MIA_DISPATCH_DTYPE(dtype, T,
-      MIA_LAUNCH((blur4_quad_kernel<T, true>), dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0,
-                 (const T*)t, (T*)pre, demod, noise, noise_w, bias, N, R, C, act_out));
+      if (noise) {
+        MIA_LAUNCH((blur4_strip_kernel<T, true, true>), dim3(blocks_for(total, TPB, 65536)),
+                   dim3(TPB), 0, (const T*)t, (T*)pre, demod, noise, noise_w, bias, N, R, C,
+                   act_out);
+      } else {
+        MIA_LAUNCH((blur4_strip_kernel<T, true, false>), dim3(blocks_for(total, TPB, 65536)),
+                   dim3(TPB), 0, (const T*)t, (T*)pre, demod, noise, noise_w, bias, N, R, C,
+                   act_out);
+      });
   return MIA_OK;
 }
 
@@ -735,9 +817,10 @@ extern "C" int mia_upconv_blur_bwd(const void* gy, void* gt, int N, int R, int C
   MIA_CHECK_ARG(gy && gt && N > 0 && R > 0, "bad args");
   const int V = dtype == MIA_F32 ? 4 : 8;
   MIA_CHECK_ARG(C % V == 0, "C must be a multiple of the vector width");
-  const int64_t total = (int64_t)N * (R + 1) * (R + 1) * (C / V);
+  const int SY = (2 * R + 1 + 2 * kBlurKQ - 1) / (2 * kBlurKQ);
+  const int64_t total = (int64_t)N * SY * (R + 1) * (C / V);
   MIA_DISPATCH_DTYPE(dtype, T,
-      MIA_LAUNCH((blur4_quad_kernel<T, false>), dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0,
+      MIA_LAUNCH((blur4_strip_kernel<T, false, false>), dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0,
                  (const T*)gy, (T*)gt, nullptr, nullptr, 0.f, nullptr, N, R, C, 0));
   return MIA_OK;
 }
@@ -788,7 +871,7 @@ extern "C" int mia_torgb_fwd(const void* pre, const float* style, const float* w
   while (tpp * 2 <= nch && tpp * 2 <= 64) tpp *= 2;
   MIA_CHECK_ARG(nch % tpp == 0, "Cin/V must be a power of two times tpp");
   const int cpt = nch / tpp;
-  const int ppb = (TPB / tpp) * 8;
+  const int ppb = (TPB / tpp) * 16;  // 4 passes of U = 4 pixels per lane group
   dim3 grid((H * W + ppb - 1) / ppb, N);
   const size_t sh = 3 * Cin * sizeof(float);
   MIA_DISPATCH_DTYPE(dtype, T,

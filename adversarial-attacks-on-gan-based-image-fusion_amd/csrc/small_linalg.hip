@@ -1,6 +1,7 @@
 // Small fp32 linear algebra of the attack step (K6 style affines, demodulation coefficients, the
 // synthetic encoder): a strided LDS-tiled SGEMM and two fused demod kernels. All of it is
 // < 1 GFLOP per step at N = 128, so simplicity wins over MFMA here.
+#include <algorithm>
 #include <string>
 
 #include "mia_common.h"
@@ -23,59 +24,132 @@ int check_launch(const char* what) {
   return MIA_OK;
 }
 
-constexpr int GT = 64, GK = 16;
+// ---- grouped multi-segment SGEMM ----------------------------------------------------------
+// One launch computes up to kMaxGroups independent products
+//   C_g = alpha_g · Σ_seg A_seg·B_seg + beta_g · C_g + bias_g
+// (a group with two segments sums two K-ranges from different operands — e.g. the two layers that
+// share one W+ latent row in the style-affine backward). Every block owns one TM×TM tile of one
+// group; TM = 64 (4×4 per thread) or 32 (2×2 per thread) is picked on the host so that a launch
+// has enough blocks to cover the 256 CUs (the attack's GEMMs have M = batch ≤ 128).
+constexpr int GK = 16;
+constexpr int kMaxGroups = 12;
 
-__global__ __launch_bounds__(256) void sgemm_kernel(int M, int Nn, int K, float alpha,
-                                                     const float* __restrict__ A, int64_t sam,
-                                                     int64_t sak, const float* __restrict__ B,
-                                                     int64_t sbk, int64_t sbn, float beta,
-                                                     float* __restrict__ C, int64_t scm,
-                                                     int64_t scn, const float* __restrict__ bias) {
-  __shared__ float As[GK][GT + 1];
-  __shared__ float Bs[GK][GT + 1];
+struct GemmSeg {
+  const float* A;
+  const float* B;
+  int64_t sam, sak, sbk, sbn;
+  int K;
+};
+struct GemmGroup {
+  float* C;
+  const float* bias;
+  int64_t scm, scn;
+  int M, N;
+  float alpha, beta;
+  int nseg, tile0, ntn;
+  GemmSeg seg[2];
+};
+struct GemmBatch {
+  int ng;
+  GemmGroup g[kMaxGroups];
+};
+
+template <int TM>
+__global__ __launch_bounds__(256) void sgemm_grouped_kernel(const GemmBatch b) {
+  constexpr int R = TM / 16;  // per-thread micro-tile R×R
+  __shared__ float As[GK][TM + 1];
+  __shared__ float Bs[GK][TM + 1];
+  int gi = 0;
+#pragma unroll 1
+  for (int i = 1; i < b.ng; ++i)
+    if ((int)blockIdx.x >= b.g[i].tile0) gi = i;
+  const GemmGroup& G = b.g[gi];
+  const int t = blockIdx.x - G.tile0;
+  const int m0 = (t / G.ntn) * TM, n0 = (t % G.ntn) * TM;
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int m0 = blockIdx.y * GT, n0 = blockIdx.x * GT;
-  const bool a_kfast = sak == 1, b_kfast = sbk == 1;
-  float acc[4][4] = {};
-  for (int k0 = 0; k0 < K; k0 += GK) {
-    // consecutive threads walk the operand's contiguous dimension (coalesced loads)
-    for (int i = threadIdx.x; i < GK * GT; i += 256) {
-      const int kk = a_kfast ? i % GK : i / GT, mm = a_kfast ? i / GK : i % GT;
-      const int gm = m0 + mm, gk = k0 + kk;
-      As[kk][mm] = (gm < M && gk < K) ? A[gm * sam + gk * sak] : 0.f;
+  float acc[R][R] = {};
+#pragma unroll 1
+  for (int sgi = 0; sgi < G.nseg; ++sgi) {
+    const GemmSeg S = G.seg[sgi];
+    const bool a_kfast = S.sak == 1, b_kfast = S.sbk == 1;
+#pragma unroll 1
+    for (int k0 = 0; k0 < S.K; k0 += GK) {
+      // consecutive threads walk the operand's contiguous dimension (coalesced loads)
+      for (int i = threadIdx.x; i < GK * TM; i += 256) {
+        const int kk = a_kfast ? i % GK : i / TM, mm = a_kfast ? i / GK : i % TM;
+        const int gm = m0 + mm, gk = k0 + kk;
+        As[kk][mm] = (gm < G.M && gk < S.K) ? S.A[gm * S.sam + gk * S.sak] : 0.f;
+      }
+      for (int i = threadIdx.x; i < GK * TM; i += 256) {
+        const int kk = b_kfast ? i % GK : i / TM, nn = b_kfast ? i / GK : i % TM;
+        const int gn = n0 + nn, gk = k0 + kk;
+        Bs[kk][nn] = (gn < G.N && gk < S.K) ? S.B[gk * S.sbk + gn * S.sbn] : 0.f;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < GK; ++kk) {
+        float a[R], bb[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) a[i] = As[kk][ty * R + i];
+#pragma unroll
+        for (int j = 0; j < R; ++j) bb[j] = Bs[kk][tx * R + j];
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+          for (int j = 0; j < R; ++j) acc[i][j] += a[i] * bb[j];
+      }
+      __syncthreads();
     }
-    for (int i = threadIdx.x; i < GK * GT; i += 256) {
-      const int kk = b_kfast ? i % GK : i / GT, nn = b_kfast ? i / GK : i % GT;
-      const int gn = n0 + nn, gk = k0 + kk;
-      Bs[kk][nn] = (gn < Nn && gk < K) ? B[gk * sbk + gn * sbn] : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < GK; ++kk) {
-      float a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = As[kk][ty * 4 + i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] += a[i] * b[j];
-    }
-    __syncthreads();
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < R; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int gm = m0 + ty * 4 + i, gn = n0 + tx * 4 + j;
-      if (gm < M && gn < Nn) {
-        float v = alpha * acc[i][j];
-        if (beta != 0.f) v += beta * C[gm * scm + gn * scn];
-        if (bias) v += bias[gn];
-        C[gm * scm + gn * scn] = v;
+    for (int j = 0; j < R; ++j) {
+      const int gm = m0 + ty * R + i, gn = n0 + tx * R + j;
+      if (gm < G.M && gn < G.N) {
+        float v = G.alpha * acc[i][j];
+        if (G.beta != 0.f) v += G.beta * G.C[gm * G.scm + gn * G.scn];
+        if (G.bias) v += G.bias[gn];
+        G.C[gm * G.scm + gn * G.scn] = v;
       }
     }
+}
+
+static int run_gemm_groups(const mia_gemm_group* groups, int ngroups, hipStream_t st) {
+  int64_t tiles64 = 0;
+  for (int i = 0; i < ngroups; ++i) {
+    const mia_gemm_group& q = groups[i];
+    tiles64 += (int64_t)((q.M + 63) / 64) * ((q.N + 63) / 64);
+  }
+  const int TM = tiles64 >= 512 ? 64 : 32;  // ≥ 2 blocks per CU either way
+  for (int base = 0; base < ngroups; base += kMaxGroups) {
+    GemmBatch b{};
+    b.ng = std::min(kMaxGroups, ngroups - base);
+    int tiles = 0;
+    for (int i = 0; i < b.ng; ++i) {
+      const mia_gemm_group& q = groups[base + i];
+      if (!q.C || q.M <= 0 || q.N <= 0 || q.nseg < 1 || q.nseg > 2)
+        return set_error("gemm: bad group (C, M, N > 0 and 1 ≤ nseg ≤ 2 required)");
+      GemmGroup& g = b.g[i];
+      g.C = q.C; g.bias = q.bias; g.scm = q.scm; g.scn = q.scn; g.M = q.M; g.N = q.N;
+      g.alpha = q.alpha; g.beta = q.beta; g.nseg = q.nseg;
+      for (int s = 0; s < q.nseg; ++s) {
+        const mia_gemm_seg& qs = q.seg[s];
+        if (!qs.A || !qs.B || qs.K <= 0) return set_error("gemm: bad segment (A, B, K > 0)");
+        g.seg[s] = GemmSeg{qs.A, qs.B, qs.sam, qs.sak, qs.sbk, qs.sbn, qs.K};
+      }
+      g.ntn = (q.N + TM - 1) / TM;
+      g.tile0 = tiles;
+      tiles += ((q.M + TM - 1) / TM) * g.ntn;
+    }
+    if (TM == 64)
+      hipLaunchKernelGGL(sgemm_grouped_kernel<64>, dim3(tiles), dim3(256), 0, st, b);
+    else
+      hipLaunchKernelGGL(sgemm_grouped_kernel<32>, dim3(tiles), dim3(256), 0, st, b);
+    const int rc = check_launch("sgemm_grouped");
+    if (rc) return rc;
+  }
+  return MIA_OK;
 }
 
 // demod[n][co] = rsqrt(scale2·Σ_ci s²·wsq[co][ci] + 1e-8); one thread per (n, co).
@@ -126,10 +200,16 @@ extern "C" int mia_gemm_f32(int M, int Nn, int K, float alpha, const float* A, i
                             int64_t sak, const float* B, int64_t sbk, int64_t sbn, float beta,
                             float* C, int64_t scm, int64_t scn, const float* bias, void* stream) {
   MIA_CHECK_ARG(A && B && C && M > 0 && Nn > 0 && K > 0, "bad args");
-  dim3 grid((Nn + GT - 1) / GT, (M + GT - 1) / GT);
-  hipLaunchKernelGGL(sgemm_kernel, grid, dim3(256), 0, (hipStream_t)stream, M, Nn, K, alpha, A,
-                     sam, sak, B, sbk, sbn, beta, C, scm, scn, bias);
-  return check_launch("sgemm");
+  mia_gemm_group g{};
+  g.C = C; g.bias = bias; g.scm = scm; g.scn = scn; g.M = M; g.N = Nn;
+  g.alpha = alpha; g.beta = beta; g.nseg = 1;
+  g.seg[0] = mia_gemm_seg{A, B, sam, sak, sbk, sbn, K};
+  return run_gemm_groups(&g, 1, (hipStream_t)stream);
+}
+
+extern "C" int mia_gemm_f32_grouped(const mia_gemm_group* groups, int ngroups, void* stream) {
+  MIA_CHECK_ARG(groups && ngroups > 0, "bad args");
+  return run_gemm_groups(groups, ngroups, (hipStream_t)stream);
 }
 
 extern "C" int mia_style_demod(const float* s, const float* wsq, float* demod, int N, int Cin,

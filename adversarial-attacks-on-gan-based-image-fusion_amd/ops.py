@@ -409,6 +409,52 @@ def gemm(M, N, K, alpha, A, sam, sak, B, sbk, sbn, beta, C, scm, scn, bias=None)
     return C
 
 
+def _span_ok(name, t, span):
+    if t.dtype != torch.float32 or not t.is_cuda:
+        raise ValueError(f"gemm {name}: cuda fp32 required")
+    avail = t.untyped_storage().nbytes() // 4 - t.storage_offset()
+    if span >= avail:
+        raise ValueError(f"gemm {name}: strided span {span} exceeds storage {avail}")
+
+
+class GemmPlan:
+    """A validated, reusable list of grouped-GEMM descriptors (mia_gemm_f32_grouped).
+
+    ``add(C, scm, scn, M, N, segs, alpha, beta, bias)`` with ``segs`` = [(A, sam, sak, B, sbk,
+    sbn, K), ...] (≤ 2). Tensors are kept alive by the plan; the descriptor array is built once
+    and launched by ``run()`` (the buffers are workspace-resident, so the pointers are stable)."""
+
+    def __init__(self):
+        self.groups = []
+        self._keep = []
+        self._arr = None
+
+    def add(self, C, scm, scn, M, N, segs, alpha=1.0, beta=0.0, bias=None):
+        if not 1 <= len(segs) <= 2:
+            raise ValueError("1 or 2 segments per group")
+        _span_ok("C", C, (M - 1) * scm + (N - 1) * scn)
+        _numel_ok(bias, N, torch.float32, "bias")
+        g = _lib.GemmGroup()
+        g.C, g.bias = C.data_ptr(), (bias.data_ptr() if bias is not None else None)
+        g.scm, g.scn, g.M, g.N = scm, scn, M, N
+        g.alpha, g.beta, g.nseg = float(alpha), float(beta), len(segs)
+        for i, (A, sam, sak, B, sbk, sbn, K) in enumerate(segs):
+            _span_ok("A", A, (M - 1) * sam + (K - 1) * sak)
+            _span_ok("B", B, (K - 1) * sbk + (N - 1) * sbn)
+            g.seg[i] = _lib.GemmSeg(A.data_ptr(), B.data_ptr(), sam, sak, sbk, sbn, K)
+            self._keep += [A, B]
+        self._keep += [C] + ([bias] if bias is not None else [])
+        self.groups.append(g)
+        self._arr = None
+
+    def run(self):
+        if not self.groups:
+            return
+        if self._arr is None:
+            self._arr = (_lib.GemmGroup * len(self.groups))(*self.groups)
+        call("mia_gemm_f32_grouped", self._arr, len(self.groups), stream())
+
+
 def style_demod(s, wsq, demod, scale2=1.0):
     N, Cin = s.shape
     Cout = wsq.shape[0]

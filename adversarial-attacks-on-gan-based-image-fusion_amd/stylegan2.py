@@ -95,19 +95,27 @@ class SynthesisNet:
 
     # --------------------------------------------------------------------------------------
     def styles(self, lat, ws):
-        """s = w+[:, idx]·(A/√512)ᵀ + b for every modulated conv; demod for the StyledConvs."""
+        """s = w+[:, idx]·(A/√512)ᵀ + b for every modulated conv (one grouped GEMM launch for all
+        layers); demod for the StyledConvs."""
         N = lat.shape[0]
         nl = self.n_latent
+        key = (lat.data_ptr(), N)
+        if getattr(self, "_style_key", None) != key:
+            plan = ops.GemmPlan()
+            for i, L in enumerate(self.convs + self.torgbs):
+                cin = L["cin"]
+                s = ws.get(f"g.s{i}", (N, cin), torch.float32)
+                wrow = lat[:, L["latent"], :]
+                plan.add(s, cin, 1, N, cin,
+                         [(wrow, nl * STYLE_DIM, 1, L["A"], 1, STYLE_DIM, STYLE_DIM)],
+                         bias=L["Ab"])
+                L["_s"] = s
+            self._style_plan, self._style_key = plan, key
+        self._style_plan.run()
         for i, L in enumerate(self.convs + self.torgbs):
-            cin = L["cin"]
-            s = ws.get(f"g.s{i}", (N, cin), torch.float32)
-            wrow = lat[:, L["latent"], :]
-            ops.gemm(N, cin, STYLE_DIM, 1.0, wrow, nl * STYLE_DIM, 1, L["A"], 1, STYLE_DIM, 0.0, s,
-                     cin, 1, bias=L["Ab"])
-            L["_s"] = s
             if "wsq" in L:
                 d = ws.get(f"g.d{i}", (N, L["cout"]), torch.float32)
-                ops.style_demod(s, L["wsq"], d)
+                ops.style_demod(L["_s"], L["wsq"], d)
                 L["_d"] = d
 
     def forward(self, lat, ws):
@@ -206,10 +214,18 @@ class SynthesisNet:
             ops.demod_bwd(q, L["_d"], L["wsq"], L["_s"], gs)
             L["_gs"] = gs
             g_a_next = gx
-        # style affine backward: ∂w+[:, idx] += ∂s · (A/√512)
-        for L in self.convs + self.torgbs:
-            cin = L["cin"]
-            gl = g_lat[:, L["latent"], :]
-            ops.gemm(N, STYLE_DIM, cin, 1.0, L["_gs"], cin, 1, L["A"], STYLE_DIM, 1, 1.0, gl,
-                     nl * STYLE_DIM, 1)
+        # style affine backward: ∂w+[:, j] += Σ_{layers reading latent j} ∂s · (A/√512); one
+        # grouped launch, one group per latent row (≤ 2 layers share a row: ToRGB_i and the next
+        # up-conv), so no two blocks write the same output.
+        key = (g_lat.data_ptr(), N)
+        if getattr(self, "_gstyle_key", None) != key:
+            users = {}
+            for L in self.convs + self.torgbs:
+                users.setdefault(L["latent"], []).append(L)
+            plan = ops.GemmPlan()
+            for j, Ls in sorted(users.items()):
+                segs = [(L["_gs"], L["cin"], 1, L["A"], STYLE_DIM, 1, L["cin"]) for L in Ls]
+                plan.add(g_lat[:, j, :], nl * STYLE_DIM, 1, N, STYLE_DIM, segs, beta=1.0)
+            self._gstyle_plan, self._gstyle_key = plan, key
+        self._gstyle_plan.run()
         return g_lat

@@ -206,6 +206,27 @@ int mia_adam_step(float* p, const float* g, float* m, float* v, int64_t len, flo
 int mia_gemm_f32(int M, int Nn, int K, float alpha, const float* A, int64_t sam, int64_t sak,
                  const float* B, int64_t sbk, int64_t sbn, float beta, float* C, int64_t scm,
                  int64_t scn, const float* bias, void* stream);
+/* Grouped form: up to any number of independent fp32 products in as few launches as possible
+ * (12 groups per launch). Group g computes C = alpha·Σ_{s<nseg} A_s·B_s + beta·C + bias with
+ * strided operands as in mia_gemm_f32; nseg ≤ 2 sums two K-ranges (e.g. the two modulated layers
+ * that read one W+ latent row, K6 backward). `groups` is a HOST array; its pointers are device
+ * pointers. Groups must not alias each other's C. */
+typedef struct mia_gemm_seg {
+  const float* A;
+  const float* B;
+  int64_t sam, sak, sbk, sbn;
+  int K;
+} mia_gemm_seg;
+typedef struct mia_gemm_group {
+  float* C;
+  const float* bias; /* [N] or NULL */
+  int64_t scm, scn;
+  int M, N;
+  float alpha, beta;
+  int nseg;
+  mia_gemm_seg seg[2];
+} mia_gemm_group;
+int mia_gemm_f32_grouped(const mia_gemm_group* groups, int ngroups, void* stream);
 /* demod[n][co] = rsqrt(scale2·Σ_ci s[n][ci]²·wsq[co][ci] + 1e-8)  (ModulatedConv2d demod [ext]) */
 int mia_style_demod(const float* s, const float* wsq, float* demod, int N, int Cin, int Cout,
                     float scale2, void* stream);

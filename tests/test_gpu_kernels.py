@@ -305,6 +305,37 @@ def test_gemm_and_demod(cuda):
     assert rel_err(d, torch.rsqrt(0.3 * (s ** 2) @ wsq.t() + 1e-8)) < 1e-5
 
 
+@pytest.mark.parametrize("M,n_groups", [(7, 3), (128, 14), (300, 20)])
+def test_gemm_grouped_two_segments(cuda, M, n_groups):
+    """Grouped GEMM: per group C = α(A1·B1 + A2·B2) + βC + bias with strided views; > 12 groups
+    exercises the launch split, M = 300 the 64-tile path, M = 7 the 32-tile path."""
+    g = torch.Generator().manual_seed(M)
+    plan = ops.GemmPlan()
+    want, outs = [], []
+    lat = torch.randn(M, n_groups, 40, generator=g)
+    latd = lat.to(cuda)
+    for i in range(n_groups):
+        N, K1, K2 = 33 + 7 * i, 19 + i, 40
+        A1 = torch.randn(M, K1, generator=g)
+        B1 = torch.randn(N, K1, generator=g)  # used transposed (k-fast)
+        B2 = torch.randn(K2, N, generator=g)
+        C = torch.randn(M, N, generator=g)
+        bias = torch.randn(N, generator=g)
+        two = i % 2 == 0
+        ref = 0.5 * (A1 @ B1.t() + (lat[:, i, :] @ B2 if two else 0)) + 2.0 * C + bias
+        Cd = C.to(cuda)
+        segs = [(A1.to(cuda), K1, 1, B1.to(cuda), 1, K1, K1)]
+        if two:
+            segs.append((latd[:, i, :], n_groups * 40, 1, B2.to(cuda), N, 1, K2))
+        plan.add(Cd, N, 1, M, N, segs, alpha=0.5, beta=2.0, bias=bias.to(cuda))
+        want.append(ref)
+        outs.append(Cd)
+    plan.run()
+    torch.cuda.synchronize()
+    for r, o in zip(want, outs):
+        assert rel_err(o, r) < 1e-5
+
+
 def test_adam_step(cuda):
     g = torch.Generator().manual_seed(2)
     p = torch.randn(1000, generator=g)

@@ -80,14 +80,18 @@ def test_library_exports_every_header_symbol():
     assert lib.mia_conv_kpad(8, 1) == 128  # host-only helper
 
 
-def test_conv_args_struct_layout_matches_c(tmp_path):
-    """ctypes mirror of mia_conv_args has the C compiler's offsets."""
-    from gfa_amd._lib import ConvArgs
-    fields = [f for f, _ in ConvArgs._fields_]
+@pytest.mark.parametrize("cname,pyname", [("mia_conv_args", "ConvArgs"),
+                                          ("mia_gemm_seg", "GemmSeg"),
+                                          ("mia_gemm_group", "GemmGroup")])
+def test_abi_struct_layout_matches_c(tmp_path, cname, pyname):
+    """ctypes mirrors of the ABI structs have the C compiler's offsets and sizes."""
+    from gfa_amd import _lib
+    S = getattr(_lib, pyname)
+    fields = [f for f, _ in S._fields_]
     src = tmp_path / "off.c"
-    body = "\n".join(f'printf("%s %zu\\n", "{f}", offsetof(mia_conv_args, {f}));' for f in fields)
+    body = "\n".join(f'printf("%s %zu\\n", "{f}", offsetof({cname}, {f}));' for f in fields)
     src.write_text(f'#include <stdio.h>\n#include <stddef.h>\n#include "miattack.h"\n'
-                   f'int main(void){{ {body} printf("size %zu\\n", sizeof(mia_conv_args)); '
+                   f'int main(void){{ {body} printf("size %zu\\n", sizeof({cname})); '
                    f'return 0; }}\n')
     exe = tmp_path / "off"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)],
@@ -96,8 +100,8 @@ def test_conv_args_struct_layout_matches_c(tmp_path):
                                                          text=True, check=True).stdout.split("\n")
                if line)
     for f in fields:
-        assert int(out[f]) == getattr(ConvArgs, f).offset, f
-    assert int(out["size"]) == ctypes.sizeof(ConvArgs)
+        assert int(out[f]) == getattr(S, f).offset, f
+    assert int(out["size"]) == ctypes.sizeof(S)
 
 
 def test_shard_bounds_cover_and_balance():

@@ -1,0 +1,302 @@
+// Shared pieces of the implicit-GEMM convolution kernels on CDNA4 MFMA (gfx950), NHWC:
+// conv_mfma.hip (generic im2col tiles: any tap window / stride / output placement, multi-group)
+// and conv_halo.hip (stride-1 3×3 layers on square output tiles with the input halo staged once
+// per channel block). Operand tiles are rows of 128 B (one K-step slice of a pixel or of an
+// output channel), filled by LDS-DMA with the bank swizzle applied through the source chunk.
+#pragma once
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+
+#include "mia_common.h"
+
+namespace mia {
+
+struct ConvGroup {
+  const void* w;
+  int kpad, kh, kw, pad_y, pad_x, ho, wo, ay, by, ax, bx, blk0, nbm, m;
+};
+
+struct ConvK {
+  mia_conv_args a;  // x, y, N, H/W = INPUT dims, Cin, Cout and the epilogue fields
+  int stride, HT, WT, ystride, cout_mod, log2cin, n_first_max, ng, nblk, nbn;
+  ConvGroup g[4];
+};
+
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+static __device__ __attribute__((aligned(16))) uint4 g_zero16[4];  // zero source for masked DMA lanes
+
+__device__ __forceinline__ int xcd_remap(int b, int nblk) {
+  // Blocks are dealt round-robin over the 8 XCDs; give each XCD a contiguous run of logical tiles
+  // so tiles sharing A rows / B columns hit the same L2 (bijective for any nblk).
+  if (nblk < 16) return b;
+  const int xcd = b & 7, q = nblk >> 3, r = nblk & 7;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + (b >> 3);
+}
+
+// Bank swizzle of a 128-B tile row: stored chunk = chunk ^ fsw(row). ds_read_b128 serves a wave
+// in 4 lane groups ({0–3,12–15,20–27}, {4–11,16–19,28–31}, +32), each one LDS cycle when its 16
+// lanes hit 16 distinct 4-bank slots (MI355X_MICROARCH.md §LDS). A fragment read takes 16
+// consecutive rows (lane & 15) and chunks q, q^1 (lane >> 4): with rows of 128 B the parity of a
+// row picks the bank half, and 2·((row >> 1) & 3) makes every window of 16 consecutive rows —
+// at ANY start row — conflict-free (found by exhaustive search; the classic (row >> 1) & 7 is
+// conflict-free only for windows starting at row ≡ 0, 1 mod 4, which the halo kernel's
+// tap-shifted reads do not respect).
+__device__ __forceinline__ int fsw(int row) { return ((row >> 1) & 3) << 1; }
+
+__device__ __forceinline__ int div_kw(int t, int kw) {
+  return kw == 3 ? (t * 11) >> 5 : (kw == 2 ? t >> 1 : t);  // exact for t < 9
+}
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma_chunk(const typename Vec<T>::type& a,
+                                            const typename Vec<T>::type& b, f32x4 c);
+template <>
+__device__ __forceinline__ f32x4 mfma_chunk<_Float16>(const f16x8& a, const f16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mfma_chunk<__bf16>(const bf16x8& a, const bf16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mfma_chunk<float>(const f32x4& a, const f32x4& b, f32x4 c) {
+  // fp32: lane group q holds k = 4q..4q+3 of the chunk; step s uses k = 4q+s for both operands
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
+  return c;
+}
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == MIA_ACT_RELU) return v > 0.f ? v : 0.f;
+  if (act == MIA_ACT_LRELU_S2) return lrelu_s2(v);
+  return v;
+}
+
+// x̃ = act(x)·s on a 16-byte fragment; for LRELU the table already holds s·√2, and
+// leaky_relu(x, 0.2) = max(x, 0.2·x).
+template <typename T>
+__device__ __forceinline__ void modulate(typename Vec<T>::type& v, const typename Vec<T>::type& s,
+                                         bool lrelu) {
+  if constexpr (std::is_same<T, _Float16>::value) {
+    if (lrelu) v = __builtin_elementwise_max(v, v * (_Float16)0.2f);
+    v = v * s;
+  } else {
+#pragma unroll
+    for (int e = 0; e < Vec<T>::N; ++e) {
+      float f = (float)v[e];
+      if (lrelu) f = fmaxf(f, 0.2f * f);
+      v[e] = (T)(f * (float)s[e]);
+    }
+  }
+}
+
+// 8 consecutive elements of T as fp32
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const typename Vec<T>::type t = *(const typename Vec<T>::type*)p;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (float)t[e];
+  } else {
+    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[e + 4] = b[e]; }
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store8(T* p, const float (&v)[8]) {
+  if constexpr (sizeof(T) == 2) {
+    typename Vec<T>::type t;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[e] = (T)v[e];
+    *(typename Vec<T>::type*)p = t;
+  } else {
+    *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+    *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+}
+__device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[e + 4] = b[e]; }
+}
+
+constexpr int ROWB = 128;  // bytes per tile row (one K-step slice)
+
+// Tile configurations: WM×WN waves, each wave FM×FN 16×16 fragments; STAGES-deep DMA ring.
+//   128×64  / 128×128 : 4 waves, 2 stages, 2 blocks per CU (small M, Cout ≤ 64)
+//   256×128           : 8 waves, 3 stages, 1 block per CU (large M: 85 FLOP per staged byte,
+//                       two K-steps of DMA in flight behind a counted vmcnt)
+template <int WM_, int WN_, int FM_, int FN_, int STAGES_>
+struct Tile {
+  static constexpr int WM = WM_, WN = WN_, FM = FM_, FN = FN_, STAGES = STAGES_;
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
+  static constexpr int A_INS = BM / (8 * NW), B_INS = BN / (8 * NW);  // 1-KB DMA pieces/wave/step
+  static constexpr int STAGE = (BM + BN) * ROWB;
+  static constexpr int EROWS = BM < 128 ? BM : 128;  // rows staged per epilogue pass
+  static constexpr int ES = BN + 4;                  // fp32 words per staged row (bank pad)
+  static_assert(A_INS >= 1 && B_INS >= 1 && A_INS * 8 * NW == BM && B_INS * 8 * NW == BN, "");
+};
+
+// ---- shared epilogue --------------------------------------------------------------------------
+// Stages the fp32 accumulator tile in LDS (EROWS rows per pass), then works on 8-channel vectors:
+// sdot reduction, out_scale, noise, bias, tap-MSE term, ReLU mask, act_out, accumulate, store.
+// rowm(local_row) gives the GEMM row (output pixel index m) of a tile row, or −1 past the end;
+// `single` = every row of the tile belongs to image n_single.
+template <typename T, typename TL, typename RowM>
+__device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G,
+                                              f32x4 (&acc)[TL::FM][TL::FN], char* smem, int n0,
+                                              bool single, int n_single, RowM rowm) {
+  constexpr int WN = TL::WN, FM = TL::FM, FN = TL::FN, NT = TL::NT, NW = TL::NW;
+  constexpr int BM = TL::BM, BN = TL::BN, ES = TL::ES, EROWS = TL::EROWS;
+  const mia_conv_args& p = k.a;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int frow = lane & 15, fq = lane >> 4;
+  const int HWo = G.ho * G.wo;
+  float* tile = (float*)smem;
+  const int Cout = p.Cout;
+  constexpr int CPR = BN / 8;          // 8-channel chunks per row
+  constexpr int RPP = NT / CPR;        // rows per pass
+  const int cc = tid % CPR, r0 = tid / CPR;
+  const int col = n0 + cc * 8;
+  const bool col_ok = col < Cout;      // Cout % 8 == 0 (host check)
+  const T* AX = (const T*)p.aux_x;
+  const T* TA = (const T*)p.tap_a;
+  const T* TT = (const T*)p.tap_t;
+  const T* MA = (const T*)p.mask_a;
+  T* __restrict__ Y = (T*)p.y;
+  float part[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[e] = 0.f;
+
+  // per-column epilogue constants, loaded once (single-image tiles: out_scale too)
+  float bias8[8], osc8[8];
+  const int cm0 = p.shuffle_out ? col % k.cout_mod : col;
+  if (p.bias && col_ok) load8f(p.bias + cm0, bias8);
+  if (p.out_scale && single && col_ok) load8f(p.out_scale + (size_t)n_single * k.cout_mod + cm0, osc8);
+  constexpr int ITERS = EROWS / RPP;
+  static_assert(ITERS * RPP == EROWS, "");
+
+  for (int h = 0; h < BM / EROWS; ++h) {
+    const int wrow0 = wm * FM * 16;
+    if (wrow0 >= h * EROWS && wrow0 < (h + 1) * EROWS) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            tile[(wrow0 - h * EROWS + 16 * i + fq * 4 + r) * ES + wn * FN * 16 + 16 * j + frow] =
+                acc[i][j][r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      const int rr = r0 + it * RPP;
+      const int row = rowm(h * EROWS + rr);
+      if (row >= 0 && col_ok) {
+        float v[8];
+        load8f(tile + rr * ES + cc * 8, v);
+        const size_t aoff = (size_t)row * Cout + col;
+        const int n = single ? n_single : row / HWo;
+        if (p.sdot) {
+          float xv[8];
+          load8<T>(AX + aoff, xv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float c = v[e] * apply_act(xv[e], p.act_aux);
+            if (single) part[e] += c;
+            else atomicAdd(&p.sdot[(size_t)n * Cout + col + e], c);
+          }
+        }
+        if (Y) {
+          const int pix = row - n * HWo;
+          const int y = pix / G.wo, x = pix - (pix / G.wo) * G.wo;
+          int cm = col, yo, xo;
+          if (p.shuffle_out) {
+            const int ph = col / k.cout_mod;
+            cm = col - ph * k.cout_mod;
+            yo = 2 * y + (ph >> 1);
+            xo = 2 * x + (ph & 1);
+          } else {
+            yo = G.ay * y + G.by;
+            xo = G.ax * x + G.bx;
+          }
+          const size_t off = ((size_t)(n * k.HT + yo) * k.WT + xo) * k.ystride + cm;
+          if (p.out_scale) {
+            if (!single) load8f(p.out_scale + (size_t)n * k.cout_mod + cm, osc8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] *= osc8[e];
+          }
+          if (p.noise) {
+            const float nz = p.noise_w * p.noise[yo * k.WT + xo];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += nz;
+          }
+          if (p.bias) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += bias8[e];
+          }
+          if (TA) {
+            float ta[8], tt[8];
+            load8<T>(TA + aoff, ta);
+            load8<T>(TT + aoff, tt);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += p.tap_coef * (ta[e] - tt[e]);
+          }
+          if (MA) {
+            float ma[8];
+            load8<T>(MA + aoff, ma);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = ma[e] > 0.f ? v[e] : 0.f;
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], p.act_out);
+          if (p.accumulate) {
+            float yo8[8];
+            load8<T>(Y + off, yo8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += yo8[e];
+          }
+          store8<T>(Y + off, v);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  if (p.sdot && single) {
+    // reduce the per-thread partial sums of equal channel chunks: lanes cc, cc+CPR, … of a wave
+    // by shuffles, then the waves through LDS, one atomic per channel per block
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      for (int o = CPR; o < 64; o <<= 1) part[e] += __shfl_xor(part[e], o, 64);
+    float* red = (float*)smem;  // [NW waves][BN]
+    if (lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[wid * BN + lane * 8 + e] = part[e];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < Cout) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s += red[w * BN + tid];
+      atomicAdd(&p.sdot[(size_t)n_single * Cout + n0 + tid], s);
+    }
+  }
+}
+
+// halo-tiled stride-1 3×3 path (conv_halo.hip)
+bool conv_halo_eligible(const ConvK& k, int dtype);
+int launch_conv_halo(ConvK& k, int dtype, hipStream_t st);
+
+}  // namespace mia

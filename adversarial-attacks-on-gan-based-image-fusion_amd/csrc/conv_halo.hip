@@ -1,0 +1,345 @@
+// Halo-tiled implicit-GEMM convolution for the stride-1, pad-1 3×3 layers (NHWC), CDNA4 MFMA.
+//
+// Serves the bulk of the attack step's FLOPs (SURVEY.md §2.1 K1, K7, K15 at 16²…256²): VGG conv
+// forward and input-gradient, StyledConv forward (modulation on the A fragments, demodulation in
+// the epilogue) and StyledConv input/style gradient. Up-sampling convs and the stride-2 adjoint
+// stay on the generic im2col kernel (conv_mfma.hip).
+//
+// Why a second kernel: the generic kernel re-gathers every input pixel once per tap (9× the
+// activation bytes through the LDS-DMA path), and a CU fills LDS at only ≈70 GB/s from L2
+// (MI355X_MICROARCH.md, gather-into-LDS table), which caps a 128×128 im2col tile at ≈64 FLOP per
+// staged byte ≈ 45 % of the MFMA peak. Here a block owns a 16×16 output patch of one image:
+//   * per 64-channel block (BK), the (16+2)×(16+2) input halo is DMA'd once into LDS and read by
+//     all 9 taps (A traffic ÷ 7 vs im2col);
+//   * the weights stream per (tap, channel block) K-step through a 3-stage ring with two K-steps
+//     in flight behind a counted vmcnt;
+//   * the next channel block's halo is DMA'd into the other halo buffer one piece per wave per
+//     K-step during the first taps of the current block.
+// GEMM view: M = 256 patch pixels (wave wm owns patch rows 4·wm … 4·wm+3, one MFMA fragment per
+// row), N = BN output channels (64 or 128), K = 9·Cin in (channel block, tap) order; the weight
+// matrix is the same tap-major [Cout][Kpad] layout as the generic kernel, so only the K-offset of
+// a step differs. The epilogue (demod, noise, bias, tap-MSE, ReLU mask, act, sdot) is shared.
+#include "conv_common.h"
+
+namespace mia {
+
+template <int BN_>
+struct HaloTile {
+  static constexpr int WM = 4, WN = 2, FM = 4, FN = BN_ / 32;
+#if defined(MIA_HALO_EXP) && MIA_HALO_EXP >= 2
+  static constexpr int NW = 8, NT = 512, BM = 256, BN = BN_, STAGES = MIA_HALO_EXP;
+  static constexpr int NHBUF = 1;  // tuning experiment: one halo buffer (wrong results)
+#else
+  static constexpr int NW = 8, NT = 512, BM = 256, BN = BN_, STAGES = 4;
+  static constexpr int NHBUF = 2;
+#endif
+  static constexpr int PATCH = 16, HSIDE = PATCH + 2, HROWS = HSIDE * HSIDE;  // 324 halo pixels
+  static constexpr int HPIECES = (HROWS + 7) / 8;  // 41 DMA pieces of 8 rows (1 KB)
+  static constexpr int HBUF = HPIECES * 8 * ROWB;  // 41 KB per halo buffer
+  // DMA roles: waves 0–3 stream the weights, waves 4–7 the halos. vmcnt retires in issue order,
+  // so a wave that mixed both would hold every L2-fast weight piece behind an HBM-slow halo piece.
+  static constexpr int BWAVES = 4, HWAVES = NW - BWAVES;
+  static constexpr int B_INS = BN / (8 * BWAVES);                  // weight pieces per B-wave per step
+  static constexpr int H_INS = (HPIECES + HWAVES - 1) / HWAVES;    // ≤ 11 halo pieces per H-wave
+  static constexpr int H_PER_STEP = 3;                             // next-block halo pieces per step
+  static constexpr int BSTAGE = BN * ROWB;
+  static constexpr int EROWS = 128, ES = BN + 4;  // epilogue staging (shared epilogue)
+  static_assert(B_INS >= 1 && B_INS * 8 * BWAVES == BN, "");
+  static_assert(H_INS <= H_PER_STEP * 6, "next block's halo must be issued by tap 5");
+};
+
+// s_waitcnt vmcnt(n) for a wave-uniform n ≤ 16 (the immediate must be a constant)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+  }
+}
+
+#ifdef MIA_HALO_TIMING
+// phase cycle sums of wave 0 over all blocks (tuning builds only: scratch/, never shipped)
+__device__ unsigned long long g_halo_dbg[8];
+#define HT_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define HT_STAMP(v)
+#endif
+
+template <typename T, typename TL, bool PRO>
+__global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvK k) {
+  HT_STAMP(t_start);
+  typedef typename Vec<T>::type VT;
+  constexpr int VEC = Vec<T>::N;
+  constexpr int BK = ROWB / (int)sizeof(T);
+  constexpr int WN = TL::WN, FM = TL::FM, FN = TL::FN, NT = TL::NT, BN = TL::BN;
+  constexpr int H_INS = TL::H_INS, B_INS = TL::B_INS, HBUF = TL::HBUF, BSTAGE = TL::BSTAGE;
+  constexpr int STAGES = TL::STAGES, PATCH = TL::PATCH, HSIDE = TL::HSIDE, HROWS = TL::HROWS;
+  constexpr int HPIECES = TL::HPIECES, BWAVES = TL::BWAVES, HWAVES = TL::HWAVES;
+  constexpr int HPS = TL::H_PER_STEP;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const hbuf = smem;                        // 2 halo buffers
+  char* const bring = smem + TL::NHBUF * HBUF;    // weight ring
+  T* const stab = (T*)(bring + STAGES * BSTAGE);  // PRO: style row of the patch's image
+
+  const mia_conv_args& p = k.a;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const ConvGroup G = k.g[0];
+  const int H = p.H, W = p.W, Cin = p.Cin, Cout = p.Cout;
+  const int bl = xcd_remap(blockIdx.x, k.nblk);
+  const int mt = bl / k.nbn, n0 = (bl % k.nbn) * BN;
+  const int ptx = W / PATCH, pty = H / PATCH;
+  const int x0 = (mt % ptx) * PATCH;
+  const int y0 = ((mt / ptx) % pty) * PATCH;
+  const int n = mt / (ptx * pty);
+
+  const T* __restrict__ X = (const T*)p.x;
+  const T* __restrict__ Wt = (const T*)G.w;
+  const T* zero = (const T*)g_zero16;
+  const bool bwave = wid < BWAVES;  // wave-uniform role
+  const int hw = wid - BWAVES;      // H-wave index
+  const int my_pieces = bwave ? 0 : (HPIECES - hw + HWAVES - 1) / HWAVES;
+
+  // ---- per-lane DMA sources ------------------------------------------------------------------
+  // H-wave hw owns halo pieces hw + 4·j (8 halo rows each); B-wave w owns weight rows
+  // (w·B_INS + j)·8 + lane/8. Lane → (row, 16-B chunk), the chunk swizzled through the source so
+  // that the lane-linear LDS image is bank-swizzled (fsw).
+  const T* src[H_INS > B_INS ? H_INS : B_INS];
+  constexpr int NSRC = H_INS > B_INS ? H_INS : B_INS;
+#pragma unroll
+  for (int j = 0; j < NSRC; ++j) {
+    src[j] = nullptr;
+    if (bwave) {
+      if (j < B_INS) {
+        const int row = (wid * B_INS + j) * 8 + (lane >> 3);
+        if (n0 + row < Cout)
+          src[j] = Wt + (size_t)(n0 + row) * G.kpad + ((lane & 7) ^ fsw(row)) * VEC;
+      }
+    } else if (j < H_INS) {
+      const int hr = (hw + HWAVES * j) * 8 + (lane >> 3);
+      const int hy = hr / HSIDE, hx = hr - (hr / HSIDE) * HSIDE;
+      const int y = y0 + hy - 1, x = x0 + hx - 1;
+      if (hr < HROWS && y >= 0 && y < H && x >= 0 && x < W)
+        src[j] = X + ((size_t)(n * H + y) * W + x) * Cin + ((lane & 7) ^ fsw(hr)) * VEC;
+    }
+  }
+  const int ncb = Cin / BK, nk = 9 * ncb;
+
+  auto issue_b = [&](int s, int st) {  // B-wave: its weight pieces of K-step s = (cb, tap)
+    const int cb = s / 9, t = s - (s / 9) * 9;
+    const int koff = t * Cin + cb * BK;
+    char* dst = bring + st * BSTAGE;
+#pragma unroll
+    for (int j = 0; j < B_INS; ++j) {
+      const T* a = src[j] ? src[j] + koff : zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)a, (lptr_t)(dst + (wid * B_INS + j) * 1024), 16, 0,
+                                       0);
+    }
+  };
+  auto issue_h = [&](int cb, int j, int buf) {  // H-wave: its halo piece j of channel block cb
+#if defined(MIA_HALO_EXP) && MIA_HALO_EXP == 1
+    return;  // tuning experiment: no halo traffic
+#endif
+    const T* a = src[j] ? src[j] + cb * BK : zero;
+    __builtin_amdgcn_global_load_lds((gptr_t)a,
+                                     (lptr_t)(hbuf + buf * HBUF + (hw + HWAVES * j) * 1024), 16,
+                                     0, 0);
+  };
+
+  // ---- prologue: style row, halo of channel block 0, weights of steps 0 … STAGES−2 -----------
+  const bool lrelu_in = p.act_in == MIA_ACT_LRELU_S2;
+  if constexpr (PRO) {
+    const float mul = lrelu_in ? SQRT2 : 1.f;
+    for (int i = tid; i < Cin; i += NT) {
+      const float sv = p.in_scale ? p.in_scale[(size_t)n * Cin + i] : 1.f;
+      stab[i] = from_f<T>(sv * mul);
+    }
+  }
+  if (bwave) {
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s) issue_b(s, s);  // nk ≥ 9
+    wait_vmcnt((STAGES - 2) * B_INS);  // step 0 landed, steps 1, 2 may stay in flight
+  } else {
+#pragma unroll
+    for (int j = 0; j < H_INS; ++j)
+      if (j < my_pieces) issue_h(0, j, 0);
+    wait_vmcnt(0);
+  }
+  __syncthreads();
+  HT_STAMP(t_pro);
+#ifdef MIA_HALO_TIMING
+  unsigned long long c_vm = 0, c_mma = 0, c_bar = 0;
+#endif
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15, fq = lane >> 4;
+  int st = 0, cb = 0, t = 0;
+  for (int s = 0; s < nk; ++s) {
+    HT_STAMP(ts1);
+    const char* ha = hbuf + (cb & (TL::NHBUF - 1)) * HBUF;
+    const char* sb = bring + st * BSTAGE;
+    const int dy = t >= 6 ? 2 : (t >= 3 ? 1 : 0), dx = t - 3 * dy;
+    // B-waves issue the weights STAGES−1 steps ahead right away (their partner H-wave on the
+    // same SIMD keeps the MFMA pipe busy if the address unit queue stalls them)
+    if (bwave && s + STAGES - 1 < nk) {
+      issue_b(s + STAGES - 1, st == 0 ? STAGES - 1 : st - 1);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ch = h * 4 + fq;
+      VT af[FM], bf[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int hr = (wm * FM + i + dy) * HSIDE + frow + dx;
+        af[i] = *(const VT*)(ha + hr * ROWB + ((ch ^ fsw(hr)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * FN * 16 + 16 * j + frow;
+        bf[j] = *(const VT*)(sb + row * ROWB + ((ch ^ fsw(row)) << 4));
+      }
+      if constexpr (PRO) {
+        const VT sv = *(const VT*)(stab + cb * BK + ch * VEC);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) modulate<T>(af[i], sv, lrelu_in);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma_chunk<T>(af[i], bf[j], acc[i][j]);
+      if (h == 0 && !bwave) {
+        // H-waves issue between the two MFMA halves: the texture-address unit takes ≈16 cycles
+        // per 1-KB LDS-DMA instruction; here the queue overlaps the partner B-wave's MFMAs.
+        __builtin_amdgcn_sched_barrier(0);
+        if (cb + 1 < ncb) {  // next block's halo, HPS pieces per step from tap 0
+#pragma unroll
+          for (int q = 0; q < HPS; ++q) {
+            const int j = t * HPS + q;
+            if (j < my_pieces) issue_h(cb + 1, j, (cb + 1) & (TL::NHBUF - 1));
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    HT_STAMP(ts2);
+    // B-wave: step s+1's weights must have landed; the weights of steps s+2 … s+STAGES−1
+    // (issued later; B-waves issue nothing else) may stay in flight. H-wave: the next block's
+    // halo must have landed before its first tap (issued by tap 3, waited at tap 8).
+    if (bwave) wait_vmcnt(B_INS * max(0, min(STAGES - 2, nk - 2 - s)));
+    else if (t == 8) wait_vmcnt(0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of stage st are done
+    HT_STAMP(ts3);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#ifdef MIA_HALO_TIMING
+    HT_STAMP(ts4);
+    c_mma += ts2 - ts1;
+    c_vm += ts3 - ts2;
+    c_bar += ts4 - ts3;
+#endif
+    st = st + 1 == STAGES ? 0 : st + 1;
+    if (++t == 9) { t = 0; ++cb; }
+  }
+  __syncthreads();
+
+  const int img_row = n * H + y0;
+  HT_STAMP(t_loop);
+  conv_epilogue<T, TL>(k, G, acc, smem, n0, true, n, [=](int r) {
+    return (img_row + (r >> 4)) * W + x0 + (r & 15);
+  });
+#ifdef MIA_HALO_TIMING
+  HT_STAMP(t_end);
+  if (tid == 0) {
+    atomicAdd(&g_halo_dbg[0], t_pro - t_start);
+    atomicAdd(&g_halo_dbg[1], c_vm);
+    atomicAdd(&g_halo_dbg[2], c_mma);
+    atomicAdd(&g_halo_dbg[3], c_bar);
+    atomicAdd(&g_halo_dbg[4], t_end - t_loop);
+    atomicAdd(&g_halo_dbg[5], 1ull);
+    atomicAdd(&g_halo_dbg[6], t_loop - t_pro);
+  }
+#endif
+}
+
+template <typename T, typename TL, bool PRO>
+static int launch_halo_tile(ConvK& k, hipStream_t st) {
+  k.nbn = (k.a.Cout + TL::BN - 1) / TL::BN;
+  const int patches = k.a.N * (k.a.H / TL::PATCH) * (k.a.W / TL::PATCH);
+  k.nblk = patches * k.nbn;
+  size_t lds = TL::NHBUF * (size_t)TL::HBUF + (size_t)TL::STAGES * TL::BSTAGE;
+  if (PRO) lds += (size_t)k.a.Cin * sizeof(T);
+  lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
+  lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
+  if (lds > 160 * 1024) return set_error("conv_halo: LDS budget exceeded");
+  auto fn = conv_halo_kernel<T, TL, PRO>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
+      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), lds, st, k);
+  return check_launch("conv_halo");
+}
+
+// Eligible: one group, stride 1, 3×3 taps with pad 1, identity output placement, no pixel
+// shuffle, 16-divisible spatial dims, whole channel blocks, > 64 output channels (at Cout = 64 the
+// generic 128×64 tile measured faster: the halo tile's fixed costs are paid for half the MFMAs).
+bool conv_halo_eligible(const ConvK& k, int dtype) {
+  const char* e = getenv("MIA_CONV_HALO");  // tuning / A-B switch: 0 disables the halo path
+  if (e && atoi(e) == 0) return false;
+  const mia_conv_args& a = k.a;
+  const ConvGroup& G = k.g[0];
+  const int bk = dtype == MIA_F32 ? 32 : 64;
+  return k.ng == 1 && k.stride == 1 && G.kh == 3 && G.kw == 3 && G.pad_y == 1 && G.pad_x == 1 &&
+         G.ho == a.H && G.wo == a.W && G.ay == 1 && G.ax == 1 && G.by == 0 && G.bx == 0 &&
+         !a.shuffle_out && a.H % 16 == 0 && a.W % 16 == 0 && a.Cin % bk == 0 && a.Cout > 64 &&
+         k.HT == a.H && k.WT == a.W;
+}
+
+int launch_conv_halo(ConvK& k, int dtype, hipStream_t st) {
+  const bool pro = k.a.in_scale != nullptr || k.a.act_in != MIA_ACT_NONE;
+  const bool n64 = k.a.Cout <= 64;
+  MIA_DISPATCH_DTYPE(dtype, T, {
+    if (n64) return pro ? launch_halo_tile<T, HaloTile<64>, true>(k, st)
+                        : launch_halo_tile<T, HaloTile<64>, false>(k, st);
+    return pro ? launch_halo_tile<T, HaloTile<128>, true>(k, st)
+               : launch_halo_tile<T, HaloTile<128>, false>(k, st);
+  });
+  return MIA_OK;
+}
+
+}  // namespace mia
+
+#ifdef MIA_HALO_TIMING
+extern "C" int mia_debug_halo_timing(unsigned long long* out, int reset) {
+  (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(mia::g_halo_dbg), sizeof(mia::g_halo_dbg));
+  if (reset) {
+    unsigned long long z[8] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(mia::g_halo_dbg), z, sizeof(z));
+  }
+  return 0;
+}
+#endif

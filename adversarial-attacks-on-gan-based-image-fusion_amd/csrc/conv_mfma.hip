@@ -25,153 +25,24 @@
 // end. The im2col gather is the per-lane SOURCE address (one pixel row + tap offset); lanes whose
 // tap falls outside the input (or whose row is past M / Cout) read a 16-byte zero vector, so the
 // loop has no branches. For Cin ≥ BK the tap is uniform per K-step and each DMA costs one 64-bit
-// add. LDS-DMA writes lane-linearly, so the bank swizzle (chunk' = chunk ^ ((row>>1)&7),
+// add. LDS-DMA writes lane-linearly, so the bank swizzle (conv_common.h fsw(),
 // conflict-free for the ds_read_b128 fragment lane groups on 128-B rows) is applied by permuting
 // which chunk each lane fetches (guide rule 21). The modulation prologue x̃ = act(x)·s[n][ci] is
 // applied to A fragments after ds_read, with s held in an LDS table for the (≤ 9) images a tile
 // spans. The epilogue stages the fp32 tile through LDS and then works on 8-channel vectors
 // (16-byte loads of every aux operand, 16-byte stores).
-#include <algorithm>
-#include <cstdlib>
-#include <type_traits>
-
-#include "mia_common.h"
+#include "conv_common.h"
 
 namespace mia {
-
-struct ConvGroup {
-  const void* w;
-  int kpad, kh, kw, pad_y, pad_x, ho, wo, ay, by, ax, bx, blk0, nbm, m;
-};
-
-struct ConvK {
-  mia_conv_args a;  // x, y, N, H/W = INPUT dims, Cin, Cout and the epilogue fields
-  int stride, HT, WT, ystride, cout_mod, log2cin, n_first_max, ng, nblk, nbn;
-  ConvGroup g[4];
-};
-
-typedef const __attribute__((address_space(1))) void* gptr_t;
-typedef __attribute__((address_space(3))) void* lptr_t;
-
-__device__ __attribute__((aligned(16))) uint4 g_zero16[4];  // zero source for masked DMA lanes
-
-__device__ __forceinline__ int xcd_remap(int b, int nblk) {
-  // Blocks are dealt round-robin over the 8 XCDs; give each XCD a contiguous run of logical tiles
-  // so tiles sharing A rows / B columns hit the same L2 (bijective for any nblk).
-  if (nblk < 16) return b;
-  const int xcd = b & 7, q = nblk >> 3, r = nblk & 7;
-  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-  return base + (b >> 3);
-}
-
-__device__ __forceinline__ int fsw(int row) { return (row >> 1) & 7; }
-
-__device__ __forceinline__ int div_kw(int t, int kw) {
-  return kw == 3 ? (t * 11) >> 5 : (kw == 2 ? t >> 1 : t);  // exact for t < 9
-}
-
-template <typename T>
-__device__ __forceinline__ f32x4 mfma_chunk(const typename Vec<T>::type& a,
-                                            const typename Vec<T>::type& b, f32x4 c);
-template <>
-__device__ __forceinline__ f32x4 mfma_chunk<_Float16>(const f16x8& a, const f16x8& b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
-template <>
-__device__ __forceinline__ f32x4 mfma_chunk<__bf16>(const bf16x8& a, const bf16x8& b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-template <>
-__device__ __forceinline__ f32x4 mfma_chunk<float>(const f32x4& a, const f32x4& b, f32x4 c) {
-  // fp32: lane group q holds k = 4q..4q+3 of the chunk; step s uses k = 4q+s for both operands
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
-  return c;
-}
-
-__device__ __forceinline__ float apply_act(float v, int act) {
-  if (act == MIA_ACT_RELU) return v > 0.f ? v : 0.f;
-  if (act == MIA_ACT_LRELU_S2) return lrelu_s2(v);
-  return v;
-}
-
-// x̃ = act(x)·s on a 16-byte fragment; for LRELU the table already holds s·√2, and
-// leaky_relu(x, 0.2) = max(x, 0.2·x).
-template <typename T>
-__device__ __forceinline__ void modulate(typename Vec<T>::type& v, const typename Vec<T>::type& s,
-                                         bool lrelu) {
-  if constexpr (std::is_same<T, _Float16>::value) {
-    if (lrelu) v = __builtin_elementwise_max(v, v * (_Float16)0.2f);
-    v = v * s;
-  } else {
-#pragma unroll
-    for (int e = 0; e < Vec<T>::N; ++e) {
-      float f = (float)v[e];
-      if (lrelu) f = fmaxf(f, 0.2f * f);
-      v[e] = (T)(f * (float)s[e]);
-    }
-  }
-}
-
-// 8 consecutive elements of T as fp32
-template <typename T>
-__device__ __forceinline__ void load8(const T* p, float (&v)[8]) {
-  if constexpr (sizeof(T) == 2) {
-    const typename Vec<T>::type t = *(const typename Vec<T>::type*)p;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (float)t[e];
-  } else {
-    const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[e + 4] = b[e]; }
-  }
-}
-template <typename T>
-__device__ __forceinline__ void store8(T* p, const float (&v)[8]) {
-  if constexpr (sizeof(T) == 2) {
-    typename Vec<T>::type t;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) t[e] = (T)v[e];
-    *(typename Vec<T>::type*)p = t;
-  } else {
-    *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
-    *(f32x4*)(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
-  }
-}
-__device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
-  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
-#pragma unroll
-  for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[e + 4] = b[e]; }
-}
-
-constexpr int ROWB = 128;  // bytes per tile row (one K-step slice)
-
-// Tile configurations: WM×WN waves, each wave FM×FN 16×16 fragments; STAGES-deep DMA ring.
-//   128×64  / 128×128 : 4 waves, 2 stages, 2 blocks per CU (small M, Cout ≤ 64)
-//   256×128           : 8 waves, 3 stages, 1 block per CU (large M: 85 FLOP per staged byte,
-//                       two K-steps of DMA in flight behind a counted vmcnt)
-template <int WM_, int WN_, int FM_, int FN_, int STAGES_>
-struct Tile {
-  static constexpr int WM = WM_, WN = WN_, FM = FM_, FN = FN_, STAGES = STAGES_;
-  static constexpr int NW = WM * WN, NT = 64 * NW;
-  static constexpr int BM = WM * FM * 16, BN = WN * FN * 16;
-  static constexpr int A_INS = BM / (8 * NW), B_INS = BN / (8 * NW);  // 1-KB DMA pieces/wave/step
-  static constexpr int STAGE = (BM + BN) * ROWB;
-  static constexpr int EROWS = BM < 128 ? BM : 128;  // rows staged per epilogue pass
-  static constexpr int ES = BN + 4;                  // fp32 words per staged row (bank pad)
-  static_assert(A_INS >= 1 && B_INS >= 1 && A_INS * 8 * NW == BM && B_INS * 8 * NW == BN, "");
-};
 
 template <typename T, typename TL, bool PRO, bool SMALLC>
 __global__ __launch_bounds__(TL::NT, TL::NW == 4 ? 2 : 1) void conv_kernel(const ConvK k) {
   typedef typename Vec<T>::type VT;
   constexpr int VEC = Vec<T>::N;
   constexpr int BK = ROWB / (int)sizeof(T);
-  constexpr int WN = TL::WN, FM = TL::FM, FN = TL::FN, NT = TL::NT, NW = TL::NW;
+  constexpr int WN = TL::WN, FM = TL::FM, FN = TL::FN, NT = TL::NT;
   constexpr int BM = TL::BM, BN = TL::BN, A_INS = TL::A_INS, B_INS = TL::B_INS;
-  constexpr int STAGE = TL::STAGE, STAGES = TL::STAGES, ES = TL::ES, EROWS = TL::EROWS;
+  constexpr int STAGE = TL::STAGE, STAGES = TL::STAGES;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -353,139 +224,16 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 ? 2 : 1) void conv_kernel(const
   }
   if constexpr (STAGES != 2) __syncthreads();
 
-  // ---- epilogue: stage the fp32 tile in LDS (EROWS rows per pass), then 8-channel vectors ---
-  float* tile = (float*)smem;
-  const int Cout = p.Cout;
-  constexpr int CPR = BN / 8;          // 8-channel chunks per row
-  constexpr int RPP = NT / CPR;        // rows per pass
-  const int cc = tid % CPR, r0 = tid / CPR;
-  const int col = n0 + cc * 8;
-  const bool col_ok = col < Cout;      // Cout % 8 == 0 (host check)
-  const T* AX = (const T*)p.aux_x;
-  const T* TA = (const T*)p.tap_a;
-  const T* TT = (const T*)p.tap_t;
-  const T* MA = (const T*)p.mask_a;
-  T* __restrict__ Y = (T*)p.y;
-  const int last = min(m0 + BM, G.m) - 1;
-  const bool single = (m0 / HWo) == (last / HWo);
-  float part[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) part[e] = 0.f;
-
-  // per-column epilogue constants, loaded once (single-image tiles: out_scale too)
-  float bias8[8], osc8[8];
-  const int cm0 = p.shuffle_out ? col % k.cout_mod : col;
-  if (p.bias && col_ok) load8f(p.bias + cm0, bias8);
-  if (p.out_scale && single && col_ok) load8f(p.out_scale + (size_t)(m0 / HWo) * k.cout_mod + cm0, osc8);
-  constexpr int ITERS = EROWS / RPP;
-  static_assert(ITERS * RPP == EROWS, "");
-
-  for (int h = 0; h < BM / EROWS; ++h) {
-    const int wrow0 = wm * FM * 16;
-    if (wrow0 >= h * EROWS && wrow0 < (h + 1) * EROWS) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            tile[(wrow0 - h * EROWS + 16 * i + fq * 4 + r) * ES + wn * FN * 16 + 16 * j + frow] =
-                acc[i][j][r];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < ITERS; ++it) {
-      const int rr = r0 + it * RPP;
-      const int row = m0 + h * EROWS + rr;
-      if (row < G.m && col_ok) {
-        float v[8];
-        load8f(tile + rr * ES + cc * 8, v);
-        const size_t aoff = (size_t)row * Cout + col;
-        const int n = single ? m0 / HWo : row / HWo;
-        if (p.sdot) {
-          float xv[8];
-          load8<T>(AX + aoff, xv);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float c = v[e] * apply_act(xv[e], p.act_aux);
-            if (single) part[e] += c;
-            else atomicAdd(&p.sdot[(size_t)n * Cout + col + e], c);
-          }
-        }
-        if (Y) {
-          const int pix = row - n * HWo;
-          const int y = pix / G.wo, x = pix - (pix / G.wo) * G.wo;
-          int cm = col, yo, xo;
-          if (p.shuffle_out) {
-            const int ph = col / k.cout_mod;
-            cm = col - ph * k.cout_mod;
-            yo = 2 * y + (ph >> 1);
-            xo = 2 * x + (ph & 1);
-          } else {
-            yo = G.ay * y + G.by;
-            xo = G.ax * x + G.bx;
-          }
-          const size_t off = ((size_t)(n * k.HT + yo) * k.WT + xo) * k.ystride + cm;
-          if (p.out_scale) {
-            if (!single) load8f(p.out_scale + (size_t)n * k.cout_mod + cm, osc8);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] *= osc8[e];
-          }
-          if (p.noise) {
-            const float nz = p.noise_w * p.noise[yo * k.WT + xo];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += nz;
-          }
-          if (p.bias) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += bias8[e];
-          }
-          if (TA) {
-            float ta[8], tt[8];
-            load8<T>(TA + aoff, ta);
-            load8<T>(TT + aoff, tt);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += p.tap_coef * (ta[e] - tt[e]);
-          }
-          if (MA) {
-            float ma[8];
-            load8<T>(MA + aoff, ma);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = ma[e] > 0.f ? v[e] : 0.f;
-          }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], p.act_out);
-          if (p.accumulate) {
-            float yo8[8];
-            load8<T>(Y + off, yo8);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += yo8[e];
-          }
-          store8<T>(Y + off, v);
-        }
-      }
-    }
-    __syncthreads();
-  }
-
-  if (p.sdot && single) {
-    // reduce the per-thread partial sums of equal channel chunks: lanes cc, cc+CPR, … of a wave
-    // by shuffles, then the waves through LDS, one atomic per channel per block
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      for (int o = CPR; o < 64; o <<= 1) part[e] += __shfl_xor(part[e], o, 64);
-    float* red = (float*)smem;  // [NW waves][BN]
-    if (lane < CPR) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) red[wid * BN + lane * 8 + e] = part[e];
-    }
-    __syncthreads();
-    if (tid < BN && n0 + tid < Cout) {
-      float s = 0.f;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) s += red[w * BN + tid];
-      atomicAdd(&p.sdot[(size_t)(m0 / HWo) * Cout + n0 + tid], s);
-    }
+  // ---- epilogue ---------------------------------------------------------------------------
+  {
+    const int last = min(m0 + BM, G.m) - 1;
+    const int n_first_img = m0 / HWo;
+    const bool single = n_first_img == last / HWo;
+    const int gm = G.m;
+    conv_epilogue<T, TL>(k, G, acc, smem, n0, single, n_first_img, [=](int r) {
+      const int m = m0 + r;
+      return m < gm ? m : -1;
+    });
   }
 }
 
@@ -585,6 +333,7 @@ static int run_conv(ConvK& k, int dtype, hipStream_t st) {
   for (int g = 0; g < k.ng; ++g) hw_min = std::min(hw_min, k.g[g].ho * k.g[g].wo);
   k.n_first_max = std::min(a.N, (256 + hw_min - 1) / hw_min + 1);
 
+  if (conv_halo_eligible(k, dtype)) return launch_conv_halo(k, dtype, st);
   MIA_DISPATCH_DTYPE(dtype, T, return launch_conv<T>(k, st));
   return MIA_OK;
 }

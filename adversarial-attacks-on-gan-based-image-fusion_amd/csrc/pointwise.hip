@@ -347,14 +347,9 @@ __global__ void torgb_fwd_kernel(const T* __restrict__ pre, const float* __restr
       const int c0 = (g + cc * tpp) * V;
       VT v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int p = pb + u * ppp + sub;
-        if (p < p_end) {
-          v[u] = *(const VT*)(img + (size_t)p * Cin + c0);
-        } else {
-#pragma unroll
-          for (int e = 0; e < V; ++e) v[u][e] = (T)0.f;
-        }
+      for (int u = 0; u < U; ++u) {  // clamped, unconditional: the U loads issue back-to-back
+        const int p = min(pb + u * ppp + sub, p_end - 1);
+        v[u] = *(const VT*)(img + (size_t)p * Cin + c0);
       }
 #pragma unroll
       for (int e = 0; e < V; ++e) {
@@ -456,6 +451,9 @@ __global__ void torgb_bwd_kernel(const float* __restrict__ grgb, const T* __rest
 
 // ---------------------------------------------------------------------------------------------
 // MaxPool 2x2 stride 2 (NHWC), PyTorch semantics incl. ceil_mode and first-max tie rule.
+// One thread per 2×2 window and 16-byte channel vector. All loads are unconditional (coordinates
+// clamped into the image; a clamped duplicate is excluded by its validity flag), so they issue
+// back-to-back instead of each behind its own branch and vmcnt(0).
 template <typename T>
 __global__ void maxpool2_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int H,
                                     int W, int C, int Ho, int Wo) {
@@ -469,86 +467,87 @@ __global__ void maxpool2_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, 
     const int ox = (int)(pix % Wo);
     const int oy = (int)((pix / Wo) % Ho);
     const int n = (int)(pix / ((int64_t)Wo * Ho));
-    VT best;
-    bool first = true;
-    for (int dy = 0; dy < 2; ++dy) {
-      const int yy = 2 * oy + dy;
-      if (yy >= H) continue;
-      for (int dx = 0; dx < 2; ++dx) {
-        const int xx = 2 * ox + dx;
-        if (xx >= W) continue;
-        const VT v = *(const VT*)(x + (((size_t)n * H + yy) * W + xx) * C + cv * V);
-        if (first) { best = v; first = false; }
-        else {
+    const int y0 = 2 * oy, x0 = 2 * ox;
+    const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
+    const T* b = x + (size_t)n * H * W * C + cv * V;
+    const VT v[4] = {*(const VT*)(b + ((size_t)y0 * W + x0) * C),
+                     *(const VT*)(b + ((size_t)y0 * W + x1) * C),
+                     *(const VT*)(b + ((size_t)y1 * W + x0) * C),
+                     *(const VT*)(b + ((size_t)y1 * W + x1) * C)};
+    const bool ok[4] = {true, x0 + 1 < W, y0 + 1 < H, x0 + 1 < W && y0 + 1 < H};
+    VT best = v[0];
 #pragma unroll
-          for (int e = 0; e < V; ++e) {
-            const float fv = to_f(v[e]), fb = to_f(best[e]);
-            if (fv > fb || fv != fv) best[e] = v[e];
-          }
-        }
+    for (int k = 1; k < 4; ++k) {
+      if (!ok[k]) continue;
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float fv = to_f(v[k][e]), fb = to_f(best[e]);
+        if (fv > fb || fv != fv) best[e] = v[k][e];  // first max wins; NaN propagates
       }
     }
     *(VT*)(y + pix * C + cv * V) = best;
   }
 }
 
-template <typename T>
+// Backward per window: the window's gradient goes to its first-max position; the tap-MSE term
+// tap_coef·(x − t) and the ReLU mask (x > 0) of the layer below are fused. Windows beyond
+// (Ho, Wo) (floor mode, odd size) only carry the tap/mask terms.
+template <typename T, bool TAP>
 __global__ void maxpool2_bwd_kernel(const T* __restrict__ x, const T* __restrict__ gout,
                                     T* __restrict__ gin, int N, int H, int W, int C, int Ho, int Wo,
                                     const T* __restrict__ tap_t, float tap_coef, int mask) {
   typedef typename Vec<T>::type VT;
   constexpr int V = Vec<T>::N;
   const int nc = C / V;
-  const int64_t total = (int64_t)N * H * W * nc;
+  const int WY = (H + 1) / 2, WX = (W + 1) / 2;
+  const int64_t total = (int64_t)N * WY * WX * nc;
   for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
     const int cv = (int)(i % nc);
-    const int64_t pix = i / nc;
-    const int xx = (int)(pix % W);
-    const int yy = (int)((pix / W) % H);
-    const int n = (int)(pix / ((int64_t)W * H));
-    const int oy = yy >> 1, ox = xx >> 1;
-    float res[V];
-    const VT xv = *(const VT*)(x + pix * C + cv * V);
-    if (oy < Ho && ox < Wo) {
-      // first-max position of the window, per channel
-      float bv[V];
-      int bpos[V];
-      bool first = true;
-      for (int dy = 0; dy < 2; ++dy) {
-        const int y2 = 2 * oy + dy;
-        if (y2 >= H) continue;
-        for (int dx = 0; dx < 2; ++dx) {
-          const int x2 = 2 * ox + dx;
-          if (x2 >= W) continue;
-          const VT v = *(const VT*)(x + (((size_t)n * H + y2) * W + x2) * C + cv * V);
+    const int64_t w = i / nc;
+    const int wx = (int)(w % WX);
+    const int wy = (int)((w / WX) % WY);
+    const int n = (int)(w / ((int64_t)WX * WY));
+    const int y0 = 2 * wy, x0 = 2 * wx;
+    const int y1 = min(y0 + 1, H - 1), x1 = min(x0 + 1, W - 1);
+    const size_t off[4] = {((size_t)y0 * W + x0) * C, ((size_t)y0 * W + x1) * C,
+                           ((size_t)y1 * W + x0) * C, ((size_t)y1 * W + x1) * C};
+    const bool ok[4] = {true, x0 + 1 < W, y0 + 1 < H, x0 + 1 < W && y0 + 1 < H};
+    const size_t img = (size_t)n * H * W * C + cv * V;
+    const bool pooled = wy < Ho && wx < Wo;
+    const VT go = *(const VT*)(gout + (((size_t)n * Ho + min(wy, Ho - 1)) * Wo + min(wx, Wo - 1)) * C +
+                               cv * V);
+    VT xv[4], tv[4];
 #pragma unroll
-          for (int e = 0; e < V; ++e) {
-            const float fv = to_f(v[e]);
-            if (first || fv > bv[e] || fv != fv) { bv[e] = fv; bpos[e] = dy * 2 + dx; }
-          }
-          first = false;
-        }
-      }
-      const VT go = *(const VT*)(gout + (((size_t)n * Ho + oy) * Wo + ox) * C + cv * V);
-      const int me = (yy - 2 * oy) * 2 + (xx - 2 * ox);
+    for (int k = 0; k < 4; ++k) xv[k] = *(const VT*)(x + img + off[k]);
+    if (TAP) {
 #pragma unroll
-      for (int e = 0; e < V; ++e) res[e] = bpos[e] == me ? to_f(go[e]) : 0.f;
-    } else {
-#pragma unroll
-      for (int e = 0; e < V; ++e) res[e] = 0.f;
+      for (int k = 0; k < 4; ++k) tv[k] = *(const VT*)(tap_t + img + off[k]);
     }
-    VT out;
-    VT tt;
-    if (tap_t) tt = *(const VT*)(tap_t + pix * C + cv * V);
+    int bpos[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      float r = res[e];
-      const float xf = to_f(xv[e]);
-      if (tap_t) r += tap_coef * (xf - to_f(tt[e]));
-      if (mask && !(xf > 0.f)) r = 0.f;
-      out[e] = from_f<T>(r);
+      float bv = to_f(xv[0][e]);
+      bpos[e] = 0;
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const float fv = to_f(xv[k][e]);
+        if (ok[k] && (fv > bv || fv != fv)) { bv = fv; bpos[e] = k; }
+      }
     }
-    *(VT*)(gin + pix * C + cv * V) = out;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (!ok[k]) continue;
+      VT o;
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float xf = to_f(xv[k][e]);
+        float r = (pooled && bpos[e] == k) ? to_f(go[e]) : 0.f;
+        if (TAP) r += tap_coef * (xf - to_f(tv[k][e]));
+        if (mask && !(xf > 0.f)) r = 0.f;
+        o[e] = from_f<T>(r);
+      }
+      *(VT*)(gin + img + off[k]) = o;
+    }
   }
 }
 
@@ -919,11 +918,17 @@ extern "C" int mia_maxpool2_bwd(const void* x, const void* g_out, void* g_in, in
   const int V = dtype == MIA_F32 ? 4 : 8;
   MIA_CHECK_ARG(C % V == 0, "C must be a multiple of the vector width");
   const int Ho = pool_out(H, ceil_mode), Wo = pool_out(W, ceil_mode);
-  const int64_t total = (int64_t)N * H * W * (C / V);
+  const int64_t total = (int64_t)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / V);
   MIA_DISPATCH_DTYPE(dtype, T,
-      MIA_LAUNCH(maxpool2_bwd_kernel<T>, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0,
-                 (const T*)x, (const T*)g_out, (T*)g_in, N, H, W, C, Ho, Wo, (const T*)tap_t,
-                 tap_coef, mask));
+      if (tap_t) {
+        MIA_LAUNCH((maxpool2_bwd_kernel<T, true>), dim3(blocks_for(total, TPB, 65536)), dim3(TPB),
+                   0, (const T*)x, (const T*)g_out, (T*)g_in, N, H, W, C, Ho, Wo, (const T*)tap_t,
+                   tap_coef, mask);
+      } else {
+        MIA_LAUNCH((maxpool2_bwd_kernel<T, false>), dim3(blocks_for(total, TPB, 65536)), dim3(TPB),
+                   0, (const T*)x, (const T*)g_out, (T*)g_in, N, H, W, C, Ho, Wo, (const T*)tap_t,
+                   tap_coef, mask);
+      });
   return MIA_OK;
 }
 

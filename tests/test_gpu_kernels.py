@@ -45,6 +45,59 @@ def test_conv3x3_bias_relu(cuda, dtype, N, H, Cin, Cout):
     assert rel_err(nchw(y), ref) < TOL[dtype]
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 16, 16, 64, 64), (1, 32, 48, 128, 192),
+                                            (2, 16, 32, 256, 128), (1, 48, 16, 64, 128)])
+@pytest.mark.parametrize("mode", ["bias_relu", "modconv", "dgrad_sdot", "tap_mask"])
+@pytest.mark.parametrize("halo", ["1", "0"])
+def test_conv3x3_halo_and_generic_paths(cuda, monkeypatch, dtype, N, H, W, Cin, Cout, mode, halo):
+    """Stride-1 3×3 layers on 16-divisible maps take the halo-tiled kernel (conv_halo.hip) unless
+    MIA_CONV_HALO=0; both paths, with every epilogue feature the attack uses, against torch."""
+    monkeypatch.setenv("MIA_CONV_HALO", halo)
+    g = torch.Generator().manual_seed(N * 7 + H + W + Cin + Cout)
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)
+    xq, wq = x.to(dtype).double(), w.to(dtype).double()
+    xd = nhwc(x, dtype).to(cuda)
+    wf = layouts.fwd_matrix(w, dtype).to(cuda)
+    y = torch.empty(N, H, W, Cout, dtype=dtype, device=cuda)
+    tol = 2 * TOL[dtype]
+    if mode == "bias_relu":
+        b = torch.randn(Cout, generator=g) * 0.1
+        ref = F.relu(F.conv2d(xq, wq, b.double(), padding=1))
+        ops.conv3x3(xd, wf, y, cout=Cout, bias=b.to(cuda), act_out=ops.ACT_RELU)
+    elif mode == "modconv":
+        s = torch.rand(N, Cin, generator=g) + 0.5
+        d = torch.rand(N, Cout, generator=g) + 0.5
+        nz = torch.randn(H * W, generator=g)
+        b = torch.randn(Cout, generator=g) * 0.1
+        pre = F.conv2d(xq * s.double().view(N, Cin, 1, 1), wq, padding=1) * d.double().view(
+            N, Cout, 1, 1) + 0.3 * nz.double().view(1, 1, H, W) + b.double().view(1, -1, 1, 1)
+        ref = F.leaky_relu(pre, 0.2) * math.sqrt(2)
+        ops.conv3x3(xd, wf, y, cout=Cout, in_scale=s.to(cuda), out_scale=d.to(cuda),
+                    noise=nz.to(cuda), noise_w=0.3, bias=b.to(cuda), act_out=ops.ACT_LRELU_S2)
+    elif mode == "dgrad_sdot":
+        s = torch.rand(N, Cout, generator=g) + 0.5
+        aux = torch.randn(N, Cout, H, W, generator=g)
+        conv = F.conv2d(xq, wq, padding=1)
+        ref = conv * s.double().view(N, Cout, 1, 1)
+        sd_ref = (conv * aux.to(dtype).double()).sum((2, 3))
+        sd = torch.zeros(N, Cout, device=cuda)
+        ops.conv3x3(xd, wf, y, cout=Cout, out_scale=s.to(cuda), aux_x=nhwc(aux, dtype).to(cuda),
+                    sdot=sd)
+    else:
+        a = torch.randn(N, Cout, H, W, generator=g).relu()
+        t = torch.randn(N, Cout, H, W, generator=g)
+        aq, tq = a.to(dtype).double(), t.to(dtype).double()
+        ref = (F.conv2d(xq, wq, padding=1) + 0.37 * (aq - tq)) * (aq > 0)
+        ops.conv3x3(xd, wf, y, cout=Cout, tap_a=nhwc(a, dtype).to(cuda),
+                    tap_t=nhwc(t, dtype).to(cuda), tap_coef=0.37, mask_a=nhwc(a, dtype).to(cuda))
+    torch.cuda.synchronize()
+    assert rel_err(nchw(y), ref) < tol
+    if mode == "dgrad_sdot":
+        assert rel_err(sd, sd_ref) < tol
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 def test_conv3x3_dgrad_tap_mask(cuda, dtype):
     g = torch.Generator().manual_seed(7)
@@ -180,25 +233,31 @@ def test_modconv_bwd_input_and_style(cuda, dtype, up, store_act):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("H", [8, 9, 36])
-def test_maxpool_fwd_bwd(cuda, dtype, H):
+@pytest.mark.parametrize("H,ceil,tap", [(8, False, True), (9, True, True), (9, False, True),
+                                        (36, False, True), (7, True, False), (10, False, False)])
+def test_maxpool_fwd_bwd(cuda, dtype, H, ceil, tap):
+    """First-max rule with ties, ceil and floor modes on odd sizes, with and without the fused
+    tap-MSE term + ReLU mask."""
     g = torch.Generator().manual_seed(H)
     N, C = 2, 16
     x = torch.randn(N, C, H, H, generator=g).relu()
     x[:, :, 0:2, 0:2] = 0.5  # ties → first max wins
     xq = x.to(dtype).double().requires_grad_(True)
-    ceil = H % 2 == 1
     y = F.max_pool2d(xq, 2, 2, ceil_mode=ceil)
     go = torch.randn(y.shape, generator=g, dtype=torch.float64).to(dtype).double()
     t = torch.randn(N, C, H, H, generator=g)
     (gx,) = torch.autograd.grad((y * go).sum(), xq)
-    ref_b = (gx + 0.5 * (xq.detach() - t.to(dtype).double())) * (xq.detach() > 0)
+    if tap:
+        ref_b = (gx + 0.5 * (xq.detach() - t.to(dtype).double())) * (xq.detach() > 0)
+    else:
+        ref_b = gx
     xd = nhwc(x, dtype).to(cuda)
     yd = torch.empty(N, y.shape[2], y.shape[3], C, dtype=dtype, device=cuda)
     ops.maxpool2_fwd(xd, yd, ceil_mode=ceil)
-    gi = torch.empty_like(xd)
+    gi = torch.full_like(xd, float("nan"))  # every element must be written
     ops.maxpool2_bwd(xd, nhwc(go, dtype).to(cuda), gi, ceil_mode=ceil,
-                     tap_t=nhwc(t, dtype).to(cuda), tap_coef=0.5, mask=True)
+                     tap_t=nhwc(t, dtype).to(cuda) if tap else None, tap_coef=0.5 if tap else 0.0,
+                     mask=tap)
     torch.cuda.synchronize()
     assert torch.equal(nchw(yd).cpu(), y.detach())
     assert rel_err(nchw(gi), ref_b) < TOL[dtype]

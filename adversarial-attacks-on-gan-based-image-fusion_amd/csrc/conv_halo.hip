@@ -23,29 +23,34 @@
 
 namespace mia {
 
-template <int BN_>
+// Tile: a PH × 16 output patch (PH = 16: 8 waves, 1 block per CU; PH = 8: 4 waves, 2 blocks per
+// CU so that one block's prologue/epilogue overlaps the other's main loop) × BN output channels.
+// Each wave owns FM = 4 patch rows (one 16-pixel MFMA fragment per row) × BN/2 channels.
+template <int BN_, int PH_, int STAGES_>
 struct HaloTile {
-  static constexpr int WM = 4, WN = 2, FM = 4, FN = BN_ / 32;
+  static constexpr int PH = PH_, PW = 16, NW = PH / 2, NT = 64 * NW, BM = PH * PW, BN = BN_;
+  static constexpr int WM = PH / 4, WN = 2, FM = 4, FN = BN_ / 32;
 #if defined(MIA_HALO_EXP) && MIA_HALO_EXP >= 2
-  static constexpr int NW = 8, NT = 512, BM = 256, BN = BN_, STAGES = MIA_HALO_EXP;
+  static constexpr int STAGES = MIA_HALO_EXP;
   static constexpr int NHBUF = 1;  // tuning experiment: one halo buffer (wrong results)
 #else
-  static constexpr int NW = 8, NT = 512, BM = 256, BN = BN_, STAGES = 4;
+  static constexpr int STAGES = STAGES_;
   static constexpr int NHBUF = 2;
 #endif
-  static constexpr int PATCH = 16, HSIDE = PATCH + 2, HROWS = HSIDE * HSIDE;  // 324 halo pixels
-  static constexpr int HPIECES = (HROWS + 7) / 8;  // 41 DMA pieces of 8 rows (1 KB)
-  static constexpr int HBUF = HPIECES * 8 * ROWB;  // 41 KB per halo buffer
-  // DMA roles: waves 0–3 stream the weights, waves 4–7 the halos. vmcnt retires in issue order,
-  // so a wave that mixed both would hold every L2-fast weight piece behind an HBM-slow halo piece.
-  static constexpr int BWAVES = 4, HWAVES = NW - BWAVES;
-  static constexpr int B_INS = BN / (8 * BWAVES);                  // weight pieces per B-wave per step
-  static constexpr int H_INS = (HPIECES + HWAVES - 1) / HWAVES;    // ≤ 11 halo pieces per H-wave
-  static constexpr int H_PER_STEP = 3;                             // next-block halo pieces per step
+  static constexpr int HW = PW + 2, HROWS = (PH + 2) * HW;  // 324 / 180 halo pixels
+  static constexpr int HPIECES = (HROWS + 7) / 8;          // DMA pieces of 8 rows (1 KB)
+  static constexpr int HBUF = HPIECES * 8 * ROWB;          // per halo buffer
+  // DMA roles: the first half of the waves stream the weights, the second half the halos.
+  // vmcnt retires in issue order, so a wave that mixed both would hold every L2-fast weight
+  // piece behind an HBM-slow halo piece.
+  static constexpr int BWAVES = NW / 2, HWAVES = NW - BWAVES;
+  static constexpr int B_INS = BN / (8 * BWAVES);                // weight pieces per B-wave per step
+  static constexpr int H_INS = (HPIECES + HWAVES - 1) / HWAVES;  // halo pieces per H-wave
+  static constexpr int H_PER_STEP = (H_INS + 3) / 4;             // next-block halo by tap 3
   static constexpr int BSTAGE = BN * ROWB;
-  static constexpr int EROWS = 128, ES = BN + 4;  // epilogue staging (shared epilogue)
+  static constexpr int EROWS = BM < 128 ? BM : 128, ES = BN + 4;  // shared epilogue staging
   static_assert(B_INS >= 1 && B_INS * 8 * BWAVES == BN, "");
-  static_assert(H_INS <= H_PER_STEP * 6, "next block's halo must be issued by tap 5");
+  static_assert(WM * FM * 16 == BM && WN * FN * 16 == BN, "");
 };
 
 // s_waitcnt vmcnt(n) for a wave-uniform n ≤ 16 (the immediate must be a constant)
@@ -80,14 +85,14 @@ __device__ unsigned long long g_halo_dbg[8];
 #endif
 
 template <typename T, typename TL, bool PRO>
-__global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvK k) {
+__global__ __launch_bounds__(TL::NT, TL::NW == 4 ? 2 : 1) void conv_halo_kernel(const ConvK k) {
   HT_STAMP(t_start);
   typedef typename Vec<T>::type VT;
   constexpr int VEC = Vec<T>::N;
   constexpr int BK = ROWB / (int)sizeof(T);
   constexpr int WN = TL::WN, FM = TL::FM, FN = TL::FN, NT = TL::NT, BN = TL::BN;
   constexpr int H_INS = TL::H_INS, B_INS = TL::B_INS, HBUF = TL::HBUF, BSTAGE = TL::BSTAGE;
-  constexpr int STAGES = TL::STAGES, PATCH = TL::PATCH, HSIDE = TL::HSIDE, HROWS = TL::HROWS;
+  constexpr int STAGES = TL::STAGES, PH = TL::PH, PW = TL::PW, HSIDE = TL::HW, HROWS = TL::HROWS;
   constexpr int HPIECES = TL::HPIECES, BWAVES = TL::BWAVES, HWAVES = TL::HWAVES;
   constexpr int HPS = TL::H_PER_STEP;
 
@@ -104,9 +109,9 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvK k) {
   const int H = p.H, W = p.W, Cin = p.Cin, Cout = p.Cout;
   const int bl = xcd_remap(blockIdx.x, k.nblk);
   const int mt = bl / k.nbn, n0 = (bl % k.nbn) * BN;
-  const int ptx = W / PATCH, pty = H / PATCH;
-  const int x0 = (mt % ptx) * PATCH;
-  const int y0 = ((mt / ptx) % pty) * PATCH;
+  const int ptx = W / PW, pty = H / PH;
+  const int x0 = (mt % ptx) * PW;
+  const int y0 = ((mt / ptx) % pty) * PH;
   const int n = mt / (ptx * pty);
 
   const T* __restrict__ X = (const T*)p.x;
@@ -285,7 +290,7 @@ __global__ __launch_bounds__(512, 1) void conv_halo_kernel(const ConvK k) {
 template <typename T, typename TL, bool PRO>
 static int launch_halo_tile(ConvK& k, hipStream_t st) {
   k.nbn = (k.a.Cout + TL::BN - 1) / TL::BN;
-  const int patches = k.a.N * (k.a.H / TL::PATCH) * (k.a.W / TL::PATCH);
+  const int patches = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW);
   k.nblk = patches * k.nbn;
   size_t lds = TL::NHBUF * (size_t)TL::HBUF + (size_t)TL::STAGES * TL::BSTAGE;
   if (PRO) lds += (size_t)k.a.Cin * sizeof(T);
@@ -310,23 +315,33 @@ static int launch_halo_tile(ConvK& k, hipStream_t st) {
 bool conv_halo_eligible(const ConvK& k, int dtype) {
   const char* e = getenv("MIA_CONV_HALO");  // tuning / A-B switch: 0 disables the halo path
   if (e && atoi(e) == 0) return false;
+  const char* e64 = getenv("MIA_HALO_N64");  // tuning: 1 = halo path for Cout = 64 too
+  const int min_cout = (e64 && atoi(e64) == 1) ? 64 : 65;
   const mia_conv_args& a = k.a;
   const ConvGroup& G = k.g[0];
   const int bk = dtype == MIA_F32 ? 32 : 64;
   return k.ng == 1 && k.stride == 1 && G.kh == 3 && G.kw == 3 && G.pad_y == 1 && G.pad_x == 1 &&
          G.ho == a.H && G.wo == a.W && G.ay == 1 && G.ax == 1 && G.by == 0 && G.bx == 0 &&
-         !a.shuffle_out && a.H % 16 == 0 && a.W % 16 == 0 && a.Cin % bk == 0 && a.Cout > 64 &&
+         !a.shuffle_out && a.H % 16 == 0 && a.W % 16 == 0 && a.Cin % bk == 0 && a.Cout >= min_cout &&
          k.HT == a.H && k.WT == a.W;
 }
 
 int launch_conv_halo(ConvK& k, int dtype, hipStream_t st) {
   const bool pro = k.a.in_scale != nullptr || k.a.act_in != MIA_ACT_NONE;
-  const bool n64 = k.a.Cout <= 64;
+  // Default: 8×16 patches (4 waves, 2 blocks per CU, 2-stage weight ring) — measured 5–10 %
+  // faster than 16×16 patches (8 waves, 1 block per CU, 4 stages) on every attack shape, the
+  // second block hiding each block's prologue, epilogue and DMA waits.
+  const char* e = getenv("MIA_HALO_TILE");  // tuning: 2 = 16×16 patches
+  const bool big = e && atoi(e) == 2;
+  typedef HaloTile<128, 16, 4> Big;
+  typedef HaloTile<128, 8, 2> Small;
+  typedef HaloTile<64, 8, 3> Small64;
   MIA_DISPATCH_DTYPE(dtype, T, {
-    if (n64) return pro ? launch_halo_tile<T, HaloTile<64>, true>(k, st)
-                        : launch_halo_tile<T, HaloTile<64>, false>(k, st);
-    return pro ? launch_halo_tile<T, HaloTile<128>, true>(k, st)
-               : launch_halo_tile<T, HaloTile<128>, false>(k, st);
+    if (k.a.Cout <= 64)
+      return pro ? launch_halo_tile<T, Small64, true>(k, st)
+                 : launch_halo_tile<T, Small64, false>(k, st);
+    if (big) return pro ? launch_halo_tile<T, Big, true>(k, st) : launch_halo_tile<T, Big, false>(k, st);
+    return pro ? launch_halo_tile<T, Small, true>(k, st) : launch_halo_tile<T, Small, false>(k, st);
   });
   return MIA_OK;
 }

@@ -24,11 +24,12 @@ def short(name):
     if m:
         base = re.sub(r"^\d+", "", m.group(1))
         tile = re.search(r"TileILi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)", name)
-        halo = re.search(r"HaloTileILi(\d+)E", name)
+        halo = re.search(r"HaloTileILi(\d+)ELi(\d+)ELi(\d+)E", name)
         flags = re.findall(r"ELb([01])", name)
         extra = ""
         if halo:
-            extra = f"<256x{halo.group(1)},pro={flags[0] if flags else '?'}>"
+            bn, ph, stg = map(int, halo.groups())
+            extra = f"<{ph}x16px x {bn}ch,{stg}st,pro={flags[0] if flags else '?'}>"
         elif tile:
             wm, wn, fm, fn, st = map(int, tile.groups())
             extra = f"<{wm * fm * 16}x{wn * fn * 16},{st}st,pro={flags[0]},smallc={flags[1]}>"

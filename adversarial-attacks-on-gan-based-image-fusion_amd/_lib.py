@@ -80,12 +80,18 @@ SIGNATURES = {
     "mia_avgpool_fwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     "mia_avgpool_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_image_to_nhwc": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
-    "mia_mse_sum": (c_int, [P, P, P, c_int, c_int64, c_int, P]),
+    "mia_mse_sum": (c_int, [P, P, P, c_int, c_int64, c_float, c_int, P]),
     "mia_mse_grad_f32": (c_int, [P, P, P, c_int64, c_float, c_int, P]),
     "mia_tap_grad": (c_int, [P, P, P, c_int64, c_float, c_int, c_int, P]),
     "mia_image_grad": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_float, c_int, P]),
     "mia_pgd_update": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, c_float,
                                c_float, c_float, c_float, c_int, P]),
+    "mia_grad_assemble": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float,
+                                  c_float, c_int, P]),
+    "mia_cw_init": (c_int, [P, P, c_int64, P]),
+    "mia_cw_tanh": (c_int, [P, P, c_int64, P]),
+    "mia_cw_grad": (c_int, [P, P, P, P, c_int64, c_float, c_float, P]),
+    "mia_cw_select": (c_int, [P, P, P, P, P, P, c_int, c_int64, c_float, P]),
     "mia_random_start": (c_int, [P, P, P, c_int64, c_float, c_float, c_float, P]),
     "mia_sign_project": (c_int, [P, P, P, c_int64, c_float, c_float, c_float, c_float, P]),
     "mia_adam_step": (c_int, [P, P, P, P, c_int64, c_float, c_float, c_float, c_float, c_int, P]),

@@ -614,7 +614,7 @@ __global__ void image_to_nhwc_kernel(const float* __restrict__ x, T* __restrict_
 // MSE pieces (K10).
 template <typename T>
 __global__ void mse_sum_kernel(const T* __restrict__ a, const T* __restrict__ b,
-                               float* __restrict__ loss, int64_t len) {
+                               float* __restrict__ loss, int64_t len, float coef) {
   const int n = blockIdx.y;
   const T* pa = a + (size_t)n * len;
   const T* pb = b + (size_t)n * len;
@@ -630,7 +630,7 @@ __global__ void mse_sum_kernel(const T* __restrict__ a, const T* __restrict__ b,
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int w = 0; w < TPB / 64; ++w) s += red[w];
-    atomicAdd(&loss[n], s);
+    atomicAdd(&loss[n], coef * s);
   }
 }
 
@@ -704,27 +704,87 @@ __global__ void sign_project_kernel(float* __restrict__ x, const float* __restri
     x[i] = project1(x[i], x0[i], g[i], a, e, lo, hi);
 }
 
+// ∇_x L at image element i (NCHW fp32, S² planes): the image-MSE term coef_img·(x − x0) plus the
+// adjoints of the two avg_pool2d's (attack_main2.py:590-591): the VGG input-path gradient at S/pf
+// (NHWC, cpad channels) and the encoder gradient at enc_res, each spread over its pooling window.
+template <typename T>
+__device__ __forceinline__ float assemble_grad(int64_t i, float xv, float x0v, const T* gv,
+                                               const float* genc, int S, int pf, int cpad,
+                                               int enc_res, float coef_img) {
+  const int R = S / pf;
+  const int ek = S / enc_res;
+  const int xx = (int)(i % S);
+  const int yy = (int)((i / S) % S);
+  const int c = (int)((i / ((int64_t)S * S)) % 3);
+  const int n = (int)(i / ((int64_t)S * S * 3));
+  float g = coef_img * (xv - x0v);
+  if (gv) g += to_f(gv[(((size_t)n * R + yy / pf) * R + xx / pf) * cpad + c]) / (float)(pf * pf);
+  if (genc) g += genc[(((size_t)n * 3 + c) * enc_res + yy / ek) * enc_res + xx / ek] / (float)(ek * ek);
+  return g;
+}
+
 template <typename T>
 __global__ void pgd_update_kernel(float* __restrict__ x, const float* __restrict__ x0,
                                   const T* __restrict__ gv, const float* __restrict__ genc, int N,
                                   int S, int pf, int cpad, int enc_res, float coef_img, float a,
                                   float e, float lo, float hi) {
-  const int R = S / pf;
-  const int ek = S / enc_res;
-  const float inv_pf = 1.f / (float)(pf * pf);
-  const float inv_ek = 1.f / (float)(ek * ek);
   const int64_t total = (int64_t)N * 3 * S * S;
   for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
-    const int xx = (int)(i % S);
-    const int yy = (int)((i / S) % S);
-    const int c = (int)((i / ((int64_t)S * S)) % 3);
-    const int n = (int)(i / ((int64_t)S * S * 3));
     const float xv = x[i], x0v = x0[i];
-    float g = coef_img * (xv - x0v);
-    if (gv) g += to_f(gv[(((size_t)n * R + yy / pf) * R + xx / pf) * cpad + c]) * inv_pf;
-    if (genc) g += genc[(((size_t)n * 3 + c) * enc_res + yy / ek) * enc_res + xx / ek] * inv_ek;
+    const float g = assemble_grad(i, xv, x0v, gv, genc, S, pf, cpad, enc_res, coef_img);
     x[i] = project1(xv, x0v, g, a, e, lo, hi);
   }
+}
+
+template <typename T>
+__global__ void grad_assemble_kernel(const float* __restrict__ x, const float* __restrict__ x0,
+                                     const T* __restrict__ gv, const float* __restrict__ genc,
+                                     float* __restrict__ g, int N, int S, int pf, int cpad,
+                                     int enc_res, float coef_img, float scale) {
+  const int64_t total = (int64_t)N * 3 * S * S;
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB)
+    g[i] = scale * assemble_grad(i, x[i], x0[i], gv, genc, S, pf, cpad, enc_res, coef_img);
+}
+
+// ---- C&W L2 in tanh space (torchattacks CW, interpolation.py:98-193), images in [-1, 1]:
+// adv = tanh(w) (= 2·½(tanh w + 1) − 1), w0 = atanh(x) with x clamped to ±(1 − 2⁻²⁰) so that
+// saturated pixels stay finite.
+__global__ void cw_init_kernel(const float* __restrict__ x, float* __restrict__ w, int64_t len) {
+  constexpr float lim = 1.f - 9.5367431640625e-07f;
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < len; i += (int64_t)gridDim.x * TPB)
+    w[i] = atanhf(fminf(fmaxf(x[i], -lim), lim));
+}
+
+__global__ void cw_tanh_kernel(const float* __restrict__ w, float* __restrict__ adv, int64_t len) {
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < len; i += (int64_t)gridDim.x * TPB)
+    adv[i] = tanhf(w[i]);
+}
+
+// ∂cost/∂w with cost = Σ_n ‖(adv − x)/2‖² + c·Σ_n f_n(adv) and adv = tanh w:
+//   gw = (½(adv − x) + c·scale·g_f)·(1 − adv²)        (g_f = ∇f, loss-scaled; scale undoes it)
+__global__ void cw_grad_kernel(const float* __restrict__ adv, const float* __restrict__ x,
+                               const float* __restrict__ gf, float* __restrict__ gw, int64_t len,
+                               float c, float scale) {
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < len; i += (int64_t)gridDim.x * TPB) {
+    const float a = adv[i];
+    gw[i] = (0.5f * (a - x[i]) + c * scale * gf[i]) * (1.f - a * a);
+  }
+}
+
+// Best-L2 bookkeeping (torchattacks CW :154-163), one block per image: an image is a success when
+// its objective is below the clean image's (f_n < f0_n, the GAN objective has no labels) and its
+// L2 = l2_scale·Σ(adv − x)² beats the best so far; then best_adv[n] ← adv[n].
+__global__ void cw_select_kernel(const float* __restrict__ adv, float* __restrict__ best_adv,
+                                 const float* __restrict__ sq, float* __restrict__ best_l2,
+                                 const float* __restrict__ f, const float* __restrict__ f0,
+                                 int64_t plane, float l2_scale) {
+  const int n = blockIdx.x;
+  const float l2 = l2_scale * sq[n];
+  const bool take = f[n] < f0[n] && best_l2[n] > l2;
+  __syncthreads();
+  if (!take) return;
+  for (int64_t i = threadIdx.x; i < plane; i += TPB) best_adv[(size_t)n * plane + i] = adv[(size_t)n * plane + i];
+  if (threadIdx.x == 0) best_l2[n] = l2;
 }
 
 // K12: Adam on pixels (torch.optim.Adam single-tensor semantics, no weight decay).
@@ -960,11 +1020,11 @@ extern "C" int mia_image_to_nhwc(const float* x, void* y, int N, int S, int pf, 
 }
 
 extern "C" int mia_mse_sum(const void* a, const void* b, float* loss, int n, int64_t len,
-                           int dtype, void* stream) {
+                           float coef, int dtype, void* stream) {
   MIA_CHECK_ARG(a && b && loss && n > 0 && len > 0, "bad args");
   dim3 grid(blocks_for(len, TPB, 1024), n);
   MIA_DISPATCH_DTYPE(dtype, T,
-      MIA_LAUNCH(mse_sum_kernel<T>, grid, dim3(TPB), 0, (const T*)a, (const T*)b, loss, len));
+      MIA_LAUNCH(mse_sum_kernel<T>, grid, dim3(TPB), 0, (const T*)a, (const T*)b, loss, len, coef));
   return MIA_OK;
 }
 
@@ -1003,6 +1063,42 @@ extern "C" int mia_pgd_update(float* x, const float* x0, const void* g_vgg, cons
       MIA_LAUNCH(pgd_update_kernel<T>, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0, x, x0,
                  (const T*)g_vgg, g_enc, N, S, pf, cpad, enc_res, coef_img, a, e, lo, hi));
   return MIA_OK;
+}
+
+extern "C" int mia_grad_assemble(const float* x, const float* x0, const void* g_vgg,
+                                 const float* g_enc, float* g, int N, int S, int pf, int cpad,
+                                 int enc_res, float coef_img, float scale, int dtype, void* stream) {
+  MIA_CHECK_ARG(x && x0 && g && pf >= 1 && S % pf == 0 && (!g_enc || S % enc_res == 0), "bad args");
+  const int64_t total = (int64_t)N * 3 * S * S;
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH(grad_assemble_kernel<T>, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0, x,
+                 x0, (const T*)g_vgg, g_enc, g, N, S, pf, cpad, enc_res, coef_img, scale));
+  return MIA_OK;
+}
+
+extern "C" int mia_cw_init(const float* x, float* w, int64_t len, void* stream) {
+  MIA_CHECK_ARG(x && w && len > 0, "bad args");
+  MIA_LAUNCH(cw_init_kernel, dim3(blocks_for(len, TPB, 65536)), dim3(TPB), 0, x, w, len);
+}
+
+extern "C" int mia_cw_tanh(const float* w, float* adv, int64_t len, void* stream) {
+  MIA_CHECK_ARG(w && adv && len > 0, "bad args");
+  MIA_LAUNCH(cw_tanh_kernel, dim3(blocks_for(len, TPB, 65536)), dim3(TPB), 0, w, adv, len);
+}
+
+extern "C" int mia_cw_grad(const float* adv, const float* x, const float* g_f, float* g_w,
+                           int64_t len, float c, float scale, void* stream) {
+  MIA_CHECK_ARG(adv && x && g_f && g_w && len > 0, "bad args");
+  MIA_LAUNCH(cw_grad_kernel, dim3(blocks_for(len, TPB, 65536)), dim3(TPB), 0, adv, x, g_f, g_w,
+             len, c, scale);
+}
+
+extern "C" int mia_cw_select(const float* adv, float* best_adv, const float* sq, float* best_l2,
+                             const float* f, const float* f0, int N, int64_t plane, float l2_scale,
+                             void* stream) {
+  MIA_CHECK_ARG(adv && best_adv && sq && best_l2 && f && f0 && N > 0 && plane > 0, "bad args");
+  MIA_LAUNCH(cw_select_kernel, dim3(N), dim3(TPB), 0, adv, best_adv, sq, best_l2, f, f0, plane,
+             l2_scale);
 }
 
 extern "C" int mia_random_start(float* x, const float* x0, const float* u, int64_t len, float e,

@@ -314,11 +314,12 @@ def image_to_nhwc(x, y, pf, cpad):
     return y
 
 
-def mse_sum(a, b, loss):
+def mse_sum(a, b, loss, coef=1.0):
+    """loss[n] += coef·Σ (a[n] − b[n])²."""
     n = a.shape[0]
     _need(b, a.shape, a.dtype, "b")
     _numel_ok(loss, n, torch.float32, "loss")
-    call("mia_mse_sum", ptr(a), ptr(b), ptr(loss), n, a.numel() // n, dt(a), stream())
+    call("mia_mse_sum", ptr(a), ptr(b), ptr(loss), n, a.numel() // n, float(coef), dt(a), stream())
     return loss
 
 
@@ -365,6 +366,55 @@ def pgd_update(x, x0, g_vgg, g_enc, pf, enc_res, coef_img, a, e, lo=-1.0, hi=1.0
     call("mia_pgd_update", ptr(x), ptr(x0), ptr(g_vgg), ptr(g_enc), N, S, pf, cpad, enc_res,
          float(coef_img), float(a), float(e), float(lo), float(hi), gdt, stream())
     return x
+
+
+def grad_assemble(x, x0, g_vgg, g_enc, g, pf, enc_res, coef_img, scale=1.0):
+    """∇_x L (fp32 NCHW) from the VGG input-path and encoder gradients (mia_grad_assemble)."""
+    N, C, S, S2 = x.shape
+    if C != 3 or S != S2:
+        raise ValueError("x must be (N,3,S,S)")
+    _need(x0, x.shape, torch.float32, "x0")
+    _need(g, x.shape, torch.float32, "g")
+    R = S // pf
+    cpad = g_vgg.shape[-1] if g_vgg is not None else 8
+    if g_vgg is not None:
+        _need(g_vgg, (N, R, R, cpad), None, "g_vgg")
+    if g_enc is not None:
+        _need(g_enc, (N, 3, enc_res, enc_res), torch.float32, "g_enc")
+    T = g_vgg.dtype if g_vgg is not None else torch.float32
+    call("mia_grad_assemble", ptr(x), ptr(x0), ptr(g_vgg), ptr(g_enc), ptr(g), N, S, pf, cpad,
+         enc_res, float(coef_img), float(scale), dt(T), stream())
+    return g
+
+
+def cw_init(x, w):
+    _need(w, x.shape, torch.float32, "w")
+    call("mia_cw_init", ptr(x), ptr(w), x.numel(), stream())
+    return w
+
+
+def cw_tanh(w, adv):
+    _need(adv, w.shape, torch.float32, "adv")
+    call("mia_cw_tanh", ptr(w), ptr(adv), w.numel(), stream())
+    return adv
+
+
+def cw_grad(adv, x, g_f, g_w, c, scale=1.0):
+    for name, t in (("x", x), ("g_f", g_f), ("g_w", g_w)):
+        _need(t, adv.shape, torch.float32, name)
+    call("mia_cw_grad", ptr(adv), ptr(x), ptr(g_f), ptr(g_w), adv.numel(), float(c), float(scale),
+         stream())
+    return g_w
+
+
+def cw_select(adv, best_adv, sq, best_l2, f, f0, l2_scale):
+    N = adv.shape[0]
+    _need(best_adv, adv.shape, torch.float32, "best_adv")
+    for name, t in (("sq", sq), ("best_l2", best_l2), ("f", f), ("f0", f0)):
+        _numel_ok(t, N, torch.float32, name)
+    call("mia_cw_select", ptr(adv), ptr(best_adv), ptr(sq), ptr(best_l2), ptr(f), ptr(f0), N,
+         adv.numel() // N, float(l2_scale), stream())
+    return best_adv
 
 
 def random_start(x, x0, u, e, lo=-1.0, hi=1.0):

@@ -86,21 +86,47 @@ class AttackEngine:
                 keep.copy_(tap)
                 dst.append(keep)
 
-    def gradient(self, x):
+    def _loss_terms(self, which, out, *tensors):
+        """out[n] += the per-image objective terms of one stage (unscaled weights, MSE means)."""
+        w, nl = self.w, self.G.n_latent * STYLE_DIM
+        S2 = 3 * self.size * self.size
+        if which == "lat":
+            lat, = tensors
+            ops.mse_sum(lat, self.lat_t, out, w["lat_t"] / nl)
+            ops.mse_sum(lat, self.lat_o, out, w["lat_o"] / nl)
+        elif which == "rec":
+            rec, a = tensors
+            ops.mse_sum(rec, self.t, out, w["img_rec_t"] / S2)
+            for k, tap in enumerate(self.V.taps(a)):
+                ops.mse_sum(tap, self.taps_t[k], out, w["vgg_rec_t"] / self.tap_numel[k])
+        else:
+            x, a = tensors
+            ops.mse_sum(x, self.x0, out, w["img_o"] / S2)
+            for k, tap in enumerate(self.V.taps(a)):
+                ops.mse_sum(tap, self.taps_o[k], out, w["vgg_img"] / self.tap_numel[k])
+
+    def gradient(self, x, loss=None):
         """One forward/backward of the objective at x. Leaves (g_vgg_x, g_enc) for the update and
-        returns them; both are scaled by loss_scale."""
+        returns them; both are scaled by loss_scale. ``loss`` (fp32 [N], zeroed by the caller)
+        receives the per-image objective at x from the same forward pass (no host sync)."""
         ws, G, V, E = self.ws, self.G, self.V, self.E
         N = x.shape[0]
         lat = E.forward(x, ws)
         rec = G.forward(lat, ws)
         self.rec = rec
+        if loss is not None:
+            self._loss_terms("lat", loss, lat)
         # reconstruction path: VGG(rec') vs VGG(t'), pixel MSE vs t
         a = V.forward(self._vgg_input(rec, "in.rec"), ws, "")
+        if loss is not None:
+            self._loss_terms("rec", loss, rec, a)
         g_rv = V.backward(a, self.taps_t, self.c_vgg_rec, ws, "r")
         g_img = ws.get("g.img", rec.shape, torch.float32)
         ops.image_grad(rec, self.t, g_rv, g_img, self.pf, self.c_img_rec)
         # input path: VGG(x') vs VGG(x0')
         a = V.forward(self._vgg_input(x, "in.x"), ws, "")
+        if loss is not None:
+            self._loss_terms("x", loss, x, a)
         g_xv = V.backward(a, self.taps_o, self.c_vgg_x, ws, "x")
         # latent terms, synthesis backward, encoder backward
         g_lat = ws.get("g.lat", lat.shape, torch.float32)
@@ -117,43 +143,93 @@ class AttackEngine:
         return x
 
     def full_gradient(self, x):
-        """∇_x L (unscaled, fp32 NCHW) assembled from the pieces — a diagnostic for tests."""
+        """∇_x L (unscaled, fp32 NCHW) at x."""
+        g = self.ws.get("g.full", x.shape, torch.float32)
         g_xv, g_enc = self.gradient(x)
-        N, S, pf = x.shape[0], self.size, self.pf
-        k = S // ENC_POOL_RES
-        g = self.c_img_o * (x - self.x0)
-        gv = g_xv[..., :3].permute(0, 3, 1, 2).float()
-        g = g + gv.repeat_interleave(pf, 2).repeat_interleave(pf, 3) / (pf * pf)
-        g = g + g_enc.repeat_interleave(k, 2).repeat_interleave(k, 3) / (k * k)
-        return g / self.loss_scale
+        ops.grad_assemble(x, self.x0, g_xv, g_enc, g, self.pf, ENC_POOL_RES, self.c_img_o,
+                          1.0 / self.loss_scale)
+        return g.clone()
 
-    def loss(self, x):
-        """Per-image objective value (fp32, host) — diagnostics only (syncs)."""
+    def objective(self, x, out):
+        """Per-image objective at x into out (fp32 [N], +=): forward passes only."""
         ws, G, V, E = self.ws, self.G, self.V, self.E
-        N = x.shape[0]
-        out = torch.zeros(8, N, device=x.device)
         lat = E.forward(x, ws)
         rec = G.forward(lat, ws)
-        nl = G.n_latent * STYLE_DIM
-        ops.mse_sum(lat, self.lat_t, out[0])
-        ops.mse_sum(lat, self.lat_o, out[1])
-        ops.mse_sum(rec, self.t, out[2])
-        ops.mse_sum(x, self.x0, out[4])
+        self._loss_terms("lat", out, lat)
         a = V.forward(self._vgg_input(rec, "in.rec"), ws, "")
-        for k, tap in enumerate(V.taps(a)):
-            tmp = torch.zeros(N, device=x.device)
-            ops.mse_sum(tap, self.taps_t[k], tmp)
-            out[3] += tmp / self.tap_numel[k]
+        self._loss_terms("rec", out, rec, a)
         a = V.forward(self._vgg_input(x, "in.x"), ws, "")
-        for k, tap in enumerate(V.taps(a)):
-            tmp = torch.zeros(N, device=x.device)
-            ops.mse_sum(tap, self.taps_o[k], tmp)
-            out[5] += tmp / self.tap_numel[k]
-        S2 = 3 * self.size * self.size
-        w = self.w
-        L = (w["lat_t"] * out[0] / nl + w["lat_o"] * out[1] / nl + w["img_rec_t"] * out[2] / S2
-             + w["vgg_rec_t"] * out[3] + w["img_o"] * out[4] / S2 + w["vgg_img"] * out[5])
-        return L.cpu()
+        self._loss_terms("x", out, x, a)
+        return out
+
+    def loss(self, x):
+        """Per-image objective value (fp32, host) — diagnostics (syncs)."""
+        out = self.ws.get("loss.diag", (x.shape[0],), torch.float32)
+        ops.zero_(out)
+        return self.objective(x, out).cpu()
+
+    def _full_grad(self, x, g, loss=None):
+        """g ← ∇_x L (loss-scaled, fp32 NCHW) by the gradient-assembly kernel."""
+        g_xv, g_enc = self.gradient(x, loss)
+        ops.grad_assemble(x, self.x0, g_xv, g_enc, g, self.pf, ENC_POOL_RES, self.c_img_o)
+        return g
+
+    def run_adam(self, x0, t, steps, lr=0.01, betas=(0.9, 0.999), eps=1e-8):
+        """``optimize_vgg`` literal mode (interpolation.py:743-843): Adam(lr) on the pixels,
+        descending L, no ε-ball or clamp. The gradient carries the loss scale λ, so Adam's eps is
+        scaled by λ too (m̂/(√v̂ + λ·eps) on λ·g ≡ m̂/(√v̂ + eps) on g)."""
+        self.prepare(x0, t)
+        ws = self.ws
+        x = ws.get("adv", x0.shape, torch.float32)
+        x.copy_(x0)
+        m = ops.zero_(ws.get("adam.m", x0.shape, torch.float32))
+        v = ops.zero_(ws.get("adam.v", x0.shape, torch.float32))
+        g = ws.get("g.full", x0.shape, torch.float32)
+        for it in range(1, steps + 1):
+            self._full_grad(x, g)
+            ops.adam_step(x, g, m, v, lr, betas[0], betas[1], eps * self.loss_scale, it)
+        return x.clone()
+
+    def run_cw(self, x0, t, steps, c=1e-4, lr=0.01, betas=(0.9, 0.999), eps=1e-8):
+        """torchattacks C&W L2 (interpolation.py:98-193) composed with the GAN objective, in
+        [-1,1] space: adv = tanh(w); cost = Σ‖(adv − x0)/2‖² + c·Σ L_n(adv); Adam(lr) on w;
+        best-L2 tracking with success = L_n(adv) < L_n(x0); early stop every steps//10 when the
+        cost rises (one host sync there). See oracle.attack_ref.cw_attack."""
+        self.prepare(x0, t)
+        ws = self.ws
+        N = x0.shape[0]
+        f32 = torch.float32
+        f0 = ops.zero_(ws.get("cw.f0", (N,), f32))
+        self.objective(x0, f0)
+        w = ops.cw_init(x0, ws.get("cw.w", x0.shape, f32))
+        adv = ws.get("adv", x0.shape, f32)
+        best = ws.get("cw.best", x0.shape, f32)
+        best.copy_(x0)
+        best_l2 = ws.get("cw.best_l2", (N,), f32)
+        best_l2.fill_(1e10)
+        m = ops.zero_(ws.get("adam.m", x0.shape, f32))
+        v = ops.zero_(ws.get("adam.v", x0.shape, f32))
+        g = ws.get("g.full", x0.shape, f32)
+        gw = ws.get("cw.gw", x0.shape, f32)
+        f = ws.get("cw.f", (N,), f32)
+        sq = ws.get("cw.sq", (N,), f32)
+        prev = 1e10
+        every = max(steps // 10, 1)
+        for step in range(steps):
+            ops.cw_tanh(w, adv)
+            ops.zero_(f)
+            self._full_grad(adv, g, loss=f)
+            ops.cw_grad(adv, x0, g, gw, c, 1.0 / self.loss_scale)
+            ops.adam_step(w, gw, m, v, lr, betas[0], betas[1], eps, step + 1)
+            ops.zero_(sq)
+            ops.mse_sum(adv, x0, sq)
+            ops.cw_select(adv, best, sq, best_l2, f, f0, 0.25)
+            if step % every == 0:
+                cost = 0.25 * float(sq.cpu().double().sum()) + c * float(f.cpu().double().sum())
+                if cost > prev:
+                    break
+                prev = cost
+        return best.clone()
 
     def run(self, x0, t, steps, eps, alpha, random_start=False, start_noise=None):
         """PGD-steps from x0 toward the objective; returns the adversarial images (new tensor)."""
@@ -179,8 +255,12 @@ def _check_images(imgs, size, name):
         raise ValueError(f"{name} must be floating point")
 
 
+NORMS = ("linf", "adam", "l2_cw")
+
+
 def attack(net, imgs, eps, steps, *, target=None, vgg=None, alpha=2 / 255, random_start=False,
-           seed=0, norm="linf", loss="gan_vgg", loss_scale=None, return_info=False):
+           seed=0, norm="linf", loss="gan_vgg", loss_scale=None, lr=0.01, cw_c=1e-4,
+           return_info=False):
     """Craft adversarial images against the GAN fusion pipeline.
 
     net     pSp-like bundle: net.encoder, net.decoder (.size), net.latent_avg, net.opts
@@ -188,12 +268,19 @@ def attack(net, imgs, eps, steps, *, target=None, vgg=None, alpha=2 / 255, rando
     imgs    (N,3,S,S) float tensor in [-1,1] (reference normalisation, transforms_config.py:29-31),
             on CPU or GPU; not modified.
     eps     L∞ radius in [0,1] pixel units (8/255 in the reference's PGD call, interpolation.py:1343).
-    steps   PGD iterations (1 with alpha=eps and random_start=False is FGSM).
+    steps   iterations (PGD: 1 with alpha=eps and random_start=False is FGSM).
     target  white-box target image(s) (N or 1, 3, S, S) — the ``img_target`` of optimize_vgg.
+    norm    'linf'  — torchattacks PGD rule (interpolation.py:62-96) on the objective;
+            'adam'  — optimize_vgg literal (interpolation.py:743-843): Adam(lr) on the pixels,
+                      no ε-ball (eps is ignored and may be None);
+            'l2_cw' — torchattacks C&W L2 (interpolation.py:98-193) with f = the objective,
+                      c = cw_c, Adam(lr) in tanh space (eps ignored; see AttackEngine.run_cw).
     Returns the adversarial images on the input's device (fp32), and a dict if return_info.
     """
-    if norm != "linf" or loss != "gan_vgg":
-        raise ValueError("only norm='linf', loss='gan_vgg' are implemented")
+    if norm not in NORMS:
+        raise ValueError(f"norm must be one of {NORMS}")
+    if loss != "gan_vgg":
+        raise ValueError("only loss='gan_vgg' (the optimize_vgg objective) is implemented")
     size = net.decoder.size
     _check_images(imgs, size, "imgs")
     if target is None:
@@ -205,8 +292,12 @@ def attack(net, imgs, eps, steps, *, target=None, vgg=None, alpha=2 / 255, rando
     _check_images(target, size, "target")
     if target.shape[0] != imgs.shape[0]:
         raise ValueError("target batch must be 1 or match imgs")
-    if not (eps > 0 and alpha > 0) or steps < 0 or int(steps) != steps:
-        raise ValueError("need eps > 0, alpha > 0, integer steps >= 0")
+    if steps < 0 or int(steps) != steps:
+        raise ValueError("need integer steps >= 0")
+    if norm == "linf" and not (eps is not None and eps > 0 and alpha > 0):
+        raise ValueError("PGD needs eps > 0 and alpha > 0")
+    if norm != "linf" and not lr > 0:
+        raise ValueError("lr must be > 0")
     if float(imgs.min()) < -1.0 or float(imgs.max()) > 1.0:
         raise ValueError("imgs must lie in [-1, 1]")
     vgg = vgg if vgg is not None else getattr(net, "vgg", None)
@@ -220,10 +311,15 @@ def attack(net, imgs, eps, steps, *, target=None, vgg=None, alpha=2 / 255, rando
     if random_start:
         g = torch.Generator().manual_seed(int(seed))
         noise = (torch.rand(x0.shape, generator=g) * 2 - 1).to(dev)
-    adv = eng.run(x0, t, int(steps), float(eps), float(alpha), random_start, noise)
+    if norm == "linf":
+        adv = eng.run(x0, t, int(steps), float(eps), float(alpha), random_start, noise)
+    elif norm == "adam":
+        adv = eng.run_adam(x0, t, int(steps), lr=float(lr))
+    else:
+        adv = eng.run_cw(x0, t, int(steps), c=float(cw_c), lr=float(lr))
     adv = adv.to(imgs.device)
     if return_info:
-        info = dict(loss=eng.loss(adv.to(dev)), steps=int(steps), eps=eps, alpha=alpha,
+        info = dict(loss=eng.loss(adv.to(dev)), steps=int(steps), eps=eps, alpha=alpha, norm=norm,
                     dtype=str(eng.dtype), loss_scale=eng.loss_scale)
         return adv, info
     return adv

@@ -171,9 +171,9 @@ int mia_avgpool_bwd(const float* gy, float* gx, int planes, int H, int W, int k,
 /* NCHW fp32 image (N,3,S,S) → avg_pool(pf) → NHWC (N,S/pf,S/pf,cpad) dtype, channels ≥3 zero. */
 int mia_image_to_nhwc(const float* x, void* y, int N, int S, int pf, int cpad, int dtype,
                       void* stream);
-/* Σ over an image of (a − b)² for a [n][len] pair (fp32 or dtype), into loss[n] (+=). K10 value. */
-int mia_mse_sum(const void* a, const void* b, float* loss, int n, int64_t len, int dtype,
-                void* stream);
+/* coef·Σ over an image of (a − b)² for a [n][len] pair (dtype), into loss[n] (+=). K10 value. */
+int mia_mse_sum(const void* a, const void* b, float* loss, int n, int64_t len, float coef,
+                int dtype, void* stream);
 /* K10 gradient for flat fp32 tensors: g (+)= coef·(a − b). */
 int mia_mse_grad_f32(const float* a, const float* b, float* g, int64_t len, float coef,
                      int accumulate, void* stream);
@@ -192,6 +192,24 @@ int mia_pgd_update(float* x, const float* x0, const void* g_vgg, const float* g_
                    float lo, float hi, int dtype, void* stream);
 /* PGD random start (torchattacks PGD.forward, interpolation.py:73-76): x = clamp(x0 + e·u, lo, hi),
  * u = host-seeded U(-1,1) draws. */
+/* ∇_x L as an fp32 image: scale·(coef_img·(x − x0) + avg_pool adjoints of the VGG input-path
+ * gradient g_vgg (N,S/pf,S/pf,cpad; dtype) and of the encoder gradient g_enc (N,3,enc_res²)).
+ * The gradient the fused PGD update (mia_pgd_update) projects, materialised for the Adam
+ * (optimize_vgg, interpolation.py:767,822) and C&W modes. */
+int mia_grad_assemble(const float* x, const float* x0, const void* g_vgg, const float* g_enc,
+                      float* g, int N, int S, int pf, int cpad, int enc_res, float coef_img,
+                      float scale, int dtype, void* stream);
+/* C&W L2 in tanh space (torchattacks CW, interpolation.py:98-193), images in [-1,1]:
+ * w = atanh(x) (x clamped to ±(1 − 2^-20)); adv = tanh(w);
+ * g_w = (½(adv − x) + c·scale·g_f)·(1 − adv²) for cost = Σ‖(adv − x)/2‖² + c·Σ f(adv);
+ * select: per image n, if f[n] < f0[n] and l2_scale·sq[n] < best_l2[n], best_adv[n] = adv[n]. */
+int mia_cw_init(const float* x, float* w, int64_t len, void* stream);
+int mia_cw_tanh(const float* w, float* adv, int64_t len, void* stream);
+int mia_cw_grad(const float* adv, const float* x, const float* g_f, float* g_w, int64_t len,
+                float c, float scale, void* stream);
+int mia_cw_select(const float* adv, float* best_adv, const float* sq, float* best_l2,
+                  const float* f, const float* f0, int N, int64_t plane, float l2_scale,
+                  void* stream);
 int mia_random_start(float* x, const float* x0, const float* u, int64_t len, float e, float lo,
                      float hi, void* stream);
 /* K11 alone, given a full fp32 gradient (bit-exact contract vs torch fp32). */

@@ -21,6 +21,8 @@ Contents (plain PyTorch CPU ops, fp32 or fp64, autograd for the backward):
                       unpinned (it is the build's own definition).
 * ``attack_ref``    — the white-box objective of ``code/attack/interpolation.py:786-818`` and the
                       torchattacks PGD update rule copied in comments at
-                      ``code/attack/interpolation.py:62-96`` (torchattacks is un-vendored and
-                      unpinned). Parity unpinned beyond the VGG part.
+                      ``code/attack/interpolation.py:62-96``, the Adam pixel mode of
+                      ``optimize_vgg`` (``:767,822``) and the torchattacks C&W rule
+                      (``:98-193``) composed with the GAN objective (torchattacks is un-vendored
+                      and unpinned). Parity unpinned beyond the VGG part.
 """

@@ -100,3 +100,57 @@ def pgd(gp, vp, ep, x0, t, size, eps, alpha, steps, random_start=False, start_no
             grads.append(g)
         adv = project_step(adv, x0, g, e, a)
     return (adv, grads) if return_grads else adv
+
+
+def adam_attack(gp, vp, ep, x0, t, size, steps, lr=0.01, betas=(0.9, 0.999), eps=1e-8,
+                dtype=torch.float32):
+    """``optimize_vgg`` literal mode (interpolation.py:743-843): ``Adam([img], lr)`` descending
+    L for ``steps`` iterations, no ε-ball, no clamp; img starts at x0 (:607-617)."""
+    x0 = x0.to(dtype)
+    refs = Refs(gp, vp, ep, x0, t.to(dtype), size)
+    img = x0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([img], lr=lr, betas=betas, eps=eps)
+    for _ in range(steps):
+        opt.zero_grad()
+        L = objective(gp, vp, ep, img, refs, size)
+        L.backward()
+        opt.step()
+    return img.detach()
+
+
+def cw_attack(gp, vp, ep, x0, t, size, steps, c=1e-4, lr=0.01, dtype=torch.float32):
+    """torchattacks ``CW.forward`` (commented copy at interpolation.py:98-193) composed with the
+    GAN objective in [-1,1] image space: adv = tanh(w) (= 2·½(tanh w + 1) − 1), w0 = atanh(x0)
+    (x0 clamped to ±(1 − 2⁻²⁰)); per image L2 = ‖(adv − x0)/2‖² (the [0,1]-space MSE sum of
+    :132-134); f_n = the objective L_n (no logits: κ does not apply); cost = Σ L2 + c·Σ f;
+    Adam(lr) on w; best-L2 tracking where "success" = L_n(adv) < L_n(x0) (the objective improved on
+    the clean image: the GAN analogue of "misclassified", :154-163); early stop every steps//10
+    when the cost rises (:166-170)."""
+    x0 = x0.to(dtype)
+    refs = Refs(gp, vp, ep, x0, t.to(dtype), size)
+    with torch.no_grad():
+        f0 = objective(gp, vp, ep, x0, refs, size, per_image=True)
+    lim = 1.0 - 2.0 ** -20
+    w = torch.atanh(x0.clamp(-lim, lim)).detach().requires_grad_(True)
+    best = x0.clone()
+    best_l2 = torch.full((x0.shape[0],), 1e10, dtype=dtype)
+    prev = 1e10
+    opt = torch.optim.Adam([w], lr=lr)
+    for step in range(steps):
+        adv = torch.tanh(w)
+        cur_l2 = (((adv - x0) / 2) ** 2).reshape(x0.shape[0], -1).sum(dim=1)
+        f = objective(gp, vp, ep, adv, refs, size, per_image=True)
+        cost = cur_l2.sum() + c * f.sum()
+        opt.zero_grad()
+        cost.backward()
+        opt.step()
+        with torch.no_grad():
+            mask = ((f < f0) & (best_l2 > cur_l2)).to(dtype)
+            best_l2 = mask * cur_l2 + (1 - mask) * best_l2
+            m4 = mask.view(-1, 1, 1, 1)
+            best = m4 * adv + (1 - m4) * best
+        if step % max(steps // 10, 1) == 0:
+            if cost.item() > prev:
+                return best
+            prev = cost.item()
+    return best

@@ -161,6 +161,50 @@ def test_pgd_matches_oracle_on_sign_stable_pixels(cuda):
     assert ((adv - x0).abs() <= e + 1e-6).all() and adv.abs().max() <= 1.0
 
 
+def test_objective_from_gradient_pass_matches_oracle(cuda):
+    """The per-image objective accumulated during the gradient pass (C&W needs it every step)
+    equals the forward-only objective and the fp64 oracle."""
+    eng, x0, t, (gp, vp, ep) = _engine(32, torch.float32, 2, cuda, seed=4)
+    x = (x0 + 0.05 * seeded(9, x0.shape)).clamp(-1, 1)
+    gp64 = {k: v.double() for k, v in gp.items()}
+    vp64 = {k: (w.double(), b.double()) for k, (w, b) in vp.items()}
+    ep64 = {k: (v.double() if torch.is_tensor(v) else v) for k, v in ep.items()}
+    refs = attack_ref.Refs(gp64, vp64, ep64, x0.double(), t.double(), 32)
+    ref = attack_ref.objective(gp64, vp64, ep64, x.double(), refs, 32, per_image=True)
+    eng.prepare(x0.to(cuda), t.to(cuda))
+    f = torch.zeros(2, device=cuda)
+    eng.gradient(x.to(cuda), loss=f)
+    assert rel_err(f, ref) < 1e-4
+    assert rel_err(eng.loss(x.to(cuda)), ref) < 1e-4
+
+
+def test_adam_mode_matches_oracle(cuda):
+    """norm='adam' (optimize_vgg literal: Adam on pixels, no ε-ball) vs torch.optim.Adam through
+    the fp32 oracle. Adam's step is ≈ lr·sign(g) where |g| ≫ eps, so pixels whose gradient sits
+    at the fp32 noise floor may move differently: ≤ 1 % of pixels beyond 1e-3."""
+    size, N, steps, lr = 32, 2, 3, 0.01
+    eng, x0, t, (gp, vp, ep) = _engine(size, torch.float32, N, cuda, seed=5)
+    adv = eng.run_adam(x0.to(cuda), t.to(cuda), steps, lr=lr).cpu()
+    ref = attack_ref.adam_attack(gp, vp, ep, x0, t, size, steps, lr=lr)
+    d = (adv - ref).abs()
+    assert (d > 1e-3).float().mean().item() <= 1e-2
+    assert d.max().item() <= 2 * lr * steps + 1e-6
+    assert (adv - x0).abs().max().item() > 0.5 * lr  # it moved
+
+
+@pytest.mark.parametrize("c", [1e-4, 10.0])
+def test_cw_mode_matches_oracle(cuda, c):
+    """norm='l2_cw' (torchattacks C&W composed with the objective) vs the oracle restatement:
+    tanh space, Adam on w, best-L2 selection with success = objective below the clean image's."""
+    size, N, steps, lr = 32, 2, 4, 0.01
+    eng, x0, t, (gp, vp, ep) = _engine(size, torch.float32, N, cuda, seed=6)
+    adv = eng.run_cw(x0.to(cuda), t.to(cuda), steps, c=c, lr=lr).cpu()
+    ref = attack_ref.cw_attack(gp, vp, ep, x0, t, size, steps, c=c, lr=lr)
+    d = (adv - ref).abs()
+    assert (d > 1e-3).float().mean().item() <= 1e-2
+    assert adv.abs().max().item() <= 1.0
+
+
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 def test_low_precision_gradient_sign_agreement(cuda, dtype):
     eng, x0, t, _ = _engine(64, dtype, 2, cuda, seed=2)

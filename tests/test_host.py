@@ -139,6 +139,12 @@ def test_attack_argument_validation_before_any_device_work():
         attack(net, x, -1.0, 2, target=t)                              # eps <= 0
     with pytest.raises(ValueError):
         attack(net, x, 8 / 255, 2, target=t, norm="l2")                # unsupported norm
+    with pytest.raises(ValueError):
+        attack(net, x, None, 2, target=t, norm="adam", lr=0.0)         # Adam needs lr > 0
+    with pytest.raises(ValueError):
+        attack(net, x, None, 2, target=t, norm="linf")                 # PGD needs eps
+    with pytest.raises(ValueError):
+        attack(net, x, 8 / 255, 1.5, target=t)                         # integer steps
 
 
 def test_no_cpu_fallback_in_product():

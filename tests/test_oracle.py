@@ -142,3 +142,23 @@ def test_vgg_conv_table():
     assert [c[1:] for c in VGG_CONVS[:9]] == [(3, 64), (64, 64), (64, 128), (128, 128),
                                               (128, 256), (256, 256), (256, 256), (256, 512),
                                               (512, 512)]
+
+
+def test_oracle_adam_and_cw_modes_basic_properties():
+    """Adam's first step moves (almost) every pixel by ≈ lr (m̂/√v̂ = sign g); C&W keeps adv in
+    (-1, 1) and returns an iterate within the Adam step bound of x0."""
+    from gfa_amd.weights import make_generator_weights, make_vgg_weights
+    size = 32
+    gp = make_generator_weights(size, seed=0)
+    ep = make_encoder_weights(size, seed=1)
+    vp = vgg_ref.load_positional(make_vgg_weights(1234))
+    g = torch.Generator().manual_seed(3)
+    x0 = torch.rand(1, 3, size, size, generator=g) * 2 - 1
+    t = torch.rand(1, 3, size, size, generator=g) * 2 - 1
+    adv = attack_ref.adam_attack(gp, vp, ep, x0, t, size, 1, lr=0.01)
+    d = (adv - x0).abs()
+    assert ((d - 0.01).abs() < 1e-3).float().mean() > 0.9
+    cw = attack_ref.cw_attack(gp, vp, ep, x0, t, size, 2, c=10.0, lr=0.01)
+    assert torch.isfinite(cw).all() and cw.abs().max() < 1.0
+    # the selected image is one of the iterates within lr-sized steps of x0 (or x0 itself)
+    assert (cw - x0).abs().max() <= 2 * 0.01 + 1e-6

@@ -12,19 +12,20 @@ Submodules import lazily so the package can be imported (and the library inspect
 without a GPU; any compute call without the library or a GPU raises.
 """
 __all__ = ["attack", "fgsm", "build_net", "vgg16", "get_latents", "StyleFusionSimple",
-           "attack_distributed"]
+           "interpolation", "attack_distributed"]
 
 
 def __getattr__(name):
     if name in ("attack", "fgsm", "AttackEngine"):
         from . import pgd as _a
         return getattr(_a, name)
-    if name in ("build_net", "vgg16", "get_latents", "PSPNet", "Decoder", "Encoder", "VGGBase"):
+    if name in ("build_net", "vgg16", "get_latents", "PSPNet", "Decoder", "Encoder", "VGGBase",
+                "MappingNet"):
         from . import networks as _n
         return getattr(_n, name)
-    if name == "StyleFusionSimple":
-        from .style_fusion_simple import StyleFusionSimple
-        return StyleFusionSimple
+    if name in ("StyleFusionSimple", "interpolation"):
+        from . import style_fusion_simple as _f
+        return getattr(_f, name)
     if name == "attack_distributed":
         from .dist import attack_distributed
         return attack_distributed

@@ -100,6 +100,8 @@ SIGNATURES = {
     "mia_gemm_f32_grouped": (c_int, [ctypes.POINTER(GemmGroup), c_int, P]),
     "mia_style_demod": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
     "mia_demod_bwd": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
+    "mia_pixel_norm": (c_int, [P, P, c_int, c_int, c_float, P]),
+    "mia_truncate": (c_int, [P, P, c_float, P, c_int, c_int, P]),
     "mia_repeat": (c_int, [P, P, c_int64, c_int, P]),
     "mia_memset": (c_int, [P, c_int, c_int64, P]),
 }

@@ -802,6 +802,38 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   }
 }
 
+// PixelNorm of the mapping network input (rosinality PixelNorm): y = x / sqrt(mean(x²) + eps)
+// over each row of `cols` values; one block per row.
+__global__ void pixel_norm_kernel(const float* __restrict__ x, float* __restrict__ y, int cols,
+                                  float eps) {
+  const float* xr = x + (size_t)blockIdx.x * cols;
+  float* yr = y + (size_t)blockIdx.x * cols;
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < cols; i += TPB) acc += xr[i] * xr[i];
+  __shared__ float red[TPB / 64];
+  __shared__ float inv;
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int w = 0; w < TPB / 64; ++w) s += red[w];
+    inv = rsqrtf(s / (float)cols + eps);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < cols; i += TPB) yr[i] = xr[i] * inv;
+}
+
+// Truncation trick (rosinality Generator.forward): out = mean + psi·(w − mean), mean broadcast
+// over rows.
+__global__ void truncate_kernel(const float* __restrict__ w, const float* __restrict__ mean,
+                                float psi, float* __restrict__ out, int64_t len, int cols) {
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < len; i += (int64_t)gridDim.x * TPB) {
+    const float m = mean[i % cols];
+    out[i] = m + psi * (w[i] - m);
+  }
+}
+
 __global__ void repeat_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                               int64_t bytes, int count) {
   const int64_t total = bytes * count;
@@ -1122,6 +1154,20 @@ extern "C" int mia_adam_step(float* p, const float* g, float* m, float* v, int64
   const float bc2sqrt = sqrtf(1.f - powf(beta2, (float)t));
   MIA_LAUNCH(adam_kernel, dim3(blocks_for(len, TPB, 65536)), dim3(TPB), 0, p, g, m, v, len, lr,
              beta1, beta2, eps, bc1, bc2sqrt);
+}
+
+extern "C" int mia_pixel_norm(const float* x, float* y, int rows, int cols, float eps,
+                              void* stream) {
+  MIA_CHECK_ARG(x && y && rows > 0 && cols > 0, "bad args");
+  MIA_LAUNCH(pixel_norm_kernel, dim3(rows), dim3(TPB), 0, x, y, cols, eps);
+}
+
+extern "C" int mia_truncate(const float* w, const float* mean, float psi, float* out, int rows,
+                            int cols, void* stream) {
+  MIA_CHECK_ARG(w && mean && out && rows > 0 && cols > 0, "bad args");
+  const int64_t len = (int64_t)rows * cols;
+  MIA_LAUNCH(truncate_kernel, dim3(blocks_for(len, TPB, 65536)), dim3(TPB), 0, w, mean, psi, out,
+             len, cols);
 }
 
 extern "C" int mia_repeat(const void* src, void* dst, int64_t bytes, int count, void* stream) {

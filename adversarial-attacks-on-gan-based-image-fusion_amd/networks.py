@@ -7,20 +7,69 @@
   (attack_main2.py:137-146; utils/model_utils.py:7-18).
 * ``VGGBase`` / ``vgg16(pth)`` — code/vgg.py:6-81: ``vgg(x) -> (conv1_1, conv1_2, conv3_2, conv4_2)``.
 * ``get_latents(net, x)`` — attack_main2.py:137-146 (adds latent_avg when the option is set).
+* ``MappingNet`` — the rosinality mapping MLP (z → w) behind the fusion entry point
+  (style_fusion_simple.py:110-119, mean_latent at :58).
 
 Forward calls here allocate their outputs and return NCHW fp32 tensors (reference layout); the
 attack itself works on the NHWC device buffers directly.
 """
 import argparse
+import math
 
 import torch
 
 from .encoder import SyntheticEncoder
 from .stylegan2 import SynthesisNet
 from .vgg import CPAD, VGGNet
-from .weights import make_encoder_weights, make_generator_weights, make_vgg_weights
+from .weights import (LR_MLP, N_MLP, STYLE_DIM, make_encoder_weights, make_generator_weights,
+                      make_vgg_weights)
 from .workspace import Workspace
 from . import ops
+
+
+class MappingNet:
+    """rosinality Generator.style on device: PixelNorm, then N_MLP × EqualLinear(512, 512,
+    lr_mul=0.01, fused_lrelu) = GEMM (mia_gemm_f32) + lrelu(·+b·lr_mul)·√2 (mia_bias_act_fwd)."""
+
+    def __init__(self, params, device="cuda"):
+        dev = torch.device(device)
+        self.device = dev
+        scale = LR_MLP / math.sqrt(STYLE_DIM)
+        self.w = [(params[f"style.{i}.weight"].double() * scale).float().contiguous().to(dev)
+                  for i in range(1, N_MLP + 1)]
+        self.b = [(params[f"style.{i}.bias"].double() * LR_MLP).float().contiguous().to(dev)
+                  for i in range(1, N_MLP + 1)]
+        self._ws = Workspace(dev)
+
+    def __call__(self, z):
+        """z: (N, 512) → w: (N, 512) fp32 (a new tensor)."""
+        z = z.to(self.device, torch.float32).contiguous()
+        N = z.shape[0]
+        if tuple(z.shape) != (N, STYLE_DIM):
+            raise ValueError("z must be (N, 512)")
+        a = self._ws.get("map.a", (N, STYLE_DIM), torch.float32)
+        b = self._ws.get("map.b", (N, STYLE_DIM), torch.float32)
+        ops.pixel_norm(z, a)
+        for w, bias in zip(self.w, self.b):
+            # y = a·Wᵀ: B[k][n] = W[n][k]
+            ops.gemm(N, STYLE_DIM, STYLE_DIM, 1.0, a, STYLE_DIM, 1, w, 1, STYLE_DIM, 0.0, b,
+                     STYLE_DIM, 1)
+            ops.bias_act_fwd(b.view(N, 1, 1, STYLE_DIM), None, 0.0, bias,
+                             a.view(N, 1, 1, STYLE_DIM))
+        return a.clone()
+
+    def mean_latent(self, n_latent=4096, seed=0):
+        """Generator.mean_latent: the mean of n_latent mapped z ~ N(0, I) (host-seeded draws;
+        the mean is a ones-vector GEMM)."""
+        g = torch.Generator().manual_seed(int(seed))
+        z = torch.randn(n_latent, STYLE_DIM, generator=g)
+        w = self(z)
+        ones = self._ws.get("map.ones", (1, n_latent), torch.float32)
+        ones.fill_(1.0)
+        mean = torch.empty(1, STYLE_DIM, device=self.device)
+        ops.gemm(1, STYLE_DIM, n_latent, 1.0 / n_latent, ones, n_latent, 1, w, STYLE_DIM, 1, 0.0,
+                 mean, STYLE_DIM, 1)
+        return mean
 
 
 class Decoder:
@@ -30,20 +79,36 @@ class Decoder:
         self.n_latent = self.impl.n_latent
         self.device = self.impl.device
         self._ws = Workspace(self.device)
+        self.mapping = MappingNet(params, device) if "style.1.weight" in params else None
+
+    def _truncate(self, lat, truncation, truncation_latent):
+        if truncation == 1:
+            return lat
+        if truncation_latent is None:
+            raise ValueError("truncation != 1 needs truncation_latent")
+        mean = truncation_latent.to(self.device, torch.float32).reshape(-1).contiguous()
+        out = torch.empty_like(lat)
+        return ops.truncate(lat, mean, float(truncation), out)
 
     def __call__(self, styles, input_is_latent=True, randomize_noise=False, return_latents=False,
                  truncation=1, truncation_latent=None):
-        if not input_is_latent:
-            raise ValueError("only input_is_latent=True is supported (the mapping MLP is not part "
-                             "of the attack path, attack_main2.py:619)")
+        """rosinality Generator.forward subset: [w] or [w+] with input_is_latent=True
+        (attack_main2.py:619-621), or [z] through the mapping MLP; truncation toward
+        truncation_latent; fixed noise only."""
         if randomize_noise:
             raise ValueError("randomize_noise=False only (fixed noise buffers, attack_main2.py:620)")
         lat = styles[0] if isinstance(styles, (list, tuple)) else styles
+        lat = lat.to(self.device, torch.float32).contiguous()
+        if not input_is_latent:
+            if self.mapping is None:
+                raise ValueError("z input needs the mapping MLP weights (style.{1..8}.*)")
+            if lat.dim() != 2:
+                raise ValueError("z must be (N, 512)")
+            lat = self.mapping(lat)
+        lat = self._truncate(lat, truncation, truncation_latent)
         if lat.dim() == 2:
             lat = lat.unsqueeze(1).repeat(1, self.n_latent, 1)
-        if truncation != 1:
-            lat = truncation_latent + truncation * (lat - truncation_latent)
-        lat = lat.to(self.device, torch.float32).contiguous()
+        lat = lat.contiguous()
         img = self.impl.forward(lat, self._ws).clone()
         return img, (lat if return_latents else None)
 

@@ -532,6 +532,22 @@ def repeat(src, dst, count):
     return dst
 
 
+def pixel_norm(x, y, eps=1e-8):
+    rows, cols = x.shape
+    _need(y, x.shape, torch.float32, "y")
+    call("mia_pixel_norm", ptr(x), ptr(y), rows, cols, float(eps), stream())
+    return y
+
+
+def truncate(w, mean, psi, out):
+    cols = w.shape[-1]
+    rows = w.numel() // cols
+    _need(out, w.shape, torch.float32, "out")
+    _numel_ok(mean, cols, torch.float32, "mean")
+    call("mia_truncate", ptr(w), ptr(mean), float(psi), ptr(out), rows, cols, stream())
+    return out
+
+
 def zero_(t):
     call("mia_memset", ptr(t), 0, t.numel() * t.element_size(), stream())
     return t

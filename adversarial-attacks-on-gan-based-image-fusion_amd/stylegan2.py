@@ -118,13 +118,58 @@ class SynthesisNet:
                 ops.style_demod(L["_s"], L["wsq"], d)
                 L["_d"] = d
 
+    def style_order(self):
+        """Modulated layers in generator forward order (conv1, to_rgb1, then per resolution:
+        up-conv, conv, to_rgb) as indices into convs + torgbs — the order of SFGenerator's style
+        vector (style_fusion_simple.py:126-153)."""
+        nc = len(self.convs)
+        order = [0, nc]
+        for k in range(len(self.torgbs) - 1):
+            order += [1 + 2 * k, 2 + 2 * k, nc + 1 + k]
+        return order
+
+    def style_vectors(self, lat, ws):
+        """Per-layer styles s (fp32 (N, Cin) each) for W+ latents, generator forward order."""
+        self.styles(lat, ws)
+        layers = self.convs + self.torgbs
+        return [layers[i]["_s"].clone() for i in self.style_order()]
+
+    def set_styles(self, styles, ws):
+        """Install given per-layer styles (generator forward order) and their demodulation."""
+        layers = self.convs + self.torgbs
+        order = self.style_order()
+        if len(styles) != len(order):
+            raise ValueError(f"{len(order)} style vectors expected, got {len(styles)}")
+        N = styles[0].shape[0]
+        for s_in, i in zip(styles, order):
+            L = layers[i]
+            if tuple(s_in.shape) != (N, L["cin"]):
+                raise ValueError(f"style of layer {L['name']}: shape {tuple(s_in.shape)} != "
+                                 f"{(N, L['cin'])}")
+            s = ws.get(f"g.s{i}", (N, L["cin"]), torch.float32)
+            s.copy_(s_in)
+            L["_s"] = s
+            if "wsq" in L:
+                d = ws.get(f"g.d{i}", (N, L["cout"]), torch.float32)
+                ops.style_demod(s, L["wsq"], d)
+                L["_d"] = d
+        self._style_key = None  # the W+ → s plan no longer describes the installed styles
+
+    def forward_styles(self, styles, ws):
+        """Image from per-layer styles (SFGenerator style_vector path)."""
+        self.set_styles(styles, ws)
+        return self._synthesize(styles[0].shape[0], ws)
+
     def forward(self, lat, ws):
         """lat: (N, n_latent, 512) fp32 → image (N,3,S,S) fp32 (the rosinality ``skip``)."""
         N = lat.shape[0]
         if tuple(lat.shape[1:]) != (self.n_latent, STYLE_DIM) or lat.dtype != torch.float32:
             raise ValueError(f"latent must be (N,{self.n_latent},512) fp32")
-        T = self.dtype
         self.styles(lat, ws)
+        return self._synthesize(N, ws)
+
+    def _synthesize(self, N, ws):
+        T = self.dtype
         x0 = ws.get("g.const", (N, 4, 4, self.const.shape[-1]), T)
         ops.repeat(self.const, x0, N)
         x = x0

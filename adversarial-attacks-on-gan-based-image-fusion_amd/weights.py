@@ -9,8 +9,9 @@ Names follow the state-dict keys of the modules the reference calls:
 * StyleGAN2 generator (rosinality ``model.py`` API, used as ``net.decoder`` at
   ``code/attack/attack_main2.py:619-621`` and as ``SFGenerator_hook`` at
   ``code/style_fusion_simple.py:51``): ``input.input``, ``conv1.*``, ``to_rgb1.*``, ``convs.{i}.*``,
-  ``to_rgbs.{i}.*``, ``noises.noise_{i}``. The mapping MLP is omitted: the attack always calls the
-  decoder with ``input_is_latent=True`` (``attack_main2.py:619``).
+  ``to_rgbs.{i}.*``, ``noises.noise_{i}``, and the mapping MLP ``style.{1..8}.*`` (used only by the
+  fusion entry point's z → W path, ``style_fusion_simple.py:110-119``; the attack calls the
+  decoder with ``input_is_latent=True``, ``attack_main2.py:619``).
 * VGG16 trunk (``code/vgg.py:12-39``): positional list of 13 convs, loaded like
   ``VGGBase.load_pretrained_layers`` (``code/vgg.py:66-76``).
 * Encoder: a deterministic linear stand-in for e4e behind the ``net.encoder`` slot
@@ -21,6 +22,8 @@ import math
 import torch
 
 STYLE_DIM = 512
+N_MLP = 8          # rosinality Generator(n_mlp=8) (style_fusion_simple.py:51: SFGenerator_hook(.., 8))
+LR_MLP = 0.01      # EqualLinear lr_mul of the mapping layers
 
 
 def generator_channels(channel_multiplier=2):
@@ -97,6 +100,12 @@ def make_generator_weights(size, seed=0, channel_multiplier=2, noise_weight=0.1,
     for i in range((log_size - 2) * 2 + 1):
         r = 2 ** ((i + 5) // 2)
         p[f"noises.noise_{i}"] = torch.randn(1, 1, r, r, generator=g)
+    # mapping MLP (own stream, so the synthesis weights above do not depend on it): EqualLinear
+    # stores weight ~ N(0,1)/lr_mul; the bias (0 at rosinality init) is made non-zero here
+    gm = torch.Generator().manual_seed(int(seed) + 7919)
+    for i in range(1, N_MLP + 1):
+        p[f"style.{i}.weight"] = torch.randn(STYLE_DIM, STYLE_DIM, generator=gm) / LR_MLP
+        p[f"style.{i}.bias"] = bias_std * torch.randn(STYLE_DIM, generator=gm) / LR_MLP
     return p
 
 

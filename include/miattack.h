@@ -251,6 +251,12 @@ int mia_style_demod(const float* s, const float* wsq, float* demod, int N, int C
 /* gs[n][ci] += −scale2·s[n][ci]·Σ_co q[n][co]·demod[n][co]²·wsq[co][ci] */
 int mia_demod_bwd(const float* q, const float* demod, const float* wsq, const float* s, float* gs,
                   int N, int Cin, int Cout, float scale2, void* stream);
+/* Mapping-network plumbing for the fusion entry point (style_fusion_simple.py:110-142 via the
+ * rosinality Generator [ext]): PixelNorm y = x / sqrt(mean_row(x²) + eps) (fp32 [rows][cols]);
+ * truncation out = mean + psi·(w − mean) with mean [cols] broadcast over rows. */
+int mia_pixel_norm(const float* x, float* y, int rows, int cols, float eps, void* stream);
+int mia_truncate(const float* w, const float* mean, float psi, float* out, int rows, int cols,
+                 void* stream);
 /* dst[i*bytes .. ] = src for i < count (broadcast the constant input over the batch). */
 int mia_repeat(const void* src, void* dst, int64_t bytes, int count, void* stream);
 int mia_memset(void* dst, int value, int64_t bytes, void* stream);

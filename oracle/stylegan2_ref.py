@@ -56,11 +56,12 @@ def style_affine(p, prefix, w):
     return F.linear(w, a * (1.0 / math.sqrt(a.shape[1])), b)
 
 
-def modulated_conv2d(p, prefix, x, w, demodulate=True, upsample=False):
+def modulated_conv2d(p, prefix, x, w, demodulate=True, upsample=False, s=None):
+    """``s``: the layer's style vector given directly (style_vector path), else A·w + b."""
     weight = p[prefix + ".weight"].to(x.dtype)  # (1, out, in, k, k)
     _, cout, cin, k, _ = weight.shape
     n = x.shape[0]
-    style = style_affine(p, prefix, w).view(n, 1, cin, 1, 1)
+    style = (style_affine(p, prefix, w) if s is None else s.to(x.dtype)).view(n, 1, cin, 1, 1)
     scale = 1.0 / math.sqrt(cin * k * k)
     wt = scale * weight * style
     if demodulate:
@@ -81,15 +82,15 @@ def modulated_conv2d(p, prefix, x, w, demodulate=True, upsample=False):
     return out
 
 
-def styled_conv(p, prefix, x, w, noise, upsample=False):
-    out = modulated_conv2d(p, prefix + ".conv", x, w, demodulate=True, upsample=upsample)
+def styled_conv(p, prefix, x, w, noise, upsample=False, s=None):
+    out = modulated_conv2d(p, prefix + ".conv", x, w, demodulate=True, upsample=upsample, s=s)
     out = out + p[prefix + ".noise.weight"].to(x.dtype) * noise.to(x.dtype)
     b = p[prefix + ".activate.bias"].to(x.dtype)
     return F.leaky_relu(out + b.view(1, -1, 1, 1), 0.2) * math.sqrt(2.0)
 
 
-def to_rgb(p, prefix, x, w, skip=None):
-    out = modulated_conv2d(p, prefix + ".conv", x, w, demodulate=False)
+def to_rgb(p, prefix, x, w, skip=None, s=None):
+    out = modulated_conv2d(p, prefix + ".conv", x, w, demodulate=False, s=s)
     out = out + p[prefix + ".bias"].to(x.dtype)
     if skip is not None:
         up = make_kernel(BLUR_1D, x.dtype) * 4.0
@@ -114,3 +115,55 @@ def synthesis(p, latent, size):
         skip = to_rgb(p, f"to_rgbs.{k}", out, latent[:, i + 2], skip)
         i += 2
     return skip
+
+
+def mapping(p, z, n_mlp=8, lr_mul=0.01):
+    """rosinality Generator.style: PixelNorm then n_mlp × EqualLinear(512, 512, lr_mul,
+    activation='fused_lrelu'): x ← lrelu(x·(W·lr_mul/√512)ᵀ + b·lr_mul, 0.2)·√2."""
+    x = z * torch.rsqrt(torch.mean(z * z, dim=1, keepdim=True) + 1e-8)
+    for i in range(1, n_mlp + 1):
+        w = p[f"style.{i}.weight"].to(z.dtype) * (lr_mul / math.sqrt(z.shape[1]))
+        b = p[f"style.{i}.bias"].to(z.dtype) * lr_mul
+        x = F.leaky_relu(x @ w.t() + b, 0.2) * math.sqrt(2)
+    return x
+
+
+def truncate(w, mean, psi):
+    """Generator.forward truncation: mean + psi·(w − mean)."""
+    return mean + psi * (w - mean)
+
+
+def style_vectors(p, latent, size):
+    """Per-layer modulation styles s for a W+ latent, in generator forward order (conv1, to_rgb1,
+    then per resolution: up-conv, conv, to_rgb) — the 'style vector' of SFGenerator
+    (style_fusion_simple.py:126-142, return_style_vector=True)."""
+    log_size = int(math.log2(size))
+    out = [style_affine(p, "conv1.conv", latent[:, 0]), style_affine(p, "to_rgb1.conv", latent[:, 1])]
+    i = 1
+    for k in range(log_size - 2):
+        out.append(style_affine(p, f"convs.{2 * k}.conv", latent[:, i]))
+        out.append(style_affine(p, f"convs.{2 * k + 1}.conv", latent[:, i + 1]))
+        out.append(style_affine(p, f"to_rgbs.{k}.conv", latent[:, i + 2]))
+        i += 2
+    return out
+
+
+def synthesis_from_styles(p, styles, size):
+    """SFGenerator(style_vector=s) (style_fusion_simple.py:146-153): the synthesis driven by given
+    per-layer styles (order of style_vectors)."""
+    n = styles[0].shape[0]
+    dt = styles[0].dtype
+    log_size = int(math.log2(size))
+    noises = [p[f"noises.noise_{i}"].to(dt) for i in range((log_size - 2) * 2 + 1)]
+    out = p["input.input"].to(dt).repeat(n, 1, 1, 1)
+    out = styled_conv(p, "conv1", out, None, noises[0], s=styles[0])
+    skip = to_rgb(p, "to_rgb1", out, None, s=styles[1])
+    j = 2
+    for k in range(log_size - 2):
+        out = styled_conv(p, f"convs.{2 * k}", out, None, noises[2 * k + 1], upsample=True,
+                          s=styles[j])
+        out = styled_conv(p, f"convs.{2 * k + 1}", out, None, noises[2 * k + 2], s=styles[j + 1])
+        skip = to_rgb(p, f"to_rgbs.{k}", out, None, skip, s=styles[j + 2])
+        j += 3
+    return skip
+

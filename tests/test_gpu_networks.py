@@ -233,3 +233,73 @@ def test_attack_api_fgsm_and_pgd(cuda):
     assert ((d - 16 / 255).abs() < 1e-6).float().mean() > 0.9  # FGSM moves (almost) every pixel by e
     with pytest.raises(ValueError):
         attack(net, x0 * 3, 8 / 255, 2, target=t)
+
+
+def test_mapping_network_vs_oracle(cuda):
+    gp = make_generator_weights(32, seed=7)
+    dec = networks.Decoder(gp, 32, device=cuda)
+    z = seeded(3, (4, 512)) * 2
+    w = dec.mapping(z).cpu().double()
+    ref = stylegan2_ref.mapping({k: v.double() for k, v in gp.items()}, z.double())
+    assert rel_err(w, ref) < 1e-5
+    mean = dec.mapping.mean_latent(256, seed=1).cpu().double()
+    g = torch.Generator().manual_seed(1)
+    zz = torch.randn(256, 512, generator=g).double()
+    ref_mean = stylegan2_ref.mapping({k: v.double() for k, v in gp.items()}, zz).mean(0, keepdim=True)
+    assert rel_err(mean, ref_mean) < 1e-5
+
+
+def test_style_fusion_simple_api(cuda):
+    """StyleFusionSimple mirror (style_fusion_simple.py:25-177) on the church config (256²,
+    14 layers, truncation 0.5): z → W+ → s → image against the oracle, the W/W+/s latent types,
+    swaps, and the arithmetic fusion of interpolation.py:658-669."""
+    from gfa_amd import StyleFusionSimple, interpolation
+    drawer = StyleFusionSimple("church", None, None, cuda, n_mean_latent=512)
+    assert (drawer.stylegan_size, drawer.stylegan_layers, drawer.truncation) == (256, 14, 0.5)
+    gp64 = {k: v.double() for k, v in make_generator_weights(256, seed=0).items()}
+    z = drawer.seed_to_z((5, 2))
+    assert tuple(z.shape) == (1, 512)
+    img, feats = drawer.generate_img(z, latents_type="z")
+    assert tuple(img.shape) == (1, 3, 256, 256) and len(feats) == 13
+    mean = drawer.mean_latent.cpu().double()
+    w = stylegan2_ref.truncate(stylegan2_ref.mapping(gp64, z.cpu().double()), mean, 0.5)
+    ref = stylegan2_ref.synthesis(gp64, w.unsqueeze(1).repeat(1, 14, 1), 256)
+    assert rel_err(img, ref) < 1e-4
+    # s path: the oracle synthesis driven by style vectors equals the W+ path
+    wp = drawer.z_to_w_plus(z)
+    s = drawer.general_latent_to_s(wp, "w+")
+    assert len(s) == 2 + 3 * 6
+    img_s, _ = drawer.s_to_image(s)
+    ref_s = stylegan2_ref.synthesis_from_styles(gp64, [t.cpu().double() for t in s], 256)
+    assert rel_err(img_s, ref_s) < 1e-4 and rel_err(img_s, ref) < 1e-4
+    img_w, _ = drawer.generate_img(wp[:, 0], latents_type="w")
+    assert rel_err(img_w, ref) < 1e-4
+    img_all, _ = drawer.generate_img(z, latents_type="z", all=drawer.seed_to_z((6, 0)))
+    assert not torch.equal(img_all, img)
+    with pytest.raises(NotImplementedError):
+        drawer.generate_img(z, latents_type="z", hair=z)
+    with pytest.raises(AssertionError):
+        drawer.general_latent_to_s(torch.zeros(2, 512, device=cuda), "z")
+    W = torch.cat([drawer.z_to_w_plus(drawer.seed_to_z((i, 0)))[:, 0] for i in range(3)])
+    fused, each, fe = interpolation(drawer, W)
+    assert tuple(fused.shape) == (1, 3, 256, 256) and tuple(each.shape) == (3, 3, 256, 256)
+    ref_f = stylegan2_ref.synthesis(gp64, W.cpu().double().mean(0, keepdim=True).unsqueeze(1)
+                                    .repeat(1, 14, 1), 256)
+    assert rel_err(fused, ref_f) < 1e-4
+    assert fe.shape[0] == 3
+
+
+def test_cfg1_fusion_pair_fgsm(cuda):
+    """BASELINE config #1 plumbing: a 256² pair from the fusion entry point, FGSM ε = 8/255 on one
+    image toward the other through the attack engine, then the arithmetic fusion of the attacked
+    image's latent with its partner's."""
+    from gfa_amd import StyleFusionSimple, fgsm
+    drawer = StyleFusionSimple("church", None, None, cuda, n_mean_latent=256)
+    pair = torch.cat([drawer.generate_img(drawer.seed_to_z((s, 0)), "z")[0] for s in (1, 2)])
+    pair = pair.clamp(-1, 1)
+    net = networks.build_net(256, seed=0, dtype=torch.float16, device=cuda)
+    adv = fgsm(net, pair[:1], 8 / 255, target=pair[1:])
+    d = (adv - pair[:1]).abs()
+    assert d.max().item() <= 16 / 255 + 1e-6 and ((d - 16 / 255).abs() < 1e-6).float().mean() > 0.5
+    lat = networks.get_latents(net, adv)
+    assert tuple(lat.shape) == (1, 14, 512)

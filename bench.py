@@ -29,6 +29,7 @@ from gfa_amd.vgg import VGGNet  # noqa: E402
 from gfa_amd.weights import (make_encoder_weights, make_generator_weights,  # noqa: E402
                              make_vgg_weights)
 
+METRIC = "attacked images/sec, PGD-20 L∞ ε=8/255 at 256², 1/2/4/8 MI355X"  # BASELINE.json
 DT = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
 DT_NAME = {"fp32": "f32", "fp16": "f16", "bf16": "bf16"}
 # MI355X_MICROARCH.md chip table: dense MFMA peaks (TFLOP/s)
@@ -153,12 +154,14 @@ def main():
     value = n_total * args.steps / elapsed
     flops_img_step = pgd.algorithmic_flops_per_image_step(eng.G, eng.V)
     out = {
-        "metric": "attacked images/sec, PGD-20 L∞ ε=8/255 at 256², 1/2/4/8 MI355X",
+        "metric": METRIC if (S, args.pgd_steps) == (256, 20) else
+                  f"attacked images/sec, PGD-{args.pgd_steps} L∞ ε=8/255 at {S}², "
+                  f"{world} MI355X (non-headline config)",
         "value": value, "unit": "attacked images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": DT_NAME[args.dtype],
-        "data": "synthetic: seeded U(-1,1) image/target pairs, seeded random-init StyleGAN2 "
-                "(256², cm=2), VGG16 trunk and linear encoder (no checkpoints offline)",
+        "data": f"synthetic: seeded U(-1,1) image/target pairs, seeded random-init StyleGAN2 "
+                f"({S}², cm=2), VGG16 trunk and linear encoder (no checkpoints offline)",
         "config": {"workload": f"PGD-{args.pgd_steps} L∞ eps=8/255 alpha=2/255 at {S}², "
                                f"{B} images/GPU (BASELINE config #4 per-GPU share), "
                                f"RCCL all-gather of outputs when N>1",

@@ -104,7 +104,7 @@ def _engine(size, dtype, N, cuda, seed=0):
     return eng, x0, t, oracle
 
 
-@pytest.mark.parametrize("size,N", [(32, 2), (256, 1)])
+@pytest.mark.parametrize("size,N", [(32, 2), (256, 1), (1024, 1)])
 def test_attack_gradient_vs_oracle(cuda, size, N):
     """∇_x L from the kernel pipeline vs autograd through the fp64 oracle."""
     eng, x0, t, (gp, vp, ep) = _engine(size, torch.float32, N, cuda)

@@ -149,7 +149,8 @@ struct Tile {
 // Stages the fp32 accumulator tile in LDS (EROWS rows per pass), then works on 8-channel vectors:
 // sdot reduction, out_scale, noise, bias, tap-MSE term, ReLU mask, act_out, accumulate, store.
 // rowm(local_row) gives the GEMM row (output pixel index m) of a tile row, or −1 past the end;
-// `single` = every row of the tile belongs to image n_single.
+// `single` = every row of the tile belongs to image n_single. Waves with index ≥ TL::NW (a
+// block's DMA-only waves) take part in the barriers only.
 template <typename T, typename TL, typename RowM>
 __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G,
                                               f32x4 (&acc)[TL::FM][TL::FN], char* smem, int n0,
@@ -160,6 +161,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / WN, wn = wid % WN;
+  const bool worker = wid < NW;
   const int frow = lane & 15, fq = lane >> 4;
   const int HWo = G.ho * G.wo;
   float* tile = (float*)smem;
@@ -188,7 +190,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
 
   for (int h = 0; h < BM / EROWS; ++h) {
     const int wrow0 = wm * FM * 16;
-    if (wrow0 >= h * EROWS && wrow0 < (h + 1) * EROWS) {
+    if (worker && wrow0 >= h * EROWS && wrow0 < (h + 1) * EROWS) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -202,7 +204,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
       const int rr = r0 + it * RPP;
-      const int row = rowm(h * EROWS + rr);
+      const int row = worker ? rowm(h * EROWS + rr) : -1;
       if (row >= 0 && col_ok) {
         float v[8];
         load8f(tile + rr * ES + cc * 8, v);
@@ -246,16 +248,16 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += bias8[e];
           }
+          float ma[8];
           if (TA) {
-            float ta[8], tt[8];
-            load8<T>(TA + aoff, ta);
+            float tt[8];
+            load8<T>(TA + aoff, ma);  // the tap tensor doubles as the mask when they coincide
             load8<T>(TT + aoff, tt);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] += p.tap_coef * (ta[e] - tt[e]);
+            for (int e = 0; e < 8; ++e) v[e] += p.tap_coef * (ma[e] - tt[e]);
           }
           if (MA) {
-            float ma[8];
-            load8<T>(MA + aoff, ma);
+            if (MA != TA) load8<T>(MA + aoff, ma);
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = ma[e] > 0.f ? v[e] : 0.f;
           }
@@ -281,7 +283,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
     for (int e = 0; e < 8; ++e)
       for (int o = CPR; o < 64; o <<= 1) part[e] += __shfl_xor(part[e], o, 64);
     float* red = (float*)smem;  // [NW waves][BN]
-    if (lane < CPR) {
+    if (worker && lane < CPR) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) red[wid * BN + lane * 8 + e] = part[e];
     }

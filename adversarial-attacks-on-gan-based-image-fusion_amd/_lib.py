@@ -28,6 +28,8 @@ class ConvArgs(ctypes.Structure):
         ("aux_x", P), ("act_aux", c_int), ("sdot", P),
         ("tap_a", P), ("tap_t", P), ("tap_coef", c_float), ("mask_a", P),
         ("accumulate", c_int),
+        ("bab_demod", P), ("bab_noise", P), ("bab_noise_w", c_float), ("bab_bias", P),
+        ("bab_q", P),
     ]
 
 
@@ -64,6 +66,8 @@ SIGNATURES = {
     "mia_upconv_blur_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     "mia_upconv_dgrad": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, c_int,
                                  P]),
+    "mia_upconv_dgrad_fused": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P, P, c_int, P, P,
+                                       c_float, P, P, c_int, P]),
     "mia_bias_act_fwd": (c_int, [P, P, c_float, P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_bias_act_bwd": (c_int, [P, P, P, c_float, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
                                  c_int, c_int, P]),

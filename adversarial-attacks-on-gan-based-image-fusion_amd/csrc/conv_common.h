@@ -176,9 +176,19 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
   const T* TT = (const T*)p.tap_t;
   const T* MA = (const T*)p.mask_a;
   T* __restrict__ Y = (T*)p.y;
-  float part[8];
+  float part[8], partq[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) part[e] = 0.f;
+  for (int e = 0; e < 8; ++e) part[e] = partq[e] = 0.f;
+  const bool bab = p.bab_demod != nullptr;
+  float bbias8[8];
+  if (bab) {
+    if (p.bab_bias && col_ok) {
+      load8f(p.bab_bias + col, bbias8);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bbias8[e] = 0.f;
+    }
+  }
 
   // per-column epilogue constants, loaded once (single-image tiles: out_scale too)
   float bias8[8], osc8[8];
@@ -210,9 +220,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
         load8f(tile + rr * ES + cc * 8, v);
         const size_t aoff = (size_t)row * Cout + col;
         const int n = single ? n_single : row / HWo;
+        float xv[8];
+        if (p.sdot || bab) load8<T>(AX + aoff, xv);
         if (p.sdot) {
-          float xv[8];
-          load8<T>(AX + aoff, xv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             const float c = v[e] * apply_act(xv[e], p.act_aux);
@@ -269,6 +279,21 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] += yo8[e];
           }
+          if (bab) {
+            // fused StyledConv backward front of the layer whose activation is aux_x
+            float dm8[8];
+            load8f(p.bab_demod + (size_t)n * Cout + col, dm8);
+            const float nz = p.bab_noise ? p.bab_noise_w * p.bab_noise[yo * k.WT + xo] : 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float gr = lrelu_s2_grad(xv[e]);
+              const float gp = v[e] * gr;
+              const float c = gp * (xv[e] / gr - nz - bbias8[e]);
+              if (single) partq[e] += c;
+              else atomicAdd(&p.bab_q[(size_t)n * Cout + col + e], c);
+              v[e] = gp * dm8[e];
+            }
+          }
           store8<T>(Y + off, v);
         }
       }
@@ -276,6 +301,25 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
     __syncthreads();
   }
 
+  if (bab && single) {
+    // q partials: the same shuffle + LDS reduction as sdot below (before it reuses the LDS)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      for (int o = CPR; o < 64; o <<= 1) partq[e] += __shfl_xor(partq[e], o, 64);
+    float* red = (float*)smem;
+    if (worker && lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[wid * BN + lane * 8 + e] = partq[e];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < Cout) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s += red[w * BN + tid];
+      atomicAdd(&p.bab_q[(size_t)n_single * Cout + n0 + tid], s);
+    }
+    __syncthreads();
+  }
   if (p.sdot && single) {
     // reduce the per-thread partial sums of equal channel chunks: lanes cc, cc+CPR, … of a wave
     // by shuffles, then the waves through LDS, one atomic per channel per block

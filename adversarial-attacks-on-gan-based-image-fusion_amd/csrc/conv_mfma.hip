@@ -310,6 +310,9 @@ static int run_conv(ConvK& k, int dtype, hipStream_t st) {
   MIA_CHECK_ARG(a.Cout % 8 == 0, "Cout must be a multiple of 8");
   MIA_CHECK_ARG(!a.shuffle_out || (a.Cout % 32 == 0 && k.ng == 1), "shuffle_out: Cout % 32, 1 group");
   MIA_CHECK_ARG(!a.sdot || a.aux_x, "sdot needs aux_x");
+  MIA_CHECK_ARG(!a.bab_demod || (a.aux_x && a.act_aux == MIA_ACT_NONE && a.bab_q && a.y &&
+                                 !a.shuffle_out),
+                "bab_demod needs aux_x (stored activations, act_aux NONE), bab_q and y");
   MIA_CHECK_ARG(!a.tap_a || a.tap_t, "tap_a needs tap_t");
   MIA_CHECK_ARG(!a.shuffle_out || !(a.tap_a || a.mask_a || a.sdot),
                 "aux inputs need un-shuffled output");
@@ -323,7 +326,8 @@ static int run_conv(ConvK& k, int dtype, hipStream_t st) {
     MIA_CHECK_ARG(G.kpad == kpad_for(G.kh * G.kw * a.Cin, dtype), "Kpad must be mia_conv_kpad()");
     MIA_CHECK_ARG(G.ho > 0 && G.wo > 0, "empty output grid");
     MIA_CHECK_ARG((int64_t)a.N * G.ho * G.wo < (1LL << 31), "too many pixels");
-    MIA_CHECK_ARG(!(a.sdot || a.tap_a || a.mask_a) || (k.ng == 1 && G.ho * G.wo == k.HT * k.WT),
+    MIA_CHECK_ARG(!(a.sdot || a.tap_a || a.mask_a || a.bab_demod) ||
+                      (k.ng == 1 && G.ho * G.wo == k.HT * k.WT),
                   "aux operands need one group with an identity output placement");
   }
   int lc = 0;
@@ -406,12 +410,35 @@ extern "C" int mia_upconv_fwd(const void* x, const void* const* w_phase, void* t
   return run_conv(k, dtype, (hipStream_t)stream);
 }
 
+static int upconv_dgrad_impl(const mia_conv_args& a, const void* w_t, int N, int R, int Cout,
+                             int Cin, int dtype, void* stream);
+
 extern "C" int mia_upconv_dgrad(const void* g_t, const void* w_t, void* gx, int N, int R, int Cout,
                                 int Cin, const void* x_fwd, int act_x, const float* style,
                                 float* sdot, int dtype, void* stream) {
   mia_conv_args a = {};
   a.x = g_t; a.y = gx; a.N = N; a.H = 2 * R + 1; a.W = 2 * R + 1; a.Cin = Cout; a.Cout = Cin;
   a.out_scale = style; a.aux_x = x_fwd; a.act_aux = act_x; a.sdot = sdot;
+  return upconv_dgrad_impl(a, w_t, N, R, Cout, Cin, dtype, stream);
+}
+
+extern "C" int mia_upconv_dgrad_fused(const void* g_t, const void* w_t, void* gx, int N, int R,
+                                      int Cout, int Cin, const void* x_fwd, const float* style,
+                                      float* sdot, int accumulate, const float* bab_demod,
+                                      const float* bab_noise, float bab_noise_w,
+                                      const float* bab_bias, float* bab_q, int dtype,
+                                      void* stream) {
+  mia_conv_args a = {};
+  a.x = g_t; a.y = gx; a.N = N; a.H = 2 * R + 1; a.W = 2 * R + 1; a.Cin = Cout; a.Cout = Cin;
+  a.out_scale = style; a.aux_x = x_fwd; a.act_aux = MIA_ACT_NONE; a.sdot = sdot;
+  a.accumulate = accumulate;
+  a.bab_demod = bab_demod; a.bab_noise = bab_noise; a.bab_noise_w = bab_noise_w;
+  a.bab_bias = bab_bias; a.bab_q = bab_q;
+  return upconv_dgrad_impl(a, w_t, N, R, Cout, Cin, dtype, stream);
+}
+
+static int upconv_dgrad_impl(const mia_conv_args& a, const void* w_t, int N, int R, int Cout,
+                             int Cin, int dtype, void* stream) {
   ConvK k = {};
   k.a = a;
   k.stride = 2;

@@ -65,8 +65,10 @@ PROFILE = None
 def conv3x3(x, w, y, *, cout, act_in=ACT_NONE, in_scale=None, out_scale=None, bias=None,
             noise=None, noise_w=0.0, act_out=ACT_NONE, shuffle_out=False, aux_x=None,
             act_aux=ACT_NONE, sdot=None, tap_a=None, tap_t=None, tap_coef=0.0, mask_a=None,
-            accumulate=False, y_cstride=0, flops=None):
+            accumulate=False, y_cstride=0, bab=None, flops=None):
     """Generic MFMA implicit-GEMM conv (mia_conv3x3). x: (N,H,W,Cin); w: (Cout,Kpad).
+    ``bab``: dict(demod, noise, noise_w, bias, q) — fused StyledConv backward front of the layer
+    whose stored activation is aux_x (mia_conv_args.bab_*).
     ``flops``: algorithmic FLOPs of this launch for profiling (default 2·N·H·W·9·Cin·Cout)."""
     N, H, W, Cin = x.shape
     T = x.dtype
@@ -91,6 +93,13 @@ def conv3x3(x, w, y, *, cout, act_in=ACT_NONE, in_scale=None, out_scale=None, bi
         if a is not None:
             _need(a, (N, H, W, cout), T, name)
     _numel_ok(sdot, N * cout, f32, "sdot")
+    if bab is not None:
+        _numel_ok(bab["demod"], N * cout, f32, "bab.demod")
+        _numel_ok(bab["q"], N * cout, f32, "bab.q")
+        _numel_ok(bab.get("noise"), H * W, f32, "bab.noise")
+        _numel_ok(bab.get("bias"), cout, f32, "bab.bias")
+        if aux_x is None:
+            raise ValueError("bab needs aux_x (the stored activation)")
     a = ConvArgs()
     a.x, a.w, a.y = ptr(x), ptr(w), ptr(y)
     a.N, a.H, a.W, a.Cin, a.Cout, a.Kpad = N, H, W, Cin, cout, kpad
@@ -103,6 +112,10 @@ def conv3x3(x, w, y, *, cout, act_in=ACT_NONE, in_scale=None, out_scale=None, bi
     a.aux_x, a.act_aux, a.sdot = ptr(aux_x), act_aux, ptr(sdot)
     a.tap_a, a.tap_t, a.tap_coef, a.mask_a = ptr(tap_a), ptr(tap_t), float(tap_coef), ptr(mask_a)
     a.accumulate = int(bool(accumulate))
+    if bab is not None:
+        a.bab_demod, a.bab_q = ptr(bab["demod"]), ptr(bab["q"])
+        a.bab_noise, a.bab_noise_w = ptr(bab.get("noise")), float(bab.get("noise_w", 0.0))
+        a.bab_bias = ptr(bab.get("bias"))
     prof = PROFILE
     if prof is not None:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -185,6 +198,31 @@ def upconv_dgrad(g_t, w_t, gx, cin, x_fwd, act_x, style, sdot, flops=None):
     _prof_call("mia_upconv_dgrad", flops if flops is not None else 2 * N * R * R * 9 * Cout * cin,
                ptr(g_t), ptr(w_t), ptr(gx), N, R, Cout, cin, ptr(x_fwd), act_x, ptr(style),
                ptr(sdot), dt(T), stream())
+    return gx
+
+
+def upconv_dgrad_fused(g_t, w_t, gx, cin, x_fwd, style, sdot, bab, accumulate, flops=None):
+    """upconv_dgrad with the fused backward front of the layer below (mia_upconv_dgrad_fused):
+    gx ← demod-scaled pre-activation gradient of that layer; bab = dict(demod, noise, noise_w,
+    bias, q)."""
+    N, TS, _, Cout = g_t.shape
+    R = (TS - 1) // 2
+    T = g_t.dtype
+    _need(w_t, (cin, conv_kpad(Cout, T)), T, "w_t")
+    _need(gx, (N, R, R, cin), T, "gx")
+    _need(x_fwd, (N, R, R, cin), T, "x_fwd")
+    _numel_ok(style, N * cin, torch.float32, "style")
+    _numel_ok(sdot, N * cin, torch.float32, "sdot")
+    _numel_ok(bab["demod"], N * cin, torch.float32, "bab.demod")
+    _numel_ok(bab["q"], N * cin, torch.float32, "bab.q")
+    _numel_ok(bab.get("noise"), R * R, torch.float32, "bab.noise")
+    _numel_ok(bab.get("bias"), cin, torch.float32, "bab.bias")
+    _prof_call("mia_upconv_dgrad_fused",
+               flops if flops is not None else 2 * N * R * R * 9 * Cout * cin,
+               ptr(g_t), ptr(w_t), ptr(gx), N, R, Cout, cin, ptr(x_fwd), ptr(style), ptr(sdot),
+               int(bool(accumulate)), ptr(bab["demod"]), ptr(bab.get("noise")),
+               float(bab.get("noise_w", 0.0)), ptr(bab.get("bias")), ptr(bab["q"]), dt(T),
+               stream())
     return gx
 
 

@@ -202,9 +202,83 @@ class SynthesisNet:
     # --------------------------------------------------------------------------------------
     def backward(self, g_img, g_lat, ws):
         """g_img = ∂L/∂image (N,3,S,S) fp32; accumulates ∂L/∂w+ into g_lat (N,n_latent,512)."""
+        if self.up_mode == "subpixel":
+            self._backward_fused(g_img, ws)
+        else:
+            self._backward_unfused(g_img, ws)
+        self._style_backward(g_lat, ws)
+        return g_lat
+
+    def _torgb_step(self, i, ti, g_rgb, ws):
+        """ToRGB backward for the (non-up) conv i: writes its activation gradient into "g.ga{i}"
+        (not accumulated) and its style gradient; returns the skip-path gradient (or None)."""
+        N = g_rgb.shape[0]
+        L, t = self.convs[i], self.torgbs[ti]
+        r = L["res"]
+        gs_t = ops.zero_(ws.get(f"g.gs_rgb{ti}", (N, t["cin"]), torch.float32))
+        ga = ws.get(f"g.ga{i}", (N, r, r, L["cout"]), self.dtype)
+        ops.torgb_bwd(g_rgb, L["_pre"], t["_s"], t["wr"], ga, gs_t, accumulate=False,
+                      act_in=ACT_NONE)
+        t["_gs"] = gs_t
+        if t["_skip"] is None:
+            return None
+        g_skip = ws.get(f"g.gskip{ti}", (N, 3, r // 2, r // 2), torch.float32)
+        ops.upfirdn2d_bwd(g_rgb, g_skip, UP_K, up=2, pad=(2, 1))
+        return g_skip
+
+    def _backward_fused(self, g_img, ws):
+        """Top-down; each conv's dgrad epilogue also runs the backward front of the conv below it
+        (ToRGB gradient accumulated, lrelu', demod scale and the q = Σ_p g_pre·o reduction:
+        mia_conv_args.bab_*), so only the topmost conv needs a separate mia_bias_act_bwd."""
         N = g_img.shape[0]
         T = self.dtype
-        nl = self.n_latent
+        last = len(self.convs) - 1
+        ti = len(self.torgbs) - 1
+        g_rgb = self._torgb_step(last, ti, g_img, ws)
+        ti -= 1
+        Lt = self.convs[last]
+        q = ops.zero_(ws.get(f"g.q{last}", (N, Lt["cout"]), torch.float32))
+        ga = ws.get(f"g.ga{last}", (N, Lt["res"], Lt["res"], Lt["cout"]), T)
+        gy = ws.get(f"g.gy{last}", ga.shape, T)
+        ops.bias_act_bwd(ga, Lt["_pre"], Lt["noise"], Lt["noise_w"], Lt["bias"], Lt["_d"], gy, q,
+                         from_act=True)
+        for i in range(last, -1, -1):
+            L = self.convs[i]
+            r, cout, cin = L["res"], L["cout"], L["cin"]
+            gs = ops.zero_(ws.get(f"g.gs{i}", (N, cin), torch.float32))
+            rin = r // 2 if L["up"] else r
+            out, bab, acc, q_below = None, None, False, None
+            if i > 0:
+                Lb = self.convs[i - 1]
+                if not Lb["up"]:
+                    g_rgb = self._torgb_step(i - 1, ti, g_rgb, ws)  # writes g.ga{i-1}
+                    ti -= 1
+                    acc = True
+                out = ws.get(f"g.ga{i - 1}", (N, rin, rin, cin), T)
+                q_below = ops.zero_(ws.get(f"g.q{i - 1}", (N, cin), torch.float32))
+                bab = dict(demod=Lb["_d"], noise=Lb["noise"], noise_w=Lb["noise_w"],
+                           bias=Lb["bias"], q=q_below)
+            if L["up"]:
+                gt = ws.get(f"g.gt{i}", (N, r + 1, r + 1, cout), T)
+                ops.upconv_blur_bwd(gy, gt)
+                if bab is not None:
+                    ops.upconv_dgrad_fused(gt, L["wd"], out, cin, L["_x"], L["_s"], gs, bab, acc,
+                                           flops=self._alg_flops(L, N))
+                else:
+                    ops.upconv_dgrad(gt, L["wd"], None, cin, L["_x"], ACT_NONE, L["_s"], gs,
+                                     flops=self._alg_flops(L, N))
+            else:
+                ops.conv3x3(gy, L["wd"], out, cout=cin, out_scale=L["_s"], aux_x=L["_x"],
+                            act_aux=ACT_NONE, sdot=gs, accumulate=acc, bab=bab,
+                            flops=self._alg_flops(L, N))
+            ops.demod_bwd(q, L["_d"], L["wsq"], L["_s"], gs)
+            L["_gs"] = gs
+            gy, q = out, q_below
+
+    def _backward_unfused(self, g_img, ws):
+        """Reference order (fused-phase up-convs): ToRGB → bias_act_bwd → dgrad per conv."""
+        N = g_img.shape[0]
+        T = self.dtype
         g_rgb = g_img
         ti = len(self.torgbs) - 1
         g_a_next = None  # ∂L/∂act of the current conv's output, written by the conv above
@@ -230,35 +304,27 @@ class SynthesisNet:
                     ops.upfirdn2d_bwd(g_rgb, g_skip, UP_K, up=2, pad=(2, 1))
                     g_rgb = g_skip
                 ti -= 1
-            # StyledConv backward front: g_pre, q, gy
             q = ws.get(f"g.q{i}", (N, cout), torch.float32)
             ops.zero_(q)
-            sub = L["up"] and self.up_mode == "subpixel"
-            if L["up"] and not sub:
+            if L["up"]:
                 gy = ws.get(f"g.gy{i}", (N, r // 2, r // 2, 4 * cout), T)
             else:
                 gy = ws.get(f"g.gy{i}", (N, r, r, cout), T)
             ops.bias_act_bwd(g_a_next, pre, L["noise"], L["noise_w"], L["bias"], L["_d"], gy, q,
-                             unshuffle=L["up"] and not sub, from_act=True)
-            # dgrad + style sdot
+                             unshuffle=L["up"], from_act=True)
             gs = ws.get(f"g.gs{i}", (N, cin), torch.float32)
             ops.zero_(gs)
             rin = r // 2 if L["up"] else r
-            if i > 0:
-                gx = ws.get(f"g.ga{i - 1}", (N, rin, rin, cin), T)
-            else:
-                gx = None
-            if sub:
-                gt = ws.get(f"g.gt{i}", (N, r + 1, r + 1, cout), T)
-                ops.upconv_blur_bwd(gy, gt)
-                ops.upconv_dgrad(gt, L["wd"], gx, cin, L["_x"], ACT_NONE, L["_s"], gs,
-                                 flops=self._alg_flops(L, N))
-            else:
-                ops.conv3x3(gy, L["wd"], gx, cout=cin, out_scale=L["_s"], aux_x=L["_x"],
-                            act_aux=ACT_NONE, sdot=gs, flops=self._alg_flops(L, N))
+            gx = ws.get(f"g.ga{i - 1}", (N, rin, rin, cin), T) if i > 0 else None
+            ops.conv3x3(gy, L["wd"], gx, cout=cin, out_scale=L["_s"], aux_x=L["_x"],
+                        act_aux=ACT_NONE, sdot=gs, flops=self._alg_flops(L, N))
             ops.demod_bwd(q, L["_d"], L["wsq"], L["_s"], gs)
             L["_gs"] = gs
             g_a_next = gx
+
+    def _style_backward(self, g_lat, ws):
+        N = g_lat.shape[0]
+        nl = self.n_latent
         # style affine backward: ∂w+[:, j] += Σ_{layers reading latent j} ∂s · (A/√512); one
         # grouped launch, one group per latent row (≤ 2 layers share a row: ToRGB_i and the next
         # up-conv), so no two blocks write the same output.

@@ -55,6 +55,10 @@ int mia_conv_kpad(int cin, int dtype);
  *   v = acc * out_scale[n][co % cout_mod]
  *   v += noise_w * noise[pixel_out] ; v += bias[co % cout_mod]
  *   v += tap_coef * (tap_a - tap_t) ; v *= (mask_a > 0) ; v = act_out(v) ; v += y (accumulate)
+ *   [fused StyledConv backward front, when bab_demod: with a = aux_x (the stored activation
+ *    lrelu(pre)·√2 of the layer below, act_aux = NONE), g = v·lrelu'(a), pre = a / lrelu'(a):
+ *    bab_q[n][co] += g·(pre − bab_noise_w·bab_noise[pixel] − bab_bias[co]); v = g·bab_demod[n][co]
+ *    — what mia_bias_act_bwd(from_act=1) would compute from this output]
  *   y[...] = v           (pixel-shuffled to (2H, 2W, Cout/4) when shuffle_out)
  */
 typedef struct mia_conv_args {
@@ -79,6 +83,11 @@ typedef struct mia_conv_args {
   float tap_coef;
   const void* mask_a;     /* [N][H][W][Cout] */
   int accumulate;
+  const float* bab_demod; /* [N][Cout] or NULL: fused backward front of the layer below */
+  const float* bab_noise; /* [H*W] or NULL */
+  float bab_noise_w;
+  const float* bab_bias;  /* [Cout] or NULL */
+  float* bab_q;           /* [N][Cout] fp32, accumulated with atomics */
 } mia_conv_args;
 
 int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream);
@@ -128,6 +137,14 @@ int mia_upconv_blur_bwd(const void* gy, void* gt, int N, int R, int C, int dtype
 int mia_upconv_dgrad(const void* g_t, const void* w_t, void* gx, int N, int R, int Cout, int Cin,
                      const void* x_fwd, int act_x, const float* style, float* sdot, int dtype,
                      void* stream);
+/* The same with the fused backward front of the layer below (see mia_conv_args: gx += (torgb
+ * part, accumulate), then bab_* on x_fwd = that layer's stored activation) — gx receives that
+ * layer's demod-scaled pre-activation gradient directly. */
+int mia_upconv_dgrad_fused(const void* g_t, const void* w_t, void* gx, int N, int R, int Cout,
+                           int Cin, const void* x_fwd, const float* style, float* sdot,
+                           int accumulate, const float* bab_demod, const float* bab_noise,
+                           float bab_noise_w, const float* bab_bias, float* bab_q, int dtype,
+                           void* stream);
 
 /* ---- elementwise / reduction kernels ----------------------------------------------------- */
 /* FusedLeakyReLU + NoiseInjection forward, standalone (K4): y = lrelu(x + nw·noise + b)·√2 (NHWC). */

@@ -514,3 +514,59 @@ def test_conv_large_m_tiles(cuda, dtype, kind, tile, monkeypatch):
     assert rel_err(nchw(y), ref) < tol
     if kind == "dgrad_sdot":
         assert rel_err(sd, sdot_ref) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("N,H,Cin,Cout,up", [(2, 16, 128, 128, False), (2, 8, 64, 128, False),
+                                             (3, 12, 64, 64, False), (2, 8, 128, 64, True)])
+def test_fused_backward_front_epilogue(cuda, dtype, N, H, Cin, Cout, up):
+    """dgrad (3×3 stride 1, or the stride-2 up-conv adjoint) with the fused StyledConv backward
+    front of the layer below (bab_*) equals dgrad → (+ ToRGB part) → mia_bias_act_bwd."""
+    g = torch.Generator().manual_seed(N + H + Cin + Cout + int(up))
+    # layer below: stored activation a (N,H,H,Cout_b = Cin of the dgrad output... naming: the
+    # dgrad maps Cin channels (layer above's outputs) to Cout channels (layer below's outputs)
+    R = H
+    if up:
+        gt = torch.randn(N, Cin, 2 * R + 1, 2 * R + 1, generator=g)
+        w = torch.randn(Cin, Cout, 3, 3, generator=g) / math.sqrt(9 * Cin)  # W[co_up][ci_up]
+        wd = layouts.upconv_dgrad_matrix(w, dtype).to(cuda)
+        xin = nhwc(gt, dtype).to(cuda)
+    else:
+        gy = torch.randn(N, Cin, R, R, generator=g)
+        w = torch.randn(Cin, Cout, 3, 3, generator=g) / math.sqrt(9 * Cout)
+        wd = layouts.dgrad_matrix(w, dtype).to(cuda)
+        xin = nhwc(gy, dtype).to(cuda)
+    a = (torch.randn(N, Cout, R, R, generator=g) * 1.5)
+    a = torch.where(a > 0, a, 0.2 * a) * math.sqrt(2)        # a valid stored activation
+    ad = nhwc(a, dtype).to(cuda)
+    s = (torch.rand(N, Cout, generator=g) + 0.5).to(cuda)
+    demod = (torch.rand(N, Cout, generator=g) + 0.5).to(cuda)
+    nz = torch.randn(R * R, generator=g).to(cuda)
+    bz = (0.1 * torch.randn(Cout, generator=g)).to(cuda)
+    trgb = nhwc(torch.randn(N, Cout, R, R, generator=g), dtype).to(cuda)  # ToRGB gradient part
+    # reference path: dgrad → + ToRGB part → bias_act_bwd
+    g_a = torch.empty(N, R, R, Cout, dtype=dtype, device=cuda)
+    sd1 = torch.zeros(N, Cout, device=cuda)
+    if up:
+        ops.upconv_dgrad(xin, wd, g_a, Cout, ad, ops.ACT_NONE, s, sd1)
+    else:
+        ops.conv3x3(xin, wd, g_a, cout=Cout, out_scale=s, aux_x=ad, sdot=sd1)
+    g_a = (g_a.float() + trgb.float()).to(dtype)
+    gy1 = torch.empty_like(g_a)
+    q1 = torch.zeros(N, Cout, device=cuda)
+    ops.bias_act_bwd(g_a, ad, nz, 0.3, bz, demod, gy1, q1, from_act=True)
+    # fused
+    gy2 = trgb.clone()
+    sd2 = torch.zeros(N, Cout, device=cuda)
+    q2 = torch.zeros(N, Cout, device=cuda)
+    bab = dict(demod=demod, noise=nz, noise_w=0.3, bias=bz, q=q2)
+    if up:
+        ops.upconv_dgrad_fused(xin, wd, gy2, Cout, ad, s, sd2, bab, accumulate=True)
+    else:
+        ops.conv3x3(xin, wd, gy2, cout=Cout, out_scale=s, aux_x=ad, sdot=sd2, accumulate=True,
+                    bab=bab)
+    torch.cuda.synchronize()
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert rel_err(gy2, gy1) < tol
+    assert rel_err(q2, q1) < (1e-4 if dtype == torch.float32 else 3e-2)
+    assert rel_err(sd2, sd1) < 1e-4

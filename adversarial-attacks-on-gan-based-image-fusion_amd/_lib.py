@@ -78,6 +78,8 @@ SIGNATURES = {
     "mia_torgb_fwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_torgb_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                               P]),
+    "mia_torgb_bwd_front": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P, P, c_float,
+                                    P, P, c_int, P]),
     "mia_maxpool2_fwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_maxpool2_bwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_float, c_int,
                                  c_int, P]),

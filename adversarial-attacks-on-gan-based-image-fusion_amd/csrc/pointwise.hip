@@ -390,14 +390,25 @@ __global__ void torgb_fwd_kernel(const T* __restrict__ pre, const float* __restr
   }
 }
 
-template <typename T>
+// FRONT: the ToRGB feeds the topmost StyledConv, whose activation gradient is this ToRGB's alone;
+// then also run that conv's backward front (as mia_bias_act_bwd(from_act) would): g_a is written
+// as gy = g·lrelu'(a)·demod and q[n][c] += g·lrelu'(a)·(pre − nw·noise − b).
+struct TorgbFront {
+  const float* demod;
+  const float* noise;
+  float nw;
+  const float* bias;
+  float* q;
+};
+
+template <typename T, bool FRONT>
 __global__ void torgb_bwd_kernel(const float* __restrict__ grgb, const T* __restrict__ pre,
                                  const float* __restrict__ s, const float* __restrict__ wr,
                                  T* __restrict__ g_a, float* __restrict__ gs, int H, int W, int Cin,
-                                 int accumulate, int pix_per_block, int act_in) {
+                                 int accumulate, int pix_per_block, int act_in, TorgbFront fr) {
   typedef typename Vec<T>::type VT;
   constexpr int V = Vec<T>::N;
-  extern __shared__ float sh[];  // wr [3][Cin], s [Cin], partials [TPB/tpp][Cin]
+  extern __shared__ float sh[];  // wr [3][Cin], s [Cin], partials [TPB/tpp][Cin] (× 2 if FRONT)
   const int n = blockIdx.y;
   float* w3 = sh;
   float* sn = sh + 3 * Cin;
@@ -412,9 +423,16 @@ __global__ void torgb_bwd_kernel(const float* __restrict__ grgb, const T* __rest
   const int t = threadIdx.x;
   const int chunk = t % tpp, sub = t / tpp;
   const int c0 = chunk * V;
-  float acc[V];
+  float acc[V], qa[V], dm[V], bs[V];
 #pragma unroll
-  for (int e = 0; e < V; ++e) acc[e] = 0.f;
+  for (int e = 0; e < V; ++e) acc[e] = qa[e] = 0.f;
+  if (FRONT) {
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      dm[e] = fr.demod[(size_t)n * Cin + c0 + e];
+      bs[e] = fr.bias ? fr.bias[c0 + e] : 0.f;
+    }
+  }
   const int p_begin = blockIdx.x * pix_per_block;
   const int p_end = min(p_begin + pix_per_block, HW);
   if (sub < ppp) {
@@ -426,26 +444,42 @@ __global__ void torgb_bwd_kernel(const float* __restrict__ grgb, const T* __rest
       const VT pr = *(const VT*)(pre + off);
       VT ga;
       if (accumulate) ga = *(const VT*)(g_a + off);
+      const float nz = (FRONT && fr.noise) ? fr.nw * fr.noise[p] : 0.f;
 #pragma unroll
       for (int e = 0; e < V; ++e) {
         const int c = c0 + e;
         const float u = g0 * w3[c] + g1 * w3[Cin + c] + g2 * w3[2 * Cin + c];
         acc[e] += (act_in ? lrelu_s2(to_f(pr[e])) : to_f(pr[e])) * u;
-        const float gv = sn[c] * u + (accumulate ? to_f(ga[e]) : 0.f);
+        float gv = sn[c] * u + (accumulate ? to_f(ga[e]) : 0.f);
+        if (FRONT) {  // stored activation a = pr (act_in NONE)
+          const float a = to_f(pr[e]);
+          const float gr = lrelu_s2_grad(a);
+          const float gp = gv * gr;
+          qa[e] += gp * (a / gr - nz - bs[e]);
+          gv = gp * dm[e];
+        }
         ga[e] = from_f<T>(gv);
       }
       *(VT*)(g_a + off) = ga;
     }
   }
+  float* partq = part + ppp * Cin;
   if (sub < ppp) {
 #pragma unroll
-    for (int e = 0; e < V; ++e) part[sub * Cin + c0 + e] = acc[e];
+    for (int e = 0; e < V; ++e) {
+      part[sub * Cin + c0 + e] = acc[e];
+      if (FRONT) partq[sub * Cin + c0 + e] = qa[e];
+    }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < Cin; c += TPB) {
-    float sum = 0.f;
-    for (int sb = 0; sb < ppp; ++sb) sum += part[sb * Cin + c];
+    float sum = 0.f, sq = 0.f;
+    for (int sb = 0; sb < ppp; ++sb) {
+      sum += part[sb * Cin + c];
+      if (FRONT) sq += partq[sb * Cin + c];
+    }
     atomicAdd(&gs[(size_t)n * Cin + c], sum);
+    if (FRONT) atomicAdd(&fr.q[(size_t)n * Cin + c], sq);
   }
 }
 
@@ -982,9 +1016,29 @@ extern "C" int mia_torgb_bwd(const float* g_rgb, const void* pre, const float* s
   dim3 grid((H * W + ppb - 1) / ppb, N);
   const size_t sh = (4 * Cin + (size_t)ppp * Cin) * sizeof(float);
   MIA_CHECK_ARG(sh <= 64 * 1024, "LDS budget");
+  const TorgbFront fr{};
   MIA_DISPATCH_DTYPE(dtype, T,
-      MIA_LAUNCH(torgb_bwd_kernel<T>, grid, dim3(TPB), sh, g_rgb, (const T*)pre, style, wr, (T*)g_a,
-                 gs, H, W, Cin, accumulate, ppb, act_in));
+      MIA_LAUNCH((torgb_bwd_kernel<T, false>), grid, dim3(TPB), sh, g_rgb, (const T*)pre, style,
+                 wr, (T*)g_a, gs, H, W, Cin, accumulate, ppb, act_in, fr));
+  return MIA_OK;
+}
+
+extern "C" int mia_torgb_bwd_front(const float* g_rgb, const void* act, const float* style,
+                                   const float* wr, void* gy, float* gs, int N, int H, int W,
+                                   int Cin, const float* demod, const float* noise, float noise_w,
+                                   const float* bias, float* q, int dtype, void* stream) {
+  MIA_CHECK_ARG(g_rgb && act && style && wr && gy && gs && demod && q, "bad args");
+  const int V = dtype == MIA_F32 ? 4 : 8;
+  MIA_CHECK_ARG(Cin % V == 0 && Cin / V <= TPB && TPB % (Cin / V) == 0, "Cin/V must divide 256");
+  const int ppp = TPB / (Cin / V);
+  const int ppb = ppp * 16;
+  dim3 grid((H * W + ppb - 1) / ppb, N);
+  const size_t sh = (4 * Cin + 2 * (size_t)ppp * Cin) * sizeof(float);
+  MIA_CHECK_ARG(sh <= 64 * 1024, "LDS budget");
+  const TorgbFront fr{demod, noise, noise_w, bias, q};
+  MIA_DISPATCH_DTYPE(dtype, T,
+      MIA_LAUNCH((torgb_bwd_kernel<T, true>), grid, dim3(TPB), sh, g_rgb, (const T*)act, style,
+                 wr, (T*)gy, gs, H, W, Cin, 0, ppb, MIA_ACT_NONE, fr));
   return MIA_OK;
 }
 

@@ -305,6 +305,23 @@ def torgb_bwd(g_rgb, pre, style, wr, g_a, gs, accumulate, act_in=ACT_LRELU_S2):
          Cin, int(bool(accumulate)), int(act_in), dt(pre), stream())
 
 
+def torgb_bwd_front(g_rgb, act, style, wr, gy, gs, demod, noise, noise_w, bias, q):
+    """ToRGB backward + the topmost StyledConv's backward front (mia_torgb_bwd_front)."""
+    N, H, W, Cin = act.shape
+    _need(g_rgb, (N, 3, H, W), torch.float32, "g_rgb")
+    _need(gy, act.shape, act.dtype, "gy")
+    _numel_ok(style, N * Cin, torch.float32, "style")
+    _numel_ok(wr, 3 * Cin, torch.float32, "wr")
+    _numel_ok(gs, N * Cin, torch.float32, "gs")
+    _numel_ok(demod, N * Cin, torch.float32, "demod")
+    _numel_ok(q, N * Cin, torch.float32, "q")
+    _numel_ok(noise, H * W, torch.float32, "noise")
+    _numel_ok(bias, Cin, torch.float32, "bias")
+    call("mia_torgb_bwd_front", ptr(g_rgb), ptr(act), ptr(style), ptr(wr), ptr(gy), ptr(gs), N,
+         H, W, Cin, ptr(demod), ptr(noise), float(noise_w), ptr(bias), ptr(q), dt(act), stream())
+    return gy
+
+
 def pool_out(H, ceil_mode):
     return (H + 1) // 2 if ceil_mode else H // 2
 

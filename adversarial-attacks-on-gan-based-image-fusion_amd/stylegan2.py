@@ -209,16 +209,22 @@ class SynthesisNet:
         self._style_backward(g_lat, ws)
         return g_lat
 
-    def _torgb_step(self, i, ti, g_rgb, ws):
+    def _torgb_step(self, i, ti, g_rgb, ws, front=None):
         """ToRGB backward for the (non-up) conv i: writes its activation gradient into "g.ga{i}"
-        (not accumulated) and its style gradient; returns the skip-path gradient (or None)."""
+        (not accumulated) and its style gradient; returns the skip-path gradient (or None).
+        ``front=(gy, q)`` (topmost conv only): also run conv i's backward front into gy / q."""
         N = g_rgb.shape[0]
         L, t = self.convs[i], self.torgbs[ti]
         r = L["res"]
         gs_t = ops.zero_(ws.get(f"g.gs_rgb{ti}", (N, t["cin"]), torch.float32))
-        ga = ws.get(f"g.ga{i}", (N, r, r, L["cout"]), self.dtype)
-        ops.torgb_bwd(g_rgb, L["_pre"], t["_s"], t["wr"], ga, gs_t, accumulate=False,
-                      act_in=ACT_NONE)
+        if front is not None:
+            gy, q = front
+            ops.torgb_bwd_front(g_rgb, L["_pre"], t["_s"], t["wr"], gy, gs_t, L["_d"], L["noise"],
+                                L["noise_w"], L["bias"], q)
+        else:
+            ga = ws.get(f"g.ga{i}", (N, r, r, L["cout"]), self.dtype)
+            ops.torgb_bwd(g_rgb, L["_pre"], t["_s"], t["wr"], ga, gs_t, accumulate=False,
+                          act_in=ACT_NONE)
         t["_gs"] = gs_t
         if t["_skip"] is None:
             return None
@@ -229,19 +235,17 @@ class SynthesisNet:
     def _backward_fused(self, g_img, ws):
         """Top-down; each conv's dgrad epilogue also runs the backward front of the conv below it
         (ToRGB gradient accumulated, lrelu', demod scale and the q = Σ_p g_pre·o reduction:
-        mia_conv_args.bab_*), so only the topmost conv needs a separate mia_bias_act_bwd."""
+        mia_conv_args.bab_*); the topmost conv's front is fused into its ToRGB backward
+        (mia_torgb_bwd_front)."""
         N = g_img.shape[0]
         T = self.dtype
         last = len(self.convs) - 1
         ti = len(self.torgbs) - 1
-        g_rgb = self._torgb_step(last, ti, g_img, ws)
-        ti -= 1
         Lt = self.convs[last]
         q = ops.zero_(ws.get(f"g.q{last}", (N, Lt["cout"]), torch.float32))
-        ga = ws.get(f"g.ga{last}", (N, Lt["res"], Lt["res"], Lt["cout"]), T)
-        gy = ws.get(f"g.gy{last}", ga.shape, T)
-        ops.bias_act_bwd(ga, Lt["_pre"], Lt["noise"], Lt["noise_w"], Lt["bias"], Lt["_d"], gy, q,
-                         from_act=True)
+        gy = ws.get(f"g.gy{last}", (N, Lt["res"], Lt["res"], Lt["cout"]), T)
+        g_rgb = self._torgb_step(last, ti, g_img, ws, front=(gy, q))
+        ti -= 1
         for i in range(last, -1, -1):
             L = self.convs[i]
             r, cout, cin = L["res"], L["cout"], L["cin"]

@@ -173,6 +173,14 @@ int mia_torgb_fwd(const void* pre, const float* style, const float* wr, const fl
 int mia_torgb_bwd(const float* g_rgb, const void* pre, const float* style, const float* wr,
                   void* g_a, float* gs, int N, int H, int W, int Cin, int accumulate, int act_in,
                   int dtype, void* stream);
+/* ToRGB backward for the topmost StyledConv (its activation gradient is this ToRGB's alone),
+ * fused with that conv's backward front (mia_bias_act_bwd, from_act=1): gy = demod·g·lrelu'(a),
+ * q += Σ_p g·lrelu'(a)·(pre − noise_w·noise − bias); gs as mia_torgb_bwd. act: stored
+ * activation (N,H,W,Cin). */
+int mia_torgb_bwd_front(const float* g_rgb, const void* act, const float* style, const float* wr,
+                        void* gy, float* gs, int N, int H, int W, int Cin, const float* demod,
+                        const float* noise, float noise_w, const float* bias, float* q, int dtype,
+                        void* stream);
 /* MaxPool 2x2/2 (K8) NHWC, ceil_mode for odd sizes (code/vgg.py:14,18,24). */
 int mia_maxpool2_fwd(const void* x, void* y, int N, int H, int W, int C, int ceil_mode,
                      int dtype, void* stream);

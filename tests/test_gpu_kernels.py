@@ -320,6 +320,37 @@ def test_torgb_fwd_bwd(cuda, dtype, cin, stored):
     assert rel_err(gs, gsr) < tol
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("cin,R", [(32, 16), (64, 9), (128, 8)])
+def test_torgb_bwd_front(cuda, dtype, cin, R):
+    """mia_torgb_bwd_front == mia_torgb_bwd then mia_bias_act_bwd(from_act) (the topmost conv)."""
+    g = torch.Generator().manual_seed(cin + R)
+    N = 3
+    a = F.leaky_relu(torch.randn(N, R, R, cin, generator=g), 0.2) * math.sqrt(2)
+    ad = a.to(dtype).to(cuda)
+    sd = torch.randn(N, cin, generator=g).to(cuda)
+    wr = (torch.randn(3, cin, generator=g) / math.sqrt(cin)).to(cuda)
+    grgb = torch.randn(N, 3, R, R, generator=g).to(cuda)
+    demod = (torch.rand(N, cin, generator=g) + 0.5).to(cuda)
+    nz = torch.randn(R * R, generator=g).to(cuda)
+    bz = torch.randn(cin, generator=g).to(cuda)
+    ga = torch.empty(N, R, R, cin, dtype=dtype, device=cuda)
+    gs1 = torch.zeros(N, cin, device=cuda)
+    ops.torgb_bwd(grgb, ad, sd, wr, ga, gs1, accumulate=False, act_in=ops.ACT_NONE)
+    gy1 = torch.empty_like(ga)
+    q1 = torch.zeros(N, cin, device=cuda)
+    ops.bias_act_bwd(ga, ad, nz, 0.3, bz, demod, gy1, q1, from_act=True)
+    gy2 = torch.empty_like(ga)
+    gs2 = torch.zeros(N, cin, device=cuda)
+    q2 = torch.zeros(N, cin, device=cuda)
+    ops.torgb_bwd_front(grgb, ad, sd, wr, gy2, gs2, demod, nz, 0.3, bz, q2)
+    torch.cuda.synchronize()
+    tol = 1e-5 if dtype == torch.float32 else 2e-2  # reference path rounds g_a to dtype
+    assert rel_err(gs2, gs1) < 1e-5
+    assert rel_err(gy2, gy1) < tol
+    assert rel_err(q2, q1) < tol
+
+
 def test_sign_project_bit_exact(cuda):
     """K11 vs the oracle's torch fp32 formula, including g == 0 and the clamp edges."""
     g = torch.Generator().manual_seed(0)

@@ -26,7 +26,8 @@ namespace mia {
 // Tile: a PH × 16 output patch (PH = 16: 8 waves, 1 block per CU; PH = 8: 4 waves, 2 blocks per
 // CU so that one block's prologue/epilogue overlaps the other's main loop) × BN output channels.
 // Each wave owns FM = 4 patch rows (one 16-pixel MFMA fragment per row) × BN/2 channels.
-template <int BN_, int PH_, int STAGES_>
+// NHBUF = 1: a single halo buffer, for Cin = one channel block only (no next-block prefetch).
+template <int BN_, int PH_, int STAGES_, int NHBUF_ = 2>
 struct HaloTile {
   static constexpr int PH = PH_, PW = 16, NW = PH / 2, NT = 64 * NW, BM = PH * PW, BN = BN_;
   static constexpr int WM = PH / 4, WN = 2, FM = 4, FN = BN_ / 32;
@@ -35,7 +36,7 @@ struct HaloTile {
   static constexpr int NHBUF = 1;  // tuning experiment: one halo buffer (wrong results)
 #else
   static constexpr int STAGES = STAGES_;
-  static constexpr int NHBUF = 2;
+  static constexpr int NHBUF = NHBUF_;
 #endif
   static constexpr int HW = PW + 2, HROWS = (PH + 2) * HW;  // 324 / 180 halo pixels
   static constexpr int HPIECES = (HROWS + 7) / 8;          // DMA pieces of 8 rows (1 KB)
@@ -237,7 +238,7 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 ? 2 : 1) void conv_halo_kernel(
         // H-waves issue between the two MFMA halves: the texture-address unit takes ≈16 cycles
         // per 1-KB LDS-DMA instruction; here the queue overlaps the partner B-wave's MFMAs.
         __builtin_amdgcn_sched_barrier(0);
-        if (cb + 1 < ncb) {  // next block's halo, HPS pieces per step from tap 0
+        if (TL::NHBUF > 1 && cb + 1 < ncb) {  // next block's halo, HPS pieces per step from tap 0
 #pragma unroll
           for (int q = 0; q < HPS; ++q) {
             const int j = t * HPS + q;
@@ -297,6 +298,8 @@ static int launch_halo_tile(ConvK& k, hipStream_t st) {
   lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
   lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
   if (lds > 160 * 1024) return set_error("conv_halo: LDS budget exceeded");
+  if (TL::NHBUF == 1 && k.a.Cin != ROWB / (int)sizeof(T))
+    return set_error("conv_halo: single-buffer tile needs Cin = one channel block");
   auto fn = conv_halo_kernel<T, TL, PRO>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -310,19 +313,22 @@ static int launch_halo_tile(ConvK& k, hipStream_t st) {
 }
 
 // Eligible: one group, stride 1, 3×3 taps with pad 1, identity output placement, no pixel
-// shuffle, 16-divisible spatial dims, whole channel blocks, > 64 output channels (at Cout = 64 the
-// generic 128×64 tile measured faster: the halo tile's fixed costs are paid for half the MFMAs).
+// shuffle, 16-divisible spatial dims, whole channel blocks, and Cout > 64 or Cout ≤ 32 (at Cout = 64
+// the generic 128×64 tile measured faster: the halo tile's fixed costs are paid for half the
+// MFMAs; at Cout ≤ 32 — the VGG input gradient, 8 channels — the generic tile computes 64 columns
+// and gathers every input row 9 times, the 32-column halo tile is memory-bound on one halo pass).
 bool conv_halo_eligible(const ConvK& k, int dtype) {
   const char* e = getenv("MIA_CONV_HALO");  // tuning / A-B switch: 0 disables the halo path
   if (e && atoi(e) == 0) return false;
   const char* e64 = getenv("MIA_HALO_N64");  // tuning: 1 = halo path for Cout = 64 too
-  const int min_cout = (e64 && atoi(e64) == 1) ? 64 : 65;
+  const bool n64 = e64 && atoi(e64) == 1;
   const mia_conv_args& a = k.a;
   const ConvGroup& G = k.g[0];
   const int bk = dtype == MIA_F32 ? 32 : 64;
   return k.ng == 1 && k.stride == 1 && G.kh == 3 && G.kw == 3 && G.pad_y == 1 && G.pad_x == 1 &&
          G.ho == a.H && G.wo == a.W && G.ay == 1 && G.ax == 1 && G.by == 0 && G.bx == 0 &&
-         !a.shuffle_out && a.H % 16 == 0 && a.W % 16 == 0 && a.Cin % bk == 0 && a.Cout >= min_cout &&
+         !a.shuffle_out && a.H % 16 == 0 && a.W % 16 == 0 && a.Cin % bk == 0 &&
+         (a.Cout > 64 || a.Cout <= 32 || (n64 && a.Cout == 64)) &&
          k.HT == a.H && k.WT == a.W;
 }
 
@@ -336,7 +342,18 @@ int launch_conv_halo(ConvK& k, int dtype, hipStream_t st) {
   typedef HaloTile<128, 16, 4> Big;
   typedef HaloTile<128, 8, 2> Small;
   typedef HaloTile<64, 8, 3> Small64;
+  // Cout ≤ 32 (VGG input gradient): little MFMA work per K-step, so the weights of all nine taps
+  // of a one-block Cin are DMA'd in the prologue (9 stages, 36 KB) and no step waits on L2.
+  typedef HaloTile<32, 8, 2> Small32;
+  typedef HaloTile<32, 8, 9, 1> Small32x9;
   MIA_DISPATCH_DTYPE(dtype, T, {
+    if (k.a.Cout <= 32) {
+      if (k.a.Cin == ROWB / (int)sizeof(T))
+        return pro ? launch_halo_tile<T, Small32x9, true>(k, st)
+                   : launch_halo_tile<T, Small32x9, false>(k, st);
+      return pro ? launch_halo_tile<T, Small32, true>(k, st)
+                 : launch_halo_tile<T, Small32, false>(k, st);
+    }
     if (k.a.Cout <= 64)
       return pro ? launch_halo_tile<T, Small64, true>(k, st)
                  : launch_halo_tile<T, Small64, false>(k, st);

@@ -47,7 +47,8 @@ def test_conv3x3_bias_relu(cuda, dtype, N, H, Cin, Cout):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 16, 16, 64, 64), (1, 32, 48, 128, 192),
-                                            (2, 16, 32, 256, 128), (1, 48, 16, 64, 128)])
+                                            (2, 16, 32, 256, 128), (1, 48, 16, 64, 128),
+                                            (2, 32, 16, 64, 8), (1, 16, 16, 128, 24)])
 @pytest.mark.parametrize("mode", ["bias_relu", "modconv", "dgrad_sdot", "tap_mask"])
 @pytest.mark.parametrize("halo", ["1", "0"])
 def test_conv3x3_halo_and_generic_paths(cuda, monkeypatch, dtype, N, H, W, Cin, Cout, mode, halo):

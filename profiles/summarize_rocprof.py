@@ -16,7 +16,10 @@ import json
 import re
 from collections import defaultdict
 
-CONV = re.compile(r"conv_kernel")
+CONV = re.compile(r"conv_(halo_)?kernel")
+# names of the bool template parameters of the elementwise kernels (csrc/pointwise.hip)
+KFLAGS = {"blur4_strip_kernel": ("fwd", "noise"), "torgb_bwd_kernel": ("front",),
+          "maxpool2_bwd_kernel": ("tap",)}
 
 
 def short(name):
@@ -33,8 +36,12 @@ def short(name):
         elif tile:
             wm, wn, fm, fn, st = map(int, tile.groups())
             extra = f"<{wm * fm * 16}x{wn * fn * 16},{st}st,pro={flags[0]},smallc={flags[1]}>"
-        elif "Lb1" in name or "Lb0" in name:
-            extra = "<fwd>" if "Lb1" in name else "<bwd>"
+        elif flags:
+            names = KFLAGS.get(base)
+            if names:
+                extra = "<" + ",".join(f"{k}={v}" for k, v in zip(names, flags)) + ">"
+            else:
+                extra = "<" + ",".join(flags) + ">"
         return base + extra
     return name.split("(")[0]
 

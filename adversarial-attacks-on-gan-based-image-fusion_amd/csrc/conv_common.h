@@ -20,6 +20,8 @@ struct ConvGroup {
 struct ConvK {
   mia_conv_args a;  // x, y, N, H/W = INPUT dims, Cin, Cout and the epilogue fields
   int stride, HT, WT, ystride, cout_mod, log2cin, n_first_max, ng, nblk, nbn;
+  int stagger_blocks;            // halo kernel: blocks of the first dispatch wave …
+  unsigned stagger_cycles;       // … of which every other one starts this many clocks late
   ConvGroup g[4];
 };
 
@@ -125,6 +127,33 @@ __device__ __forceinline__ void load8f(const float* p, float (&v)[8]) {
   const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
 #pragma unroll
   for (int e = 0; e < 4; ++e) { v[e] = a[e]; v[e + 4] = b[e]; }
+}
+
+// 4 consecutive elements of T as fp32 (8-byte or 16-byte access)
+template <typename T>
+__device__ __forceinline__ void load4(const T* p, float (&v)[4]) {
+  if constexpr (sizeof(T) == 2) {
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    const t4 t = *(const t4*)p;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = (float)t[e];
+  } else {
+    const f32x4 a = *(const f32x4*)p;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = a[e];
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store4(T* p, const float (&v)[4]) {
+  if constexpr (sizeof(T) == 2) {
+    typedef T t4 __attribute__((ext_vector_type(4)));
+    t4 t;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) t[e] = (T)v[e];
+    *(t4*)p = t;
+  } else {
+    *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+  }
 }
 
 constexpr int ROWB = 128;  // bytes per tile row (one K-step slice)

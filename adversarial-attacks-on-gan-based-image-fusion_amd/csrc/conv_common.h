@@ -370,8 +370,38 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
   }
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform n ≤ 16 (the immediate must be a constant)
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
+    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
+    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+  }
+}
+
 // halo-tiled stride-1 3×3 path (conv_halo.hip)
 bool conv_halo_eligible(const ConvK& k, int dtype);
 int launch_conv_halo(ConvK& k, int dtype, hipStream_t st);
+// up-sampling StyledConv forward, halo-tiled interior (conv_upconv.hip)
+bool upconv_halo_eligible(int dtype, int R, int Cin, int Cout);
+int launch_upconv_halo(const void* x, const void* w_up, void* t, int N, int R, int Cin, int Cout,
+                       int act_in, const float* style, int dtype, hipStream_t st);
+// thin-channel layers: VGG conv1_1 forward and its input gradient (conv_thin.hip)
+bool conv_thin_eligible(const ConvK& k, int dtype);
+int launch_conv_thin(ConvK& k, int dtype, hipStream_t st);
 
 }  // namespace mia

@@ -59,29 +59,6 @@ struct HaloTile {
   static_assert(WM * FM * 16 == BM && WN * FN * 16 == BN, "");
 };
 
-// s_waitcnt vmcnt(n) for a wave-uniform n ≤ 16 (the immediate must be a constant)
-__device__ __forceinline__ void wait_vmcnt(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-  }
-}
-
 #ifdef MIA_HALO_TIMING
 // phase cycle sums of wave 0 over all blocks (tuning builds only: scratch/, never shipped)
 // one row per 4096th block: the atomics of one launch spread over 4096 addresses (a single row
@@ -316,11 +293,21 @@ __device__ __forceinline__ void halo_epilogue_f(const ConvK& k, const f32x4 (&ac
       }
     }
   }
-  float nz[FM], bnz[FM];
-  R4 rx[FM][FN], rta[FM][FN], rtt[FM][FN], rma[FM][FN], ryo[FM][FN];
+  float part[FN][4], partq[FN][4];
 #pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int y = y0 + wm * FM + i, x = x0 + px;
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) part[j][e] = partq[j][e] = 0.f;
+  // rows in chunks of FMC (the aux loads of a chunk are hoisted together; chunks bound the live
+  // registers for tall wave tiles)
+  constexpr int FMC = FM < 4 ? FM : 4;
+#pragma unroll
+  for (int i0 = 0; i0 < FM; i0 += FMC) {
+  float nz[FMC], bnz[FMC];
+  R4 rx[FMC][FN], rta[FMC][FN], rtt[FMC][FN], rma[FMC][FN], ryo[FMC][FN];
+#pragma unroll
+  for (int i = 0; i < FMC; ++i) {
+    const int y = y0 + wm * FM + i0 + i, x = x0 + px;
     const int m = (n * H + y) * W + x;
     nz[i] = bnz[i] = 0.f;
     if constexpr (NOISE) nz[i] = p.noise_w * p.noise[y * W + x];
@@ -344,21 +331,16 @@ __device__ __forceinline__ void halo_epilogue_f(const ConvK& k, const f32x4 (&ac
     }
   }
 
-  float part[FN][4], partq[FN][4];
 #pragma unroll
-  for (int j = 0; j < FN; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) part[j][e] = partq[j][e] = 0.f;
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int m = (n * H + y0 + wm * FM + i) * W + x0 + px;
+  for (int i = 0; i < FMC; ++i) {
+    const int m = (n * H + y0 + wm * FM + i0 + i) * W + x0 + px;
     float vo[FN][4];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) vo[j][e] = 0.f;
       if (!cok[j]) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      float v[4] = {acc[i0 + i][j][0], acc[i0 + i][j][1], acc[i0 + i][j][2], acc[i0 + i][j][3]};
       float xv[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) xv[e] = (SDOT || BAB) ? (float)rx[i][j][e] : 0.f;
@@ -414,6 +396,7 @@ __device__ __forceinline__ void halo_epilogue_f(const ConvK& k, const f32x4 (&ac
       }
     }
   }
+  }  // row chunks
   if constexpr (SDOT || BAB) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {

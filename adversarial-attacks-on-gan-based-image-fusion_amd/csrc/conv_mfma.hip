@@ -337,6 +337,7 @@ static int run_conv(ConvK& k, int dtype, hipStream_t st) {
   for (int g = 0; g < k.ng; ++g) hw_min = std::min(hw_min, k.g[g].ho * k.g[g].wo);
   k.n_first_max = std::min(a.N, (256 + hw_min - 1) / hw_min + 1);
 
+  if (conv_thin_eligible(k, dtype)) return launch_conv_thin(k, dtype, st);
   if (conv_halo_eligible(k, dtype)) return launch_conv_halo(k, dtype, st);
   MIA_DISPATCH_DTYPE(dtype, T, return launch_conv<T>(k, st));
   return MIA_OK;
@@ -405,6 +406,55 @@ extern "C" int mia_upconv_fwd(const void* x, const void* const* w_phase, void* t
     G.ay = G.ax = 2;
     G.by = py;
     G.bx = px;
+    G.m = N * G.ho * G.wo;
+  }
+  return run_conv(k, dtype, (hipStream_t)stream);
+}
+
+extern "C" int mia_upconv_fwd_halo(const void* x, const void* const* w_phase, const void* w_up,
+                                   void* t_out, int N, int R, int Cin, int Cout, int act_in,
+                                   const float* style, int dtype, void* stream) {
+  if (!w_up || !upconv_halo_eligible(dtype, R, Cin, Cout))
+    return mia_upconv_fwd(x, w_phase, t_out, N, R, Cin, Cout, act_in, style, dtype, stream);
+  MIA_CHECK_ARG(x && w_phase && t_out && N > 0 && Cout % 8 == 0, "bad args");
+  MIA_CHECK_ARG((int64_t)N * R * R * Cin < (1LL << 31), "input too large for 32-bit offsets");
+  const int rc = launch_upconv_halo(x, w_up, t_out, N, R, Cin, Cout, act_in, style, dtype,
+                                    (hipStream_t)stream);
+  if (rc) return rc;
+  // the last row / column of the even phase grids (y = R or x = R): four one-row / one-column
+  // groups on the generic kernel; the group's input window starts at R − 1 (pad = 1 − R) and its
+  // outputs land at T row / column 2R
+  mia_conv_args a = {};
+  a.x = x; a.y = t_out; a.N = N; a.H = R; a.W = R; a.Cin = Cin; a.Cout = Cout;
+  a.act_in = act_in; a.in_scale = style;
+  ConvK k = {};
+  k.a = a;
+  k.stride = 1;
+  k.ng = 4;
+  k.HT = k.WT = 2 * R + 1;
+  k.cout_mod = Cout;
+  k.ystride = Cout;
+  // {phase, row group?}: (0,0) row y = R (x ∈ [0,R]), (0,1) row y = R (x ∈ [0,R)),
+  //                      (0,0) column x = R (y ∈ [0,R)), (1,0) column x = R (y ∈ [0,R))
+  const int phs[4] = {0, 1, 0, 2};
+  const bool rowg[4] = {true, true, false, false};
+  for (int g = 0; g < 4; ++g) {
+    const int ph = phs[g], py = ph >> 1, px = ph & 1;
+    ConvGroup& G = k.g[g];
+    G.w = w_phase[ph];
+    G.kh = 2 - py;
+    G.kw = 2 - px;
+    G.kpad = kpad_for(G.kh * G.kw * Cin, dtype);
+    G.ay = G.ax = 2;
+    if (rowg[g]) {
+      G.ho = 1; G.wo = R + 1 - px;
+      G.pad_y = (G.kh - 1) - R; G.pad_x = G.kw - 1;
+      G.by = 2 * R + py; G.bx = px;
+    } else {
+      G.ho = R; G.wo = 1;
+      G.pad_y = G.kh - 1; G.pad_x = (G.kw - 1) - R;
+      G.by = py; G.bx = 2 * R + px;
+    }
     G.m = N * G.ho * G.wo;
   }
   return run_conv(k, dtype, (hipStream_t)stream);

@@ -1,0 +1,248 @@
+// Thin-channel 3×3 convolutions (stride 1, pad 1, NHWC, 2-byte types): the VGG input layer
+// conv1_1 (code/vgg.py:45, 3 → 64 channels; the image is padded to 8 channels) and its input
+// gradient (64 → 8 channels, 3 real). Both move far more bytes than they compute (forward: 16 B
+// read and 128 B written per pixel for 27·64 MACs; gradient: 128 B read and 16 B written), so they
+// are HBM/TA-bound, not MFMA-bound. The implicit-GEMM tiles (conv_mfma.hip, conv_halo.hip) pad K
+// or N to a 128-B operand row and re-stage the whole weight tensor per tile, which made these two
+// launches run at ≈1 TB/s. Here:
+//   * the weights live in VGPRs for the whole kernel (each wave loads them once);
+//   * a wave computes 16 consecutive pixels of one image row per step with MFMA 16×16×32,
+//     D[channel][pixel]; the pixel operand is gathered straight from global memory into VGPRs
+//     (one 16-B vector per lane per K-chunk, the neighbours' re-reads hit L1/L2), so there is no
+//     LDS traffic and no barrier;
+//   * forward stores: pairs of channel fragments are exchanged between lane rows
+//     (v_permlane16_swap) so every lane writes 8 consecutive channels with one 16-B store;
+//   * the gradient kernel stages each input pixel once per wave work item in LDS (9 taps read it);
+//   * waves stride over the pixel groups / work items.
+#include "conv_common.h"
+
+namespace mia {
+
+template <typename T>
+__device__ __forceinline__ typename Vec<T>::type ld16_or_zero(const T* p, bool ok) {
+  typedef typename Vec<T>::type VT;
+  VT v;
+  if (ok) {
+    v = *(const VT*)p;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (T)0.f;
+  }
+  return v;
+}
+
+// ---- forward, Cin = 8 (image padded to 8 channels) → COUT channels, + bias, act ----------------
+// K = 9 taps × 8 channels = 72 in three MFMA K-chunks of 32 (chunk m, lane group fq → tap 4m+fq,
+// taps ≥ 9 are zero; the weight matrix [Cout][Kpad ≥ 96] is zero there too).
+template <typename T, int COUT>
+__global__ __launch_bounds__(256) void conv_thin_in_kernel(const T* __restrict__ x,
+                                                           const T* __restrict__ w, int kpad,
+                                                           const float* __restrict__ bias, int act,
+                                                           T* __restrict__ y, int N, int H, int W) {
+  typedef typename Vec<T>::type VT;
+  constexpr int FN = COUT / 16;
+  const int lane = threadIdx.x & 63, frow = lane & 15, fq = lane >> 4;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
+  VT wr[FN][3];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int m = 0; m < 3; ++m) wr[j][m] = *(const VT*)(w + (size_t)(16 * j + frow) * kpad + 8 * (4 * m + fq));
+  float bs[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bs[j][r] = bias ? bias[16 * j + 4 * fq + r] : 0.f;
+
+  const int gpr = W / 16, ngroups = N * H * gpr;
+  for (int g = wave; g < ngroups; g += nwaves) {
+    const int row = g / gpr, xg = (g - row * gpr) * 16;
+    const int n = row / H, yy = row - n * H;
+    const int px = xg + frow;
+    VT af[3];
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int t = 4 * m + fq;  // lane-dependent tap
+      const int dy = t / 3 - 1, dx = t - (t / 3) * 3 - 1;
+      const int sy = yy + dy, sx = px + dx;
+      const bool ok = t < 9 && sy >= 0 && sy < H && sx >= 0 && sx < W;
+      af[m] = ld16_or_zero<T>(x + ((size_t)(n * H + (ok ? sy : 0)) * W + (ok ? sx : 0)) * 8, ok);
+    }
+    f32x4 acc[FN];
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int m = 0; m < 3; ++m) acc[j] = mfma_chunk<T>(wr[j][m], af[m], acc[j]);
+    }
+    // lane (frow = pixel, fq) holds channels 16j + 4fq … +3 of its pixel
+    T* yp = y + ((size_t)row * W + px) * COUT;
+    typedef T t2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int q = 0; q < FN / 2; ++q) {
+      unsigned a[2], b[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float va[2], vb[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          va[e] = acc[2 * q][2 * h + e] + bs[2 * q][2 * h + e];
+          vb[e] = acc[2 * q + 1][2 * h + e] + bs[2 * q + 1][2 * h + e];
+          va[e] = apply_act(va[e], act);
+          vb[e] = apply_act(vb[e], act);
+        }
+        const t2 ta = {(T)va[0], (T)va[1]};
+        const t2 tb = {(T)vb[0], (T)vb[1]};
+        const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, ta),
+                                                        __builtin_bit_cast(unsigned, tb), false,
+                                                        false);
+        a[h] = r[0];
+        b[h] = r[1];
+      }
+      // after the swap lane row fq holds channels [16·(2q + (fq & 1)) + 8·(fq >> 1), +8)
+      const int c = 16 * (2 * q + (fq & 1)) + 8 * (fq >> 1);
+      *(uint4*)(yp + c) = make_uint4(a[0], a[1], b[0], b[1]);
+    }
+  }
+}
+
+// ---- input gradient, CIN = 64 channels → 8 output channels (store), no epilogue ---------------
+// Every input pixel feeds 9 taps, so the pixel operand is staged per wave in LDS: a work item is
+// RS = 2 output rows × 16 pixels; its (RS+2) × 18 input pixels (72 rows of 128 B, 9 LDS-DMA pieces
+// of 1 KB, bank-swizzled through the source chunk as in conv_halo.hip) are DMA'd once, then read
+// by the 9 taps × 2 K-chunks as MFMA B fragments. Each wave owns two such buffers and prefetches
+// its next item while computing the current one; no block barrier (a wave reads only what its own
+// DMA wrote, after its own vmcnt).
+// D[channel][pixel] with channel rows 0 … 15 (rows ≥ COUT zero weights); K = 9 taps × 64 in
+// chunks of 32: chunk s = (tap s / 2, channels 32·(s & 1) + 8·fq …).
+constexpr int THIN_RS = 2, THIN_HW = 18, THIN_ROWS = (THIN_RS + 2) * THIN_HW;  // 72
+constexpr int THIN_PIECES = (THIN_ROWS + 7) / 8;                               // 9
+constexpr int THIN_WBUF = THIN_PIECES * 1024;
+
+template <typename T, int COUT>
+__global__ __launch_bounds__(256) void conv_thin_out_kernel(const T* __restrict__ g,
+                                                            const T* __restrict__ w, int kpad,
+                                                            T* __restrict__ y, int N, int H,
+                                                            int W) {
+  typedef typename Vec<T>::type VT;
+  constexpr int CIN = 64, S = 18;
+  static_assert(COUT == 8, "");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, frow = lane & 15, fq = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  char* const wbuf = smem + wid * 2 * THIN_WBUF;
+  const int wave = blockIdx.x * 4 + wid, nwaves = gridDim.x * 4;
+  VT wr[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    wr[s] = ld16_or_zero<T>(w + (size_t)(frow < COUT ? frow : 0) * kpad + 32 * s + 8 * fq,
+                            frow < COUT);
+  const T* zero = (const T*)g_zero16;
+  const int gpr = W / 16, rpi = (H + THIN_RS - 1) / THIN_RS, nitems = N * rpi * gpr;
+
+  auto issue = [&](int it, int buf) {  // the input window of item it into buffer buf
+    const int row = it / gpr, x0 = (it - row * gpr) * 16;
+    const int n = row / rpi, y0 = (row - n * rpi) * THIN_RS;
+#pragma unroll
+    for (int q = 0; q < THIN_PIECES; ++q) {
+      const int r = q * 8 + (lane >> 3);
+      const int hy = r / THIN_HW, hx = r - (r / THIN_HW) * THIN_HW;
+      const int sy = y0 + hy - 1, sx = x0 + hx - 1;
+      const bool ok = r < THIN_ROWS && sy >= 0 && sy < H && sx >= 0 && sx < W;
+      const T* src = ok ? g + ((size_t)(n * H + sy) * W + sx) * CIN + ((lane & 7) ^ fsw(r)) * 8
+                        : zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(wbuf + buf * THIN_WBUF + q * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  int it = wave, buf = 0;
+  if (it < nitems) issue(it, 0);
+  for (; it < nitems; it += nwaves, buf ^= 1) {
+    const int nxt = it + nwaves;
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): reads of the other buffer are done
+    if (nxt < nitems) {
+      issue(nxt, buf ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(THIN_PIECES) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const char* hb = wbuf + buf * THIN_WBUF;
+    const int row = it / gpr, x0 = (it - row * gpr) * 16;
+    const int n = row / rpi, y0 = (row - n * rpi) * THIN_RS;
+#pragma unroll
+    for (int ry = 0; ry < THIN_RS; ++ry) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int r = (ry + t / 3) * THIN_HW + frow + t % 3;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const VT bf = *(const VT*)(hb + r * ROWB + (((4 * c + fq) ^ fsw(r)) << 4));
+          acc = mfma_chunk<T>(wr[2 * t + c], bf, acc);
+        }
+      }
+      // lane (frow = pixel, fq) holds output channels 4fq … 4fq+3; channels < 8 are real
+      const int yy = y0 + ry;
+      if (fq < COUT / 4 && yy < H) {
+        float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+        store4<T>(y + ((size_t)(n * H + yy) * W + x0 + frow) * COUT + 4 * fq, v);
+      }
+    }
+  }
+}
+
+static int grid_for(int64_t groups, int waves_per_cu = 32) {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+  }
+  const int64_t waves = std::min<int64_t>(groups, (int64_t)ncu * waves_per_cu);
+  return (int)std::max<int64_t>(1, (waves + 3) / 4);
+}
+
+// Eligible launches (checked by run_conv): 2-byte type, one group, stride 1, 3×3 pad 1, identity
+// output placement, W % 16 == 0, and either (Cin 8 → Cout 64, epilogue = bias/act only) or
+// (Cin 64 → Cout 8, no epilogue).
+bool conv_thin_eligible(const ConvK& k, int dtype) {
+  const char* e = getenv("MIA_CONV_THIN");  // tuning / A-B switch: 0 disables the thin kernels
+  if (e && atoi(e) == 0) return false;
+  const mia_conv_args& a = k.a;
+  const ConvGroup& G = k.g[0];
+  if (dtype == MIA_F32 || k.ng != 1 || k.stride != 1 || G.kh != 3 || G.kw != 3 || G.pad_y != 1 ||
+      G.pad_x != 1 || G.ho != a.H || G.wo != a.W || G.ay != 1 || G.ax != 1 || G.by != 0 ||
+      G.bx != 0 || a.shuffle_out || a.W % 16 != 0 || k.HT != a.H || k.WT != a.W ||
+      k.ystride != a.Cout || a.act_in != MIA_ACT_NONE || a.in_scale || a.out_scale || a.noise ||
+      a.tap_a || a.mask_a || a.sdot || a.bab_demod || a.accumulate || !a.y)
+    return false;
+  if (a.Cin == 8 && a.Cout == 64 && G.kpad >= 96) return true;
+  if (a.Cin == 64 && a.Cout == 8 && !a.bias && a.act_out == MIA_ACT_NONE) return true;
+  return false;
+}
+
+int launch_conv_thin(ConvK& k, int dtype, hipStream_t st) {
+  const mia_conv_args& a = k.a;
+  const int grid = grid_for((int64_t)a.N * a.H * (a.W / 16));  // ≤ 8 waves per SIMD
+  MIA_DISPATCH_DTYPE(dtype, T, {
+    if constexpr (sizeof(T) == 2) {
+      if (a.Cin == 8) {
+        hipLaunchKernelGGL((conv_thin_in_kernel<T, 64>), dim3(grid), dim3(256), 0, st,
+                           (const T*)a.x, (const T*)k.g[0].w, k.g[0].kpad, a.bias, a.act_out,
+                           (T*)a.y, a.N, a.H, a.W);
+      } else {
+        const int64_t items = (int64_t)a.N * ((a.H + THIN_RS - 1) / THIN_RS) * (a.W / 16);
+        const int lds = 4 * 2 * THIN_WBUF;
+        hipLaunchKernelGGL((conv_thin_out_kernel<T, 8>), dim3(grid_for(items, 16)), dim3(256),
+                           lds, st, (const T*)a.x, (const T*)k.g[0].w, k.g[0].kpad, (T*)a.y,
+                           a.N, a.H, a.W);
+      }
+      return check_launch("conv_thin");
+    }
+  });
+  return set_error("conv_thin: 2-byte types only");
+}
+
+}  // namespace mia

@@ -67,6 +67,30 @@ def upconv_subpixel_matrices(w, dtype):
     return out
 
 
+# K-steps of the halo-tiled up-conv (mia_upconv_fwd_halo): input offset (jy, jx) → (−jy, −jx) and
+# the phases p = 2·py + px of its two weight slots (None = zero slot)
+UPCONV_HALO_STEPS = (((0, 0), (0, 1)), ((0, 0), (2, 3)), ((0, 1), (0, 2)), ((1, 0), (0, 1)),
+                     ((1, 1), (0, None)))
+
+
+def upconv_halo_matrix(w, dtype):
+    """Packed weights of mia_upconv_fwd_halo: (Cin/64, 5, 2, Cout, 64), slot weight
+    W[:, ci, py + 2·jy, px + 2·jx] (T[2m+p] = Σ_j x[m−j]·W[p+2j], as upconv_subpixel_matrices)."""
+    cout, cin = w.shape[:2]
+    if cin % 64:
+        raise ValueError("Cin must be a multiple of 64")
+    w = w.double()
+    out = torch.zeros(cin // 64, 5, 2, cout, 64, dtype=torch.float64)
+    for st, ((jy, jx), phases) in enumerate(UPCONV_HALO_STEPS):
+        for slot, ph in enumerate(phases):
+            if ph is None:
+                continue
+            py, px = ph >> 1, ph & 1
+            wk = w[:, :, py + 2 * jy, px + 2 * jx]  # (cout, cin)
+            out[:, st, slot] = wk.reshape(cout, cin // 64, 64).permute(1, 0, 2)
+    return out.to(dtype)
+
+
 def upconv_dgrad_matrix(w, dtype):
     """Input gradient of conv_transpose2d(stride 2): gx[i] = Σ_k gT[2i+k]·W[k] — a stride-2 3×3
     conv with Wd[ci][(ky·3+kx)·Cout + co] = W[co][ci][ky][kx] (no flip)."""

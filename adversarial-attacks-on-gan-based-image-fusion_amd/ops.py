@@ -144,9 +144,10 @@ def upconv_kpad(cin, phase, dtype):
     return (kh * kw * cin + bk - 1) // bk * bk
 
 
-def upconv_fwd(x, w_phases, t_out, cout, act_in=ACT_NONE, style=None, flops=None):
+def upconv_fwd(x, w_phases, t_out, cout, act_in=ACT_NONE, style=None, flops=None, w_up=None):
     """conv_transpose2d(stride 2) as 4 sub-pixel phase GEMMs (one launch). x: (N,R,R,Cin) →
-    T: (N, 2R+1, 2R+1, Cout)."""
+    T: (N, 2R+1, 2R+1, Cout). ``w_up`` (layouts.upconv_halo_matrix): the halo-tiled kernel
+    (mia_upconv_fwd_halo; the library falls back to the phase GEMMs where it does not apply)."""
     N, R, R2, Cin = x.shape
     T = x.dtype
     if R != R2:
@@ -160,8 +161,14 @@ def upconv_fwd(x, w_phases, t_out, cout, act_in=ACT_NONE, style=None, flops=None
     wp = (ctypes.c_void_p * 4)(*[w.data_ptr() for w in w_phases])
     for w in w_phases:
         ptr(w)
-    _prof_call("mia_upconv_fwd", flops if flops is not None else 2 * N * R * R * 9 * Cin * cout,
-               ptr(x), wp, ptr(t_out), N, R, Cin, cout, act_in, ptr(style), dt(T), stream())
+    fl = flops if flops is not None else 2 * N * R * R * 9 * Cin * cout
+    if w_up is not None:
+        _need(w_up, (Cin // 64, 5, 2, cout, 64), T, "w_up")
+        _prof_call("mia_upconv_fwd_halo", fl, ptr(x), wp, ptr(w_up), ptr(t_out), N, R, Cin, cout,
+                   act_in, ptr(style), dt(T), stream())
+        return t_out
+    _prof_call("mia_upconv_fwd", fl, ptr(x), wp, ptr(t_out), N, R, Cin, cout, act_in, ptr(style),
+               dt(T), stream())
     return t_out
 
 

@@ -58,6 +58,8 @@ class SynthesisNet:
             if c["up"] and up_mode == "subpixel":
                 L["wph"] = [m.contiguous().to(dev)
                             for m in layouts.upconv_subpixel_matrices(ws, dtype)]
+                if dtype != torch.float32 and cin % 64 == 0 and cout % 64 == 0:
+                    L["wup"] = layouts.upconv_halo_matrix(ws, dtype).contiguous().to(dev)
                 L["wd"] = layouts.upconv_dgrad_matrix(ws, dtype).contiguous().to(dev)
             elif c["up"]:
                 ph = layouts.upconv_phases(ws)
@@ -180,7 +182,8 @@ class SynthesisNet:
             pre = ws.get(f"g.pre{i}", (N, r, r, cout), T)
             if L["up"] and self.up_mode == "subpixel":
                 t = ws.get(f"g.t{i}", (N, r + 1, r + 1, cout), T)
-                ops.upconv_fwd(x, L["wph"], t, cout, style=L["_s"], flops=self._alg_flops(L, N))
+                ops.upconv_fwd(x, L["wph"], t, cout, style=L["_s"], flops=self._alg_flops(L, N),
+                               w_up=L.get("wup"))
                 ops.upconv_blur_fwd(t, pre, L["_d"], L["noise"], L["noise_w"], L["bias"],
                                     act_out=ACT_LRELU_S2)
             else:

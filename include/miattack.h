@@ -124,6 +124,16 @@ int mia_vgg_conv_dgrad(const void* g, const void* w_t, void* gx, int N, int H, i
 int mia_upconv_kpad(int cin, int phase, int dtype);
 int mia_upconv_fwd(const void* x, const void* const* w_phase, void* t_out, int N, int R, int Cin,
                    int Cout, int act_in, const float* style, int dtype, void* stream);
+/* Same result as mia_upconv_fwd from ONE halo-tiled MFMA launch over the interior (input halo
+ * staged in LDS once per 64-channel block and read by all 9 (offset, phase) products) plus a
+ * generic launch for the last row / column of the even phase grids. w_up: the packed weights
+ * [Cin/64][5][2][Cout][64] of layouts.upconv_halo_matrix (K-step st = offset (0,0)·{p0,p1},
+ * (0,0)·{p2,p3}, (0,−1)·{p0,p2}, (−1,0)·{p0,p1}, (−1,−1)·{p0}; phase p = 2·py + px; slot weight
+ * W[:, :, py + 2·jy, px + 2·jx]). Falls back to mia_upconv_fwd (w_phase) for fp32, R % 16 ≠ 0,
+ * Cin % 64 ≠ 0, Cout % 64 ≠ 0 or w_up == NULL. Replaces the same [ext] conv_transpose2d. */
+int mia_upconv_fwd_halo(const void* x, const void* const* w_phase, const void* w_up, void* t_out,
+                        int N, int R, int Cin, int Cout, int act_in, const float* style,
+                        int dtype, void* stream);
 /* pre = demod·Blur(T) + noise_w·noise + bias, (N, 2R, 2R, C) (rosinality Blur pad (1,1));
  * act_out = MIA_ACT_LRELU_S2 stores the StyledConv activation lrelu(pre)·√2 instead. */
 int mia_upconv_blur_fwd(const void* t, void* pre, const float* demod, const float* noise,

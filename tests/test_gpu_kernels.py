@@ -602,3 +602,69 @@ def test_fused_backward_front_epilogue(cuda, dtype, N, H, Cin, Cout, up):
     assert rel_err(gy2, gy1) < tol
     assert rel_err(q2, q1) < (1e-4 if dtype == torch.float32 else 3e-2)
     assert rel_err(sd2, sd1) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 17, 16), (3, 16, 64)])
+@pytest.mark.parametrize("thin", ["1", "0"])
+def test_conv_thin_vgg_input_layer(cuda, monkeypatch, dtype, N, H, W, thin):
+    """VGG conv1_1 forward (8-channel padded image → 64, bias, ReLU) and its input gradient
+    (64 → 8 channels, 3 real) on the thin-channel kernels (conv_thin.hip; MIA_CONV_THIN=0 = the
+    implicit-GEMM tiles), against torch fp64 on the same rounded operands."""
+    monkeypatch.setenv("MIA_CONV_THIN", thin)
+    g = torch.Generator().manual_seed(N * 100 + H + W)
+    x = torch.zeros(N, 8, H, W)
+    x[:, :3] = torch.rand(N, 3, H, W, generator=g) * 2 - 1
+    w = torch.randn(64, 3, 3, 3, generator=g) / math.sqrt(27)
+    b = torch.randn(64, generator=g) * 0.1
+    wp = torch.zeros(64, 8, 3, 3)
+    wp[:, :3] = w
+    xq, wq = x.to(dtype).double(), wp.to(dtype).double()
+    ref = F.relu(F.conv2d(xq, wq, b.double(), padding=1))
+    y = torch.empty(N, H, W, 64, dtype=dtype, device=cuda)
+    ops.conv3x3(nhwc(x, dtype).to(cuda), layouts.fwd_matrix(w, dtype, cin_pad=8).to(cuda), y,
+                cout=64, bias=b.to(cuda), act_out=ops.ACT_RELU)
+    # input gradient of conv1_1: g (64 ch) → 8 channels
+    gout = torch.randn(N, 64, H, W, generator=g)
+    gq = gout.to(dtype).double()
+    xx = torch.zeros(N, 8, H, W, dtype=torch.float64, requires_grad=True)
+    (gx_ref,) = torch.autograd.grad((F.conv2d(xx, wq, padding=1) * gq).sum(), xx)
+    gx = torch.empty(N, H, W, 8, dtype=dtype, device=cuda)
+    ops.conv3x3(nhwc(gout, dtype).to(cuda), layouts.dgrad_matrix(w, dtype, cin_pad=8).to(cuda), gx,
+                cout=8)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(y), ref) < 2 * TOL[dtype]
+    assert rel_err(nchw(gx), gx_ref) < 2 * TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,cin,cout,R", [(2, 64, 64, 16), (1, 128, 192, 32), (2, 256, 128, 16),
+                                          (1, 64, 64, 8)])
+@pytest.mark.parametrize("lrelu_in", [False, True])
+def test_upconv_halo_fwd(cuda, dtype, N, cin, cout, R, lrelu_in):
+    """mia_upconv_fwd_halo (halo-tiled interior + generic last row / column) against the
+    transposed conv in fp64 on the same rounded operands, and against the phase-GEMM path
+    (R = 8: the library falls back to it)."""
+    g = torch.Generator().manual_seed(N + cin + cout + R)
+    x = torch.randn(N, cin, R, R, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(9 * cin)
+    s = torch.rand(N, cin, generator=g) + 0.5
+    xq = x.to(dtype).double()
+    xin = F.leaky_relu(xq, 0.2) * math.sqrt(2) if lrelu_in else xq
+    sq = (s * (math.sqrt(2) if lrelu_in else 1.0)).to(dtype).double() / (
+        math.sqrt(2) if lrelu_in else 1.0)
+    xm = (xin * sq.view(N, cin, 1, 1))
+    wq = w.to(dtype).double()
+    ref = F.conv_transpose2d(xm, wq.transpose(0, 1), stride=2)  # (N, cout, 2R+1, 2R+1)
+    xd = nhwc(x, dtype).to(cuda)
+    wph = [m.to(cuda) for m in layouts.upconv_subpixel_matrices(w, dtype)]
+    wup = layouts.upconv_halo_matrix(w, dtype).to(cuda)
+    act = ops.ACT_LRELU_S2 if lrelu_in else ops.ACT_NONE
+    t1 = torch.full((N, 2 * R + 1, 2 * R + 1, cout), float("nan"), dtype=dtype, device=cuda)
+    t2 = torch.empty_like(t1)
+    ops.upconv_fwd(xd, wph, t1, cout, act_in=act, style=s.to(cuda), w_up=wup)
+    ops.upconv_fwd(xd, wph, t2, cout, act_in=act, style=s.to(cuda))
+    torch.cuda.synchronize()
+    assert not torch.isnan(t1).any(), "halo path left T positions unwritten"
+    assert rel_err(nchw(t1), ref) < 3 * TOL[dtype]
+    assert rel_err(t1.float(), t2.float()) < 2 * TOL[dtype]

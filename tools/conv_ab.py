@@ -1,0 +1,132 @@
+"""A/B timing of the 3×3 conv kernels on the attack step's layer shapes (GPU, tuning aid).
+
+Usage: python tools/conv_ab.py [--batch 128] [--iters 5] VAR=a,b ...
+Each VAR=v1,v2 names an environment switch read per launch by libmiattack (MIA_HALO_RB,
+MIA_CONV_HALO, ...); every combination is timed on every shape with HIP events on the current
+stream, and the algorithmic TFLOP/s (2·M·9·Cin·Cout) is printed. Not part of the product path."""
+import argparse
+import itertools
+import math
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import gfa_import  # noqa: E402,F401
+from gfa_amd import ops  # noqa: E402
+
+# (name, H, Cin, Cout, mode)
+SHAPES = [
+    ("mod 256² 128→128", 256, 128, 128, "mod"),
+    ("mod 128² 256→256", 128, 256, 256, "mod"),
+    ("mod 64² 512→512", 64, 512, 512, "mod"),
+    ("vgg 128² 64→128", 128, 64, 128, "vgg"),
+    ("vgg 128² 128→128", 128, 128, 128, "vgg"),
+    ("vgg 64² 256→256", 64, 256, 256, "vgg"),
+    ("vgg 32² 512→512", 32, 512, 512, "vgg"),
+    ("dgrad+sdot 256² 128→128", 256, 128, 128, "sdot"),
+    ("dgrad+tap 64² 256→256", 64, 256, 256, "tap"),
+    ("thin vgg1_1 256² 8→64", 256, 8, 64, "vgg"),
+    ("thin dgrad 256² 64→8", 256, 64, 8, "plain"),
+    ("vgg 256² 64→64", 256, 64, 64, "vgg"),
+    ("dgrad+tap 256² 64→64", 256, 64, 64, "tap"),
+    ("dgrad 128² 128→64", 128, 128, 64, "plain"),
+    ("up 128²→256² 256→128", 128, 256, 128, "up"),
+    ("up 64²→128² 512→256", 64, 512, 256, "up"),
+    ("up 32²→64² 512→512", 32, 512, 512, "up"),
+]
+
+
+def run_up(H, Cin, Cout, N, iters, dtype, dev):
+    from gfa_amd import layouts
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(N, H, H, Cin, device=dev, generator=g).to(dtype)
+    w = torch.randn(Cout, Cin, 3, 3, generator=torch.Generator().manual_seed(1)) / math.sqrt(9 * Cin)
+    wph = [m.to(dev) for m in layouts.upconv_subpixel_matrices(w, dtype)]
+    wup = layouts.upconv_halo_matrix(w, dtype).to(dev)
+    s = torch.rand(N, Cin, device=dev, generator=g) + 0.5
+    t = torch.empty(N, 2 * H + 1, 2 * H + 1, Cout, device=dev, dtype=dtype)
+    call = lambda: ops.upconv_fwd(x, wph, t, Cout, style=s, w_up=wup)  # noqa: E731
+    call()
+    torch.cuda.synchronize()
+    ref = t.float().clone()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        call()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    return ms, 2.0 * N * H * H * 9 * Cin * Cout / (ms * 1e-3) / 1e12, ref
+
+
+def run(name, H, Cin, Cout, mode, N, iters, dtype, dev):
+    if mode == "up":
+        return run_up(H, Cin, Cout, N, iters, dtype, dev)
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(N, H, H, Cin, device=dev, generator=g).to(dtype)
+    kp = ops.conv_kpad(Cin, dtype)
+    w = (torch.randn(Cout, kp, device=dev, generator=g) / math.sqrt(9 * Cin)).to(dtype)
+    y = torch.empty(N, H, H, Cout, device=dev, dtype=dtype)
+    kw = {}
+    if mode == "mod":
+        kw = dict(in_scale=torch.rand(N, Cin, device=dev, generator=g) + 0.5,
+                  out_scale=torch.rand(N, Cout, device=dev, generator=g) + 0.5,
+                  noise=torch.randn(H * H, device=dev, generator=g), noise_w=0.1,
+                  bias=torch.randn(Cout, device=dev, generator=g), act_out=ops.ACT_LRELU_S2)
+    elif mode == "vgg":
+        kw = dict(bias=torch.randn(Cout, device=dev, generator=g), act_out=ops.ACT_RELU)
+    elif mode == "sdot":
+        kw = dict(out_scale=torch.rand(N, Cout, device=dev, generator=g) + 0.5,
+                  aux_x=torch.randn(N, H, H, Cout, device=dev, generator=g).to(dtype),
+                  sdot=torch.zeros(N, Cout, device=dev))
+    elif mode == "tap":
+        a = torch.randn(N, H, H, Cout, device=dev, generator=g).relu().to(dtype)
+        kw = dict(tap_a=a, tap_t=torch.randn(N, H, H, Cout, device=dev, generator=g).to(dtype), tap_coef=0.3, mask_a=a)
+    ops.conv3x3(x, w, y, cout=Cout, **kw)
+    torch.cuda.synchronize()
+    ref = y.float().clone()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        ops.conv3x3(x, w, y, cout=Cout, **kw)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    tf = 2.0 * N * H * H * 9 * Cin * Cout / (ms * 1e-3) / 1e12
+    return ms, tf, ref
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16"])
+    ap.add_argument("--only", default="")
+    ap.add_argument("vars", nargs="*")
+    a = ap.parse_args()
+    dtype = torch.float16 if a.dtype == "fp16" else torch.bfloat16
+    dev = torch.device("cuda:0")
+    keys = [v.split("=")[0] for v in a.vars]
+    vals = [v.split("=")[1].split(",") for v in a.vars]
+    combos = list(itertools.product(*vals)) or [()]
+    for name, H, Cin, Cout, mode in SHAPES:
+        if a.only and not any(o in name for o in a.only.split("|")):
+            continue
+        refs = []
+        line = f"{name:28s}"
+        for c in combos:
+            for k, v in zip(keys, c):
+                os.environ[k] = v
+            ms, tf, ref = run(name, H, Cin, Cout, mode, a.batch, a.iters, dtype, dev)
+            refs.append(ref)
+            d = (ref - refs[0]).abs().max().item() / max(refs[0].abs().max().item(), 1e-30)
+            tag = ",".join(f"{k}={v}" for k, v in zip(keys, c))
+            line += f" | {tag}: {ms:7.3f} ms {tf:6.1f} TF/s (d={d:.1e})"
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -181,9 +181,9 @@ def main():
         peak = PEAK_TFLOPS[args.dtype]
         traffic, src = pmc_traffic(args.dtype, B, S, args.pgd_steps)
         out["roofline"] = {
-            "kernel": "3x3 conv: mia::conv_halo_kernel<...> + mia::conv_kernel<...> (every "
-                      "instantiation and launch: StyledConv fwd, sub-pixel up-conv, dgrads, VGG "
-                      "fwd/dgrad)",
+            "kernel": "3x3 conv: every conv API call of the step (mia::conv_halo_kernel, "
+                      "mia::upconv_halo_kernel + its edge launch, mia::conv_kernel, "
+                      "mia::conv_thin_*: StyledConv fwd, up-conv, dgrads, VGG fwd/dgrad)",
             "bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
             "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": src,
             "launches": n, "avg_launch_us": tot_ms / n * 1e3,

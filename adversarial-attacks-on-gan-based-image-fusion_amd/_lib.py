@@ -14,7 +14,7 @@ c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64
 P = c_void_p
 
 MIA_F32, MIA_F16, MIA_BF16 = 0, 1, 2
-ACT_NONE, ACT_RELU, ACT_LRELU_S2 = 0, 1, 2
+ACT_NONE, ACT_RELU, ACT_LRELU_S2, ACT_PRELU = 0, 1, 2, 3
 
 
 class ConvArgs(ctypes.Structure):
@@ -30,7 +30,15 @@ class ConvArgs(ctypes.Structure):
         ("accumulate", c_int),
         ("bab_demod", P), ("bab_noise", P), ("bab_noise_w", c_float), ("bab_bias", P),
         ("bab_q", P),
+        ("mask_slope", P), ("act_slope", P), ("csum", P),
     ]
+
+
+class ConvGroup(ctypes.Structure):
+    """Mirror of ``mia_conv_group``."""
+    _fields_ = [("w", P), ("kh", c_int), ("kw", c_int), ("pad_y", c_int), ("pad_x", c_int),
+                ("ho", c_int), ("wo", c_int), ("ay", c_int), ("by", c_int), ("ax", c_int),
+                ("bx", c_int)]
 
 
 class GemmSeg(ctypes.Structure):
@@ -111,6 +119,21 @@ SIGNATURES = {
     "mia_truncate": (c_int, [P, P, c_float, P, c_int, c_int, P]),
     "mia_repeat": (c_int, [P, P, c_int64, c_int, P]),
     "mia_memset": (c_int, [P, c_int, c_int64, P]),
+    "mia_conv2d_kpad": (c_int, [c_int, c_int, c_int]),
+    "mia_conv2d": (c_int, [ctypes.POINTER(ConvArgs), c_int, ctypes.POINTER(ConvGroup), c_int,
+                           c_int, c_int, c_int, P]),
+    "mia_se_fwd": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
+    "mia_se_apply": (c_int, [P, P, P, c_int, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "mia_chan_dot": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "mia_se_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
+    "mia_se_grad_scale": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
+    "mia_prelu_bwd_scale": (c_int, [P, P, P, P, P, c_int64, c_int, c_int, P]),
+    "mia_subsample_add": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "mia_cast": (c_int, [P, c_int, P, c_int, c_int64, c_float, P]),
+    "mia_bilinear_fwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                 P]),
+    "mia_bilinear_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                 P]),
 }
 
 _lib = None

@@ -205,9 +205,16 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
   const T* TT = (const T*)p.tap_t;
   const T* MA = (const T*)p.mask_a;
   T* __restrict__ Y = (T*)p.y;
-  float part[8], partq[8];
+  float part[8], partq[8], pcs[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) part[e] = partq[e] = 0.f;
+  for (int e = 0; e < 8; ++e) part[e] = partq[e] = pcs[e] = 0.f;
+  // encoder features: PReLU act / mask slopes per column
+  float aslope8[8], mslope8[8];
+  const bool prelu = p.act_out == MIA_ACT_PRELU;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) aslope8[e] = mslope8[e] = 0.f;
+  if (prelu && col_ok) load8f(p.act_slope + col, aslope8);
+  if (p.mask_slope && col_ok) load8f(p.mask_slope + col, mslope8);
   const bool bab = p.bab_demod != nullptr;
   float bbias8[8];
   if (bab) {
@@ -247,8 +254,21 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
       if (row >= 0 && col_ok) {
         float v[8];
         load8f(tile + rr * ES + cc * 8, v);
-        const size_t aoff = (size_t)row * Cout + col;
         const int n = single ? n_single : row / HWo;
+        // output placement (aux operands share the output's pixel grid, channel stride Cout)
+        const int pix = row - n * HWo;
+        const int y = pix / G.wo, x = pix - (pix / G.wo) * G.wo;
+        int cm = col, yo, xo;
+        if (p.shuffle_out) {
+          const int ph = col / k.cout_mod;
+          cm = col - ph * k.cout_mod;
+          yo = 2 * y + (ph >> 1);
+          xo = 2 * x + (ph & 1);
+        } else {
+          yo = G.ay * y + G.by;
+          xo = G.ax * x + G.bx;
+        }
+        const size_t aoff = ((size_t)(n * k.HT + yo) * k.WT + xo) * Cout + col;
         float xv[8];
         if (p.sdot || bab) load8<T>(AX + aoff, xv);
         if (p.sdot) {
@@ -260,18 +280,6 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
           }
         }
         if (Y) {
-          const int pix = row - n * HWo;
-          const int y = pix / G.wo, x = pix - (pix / G.wo) * G.wo;
-          int cm = col, yo, xo;
-          if (p.shuffle_out) {
-            const int ph = col / k.cout_mod;
-            cm = col - ph * k.cout_mod;
-            yo = 2 * y + (ph >> 1);
-            xo = 2 * x + (ph & 1);
-          } else {
-            yo = G.ay * y + G.by;
-            xo = G.ax * x + G.bx;
-          }
           const size_t off = ((size_t)(n * k.HT + yo) * k.WT + xo) * k.ystride + cm;
           if (p.out_scale) {
             if (!single) load8f(p.out_scale + (size_t)n * k.cout_mod + cm, osc8);
@@ -298,10 +306,15 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
           if (MA) {
             if (MA != TA) load8<T>(MA + aoff, ma);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = ma[e] > 0.f ? v[e] : 0.f;
+            for (int e = 0; e < 8; ++e) v[e] = ma[e] > 0.f ? v[e] : mslope8[e] * v[e];
           }
+          if (prelu) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], p.act_out);
+            for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : aslope8[e] * v[e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], p.act_out);
+          }
           if (p.accumulate) {
             float yo8[8];
             load8<T>(Y + off, yo8);
@@ -321,6 +334,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
               if (single) partq[e] += c;
               else atomicAdd(&p.bab_q[(size_t)n * Cout + col + e], c);
               v[e] = gp * dm8[e];
+            }
+          }
+          if (p.csum) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              if (single) pcs[e] += v[e];
+              else atomicAdd(&p.csum[(size_t)n * Cout + col + e], v[e]);
             }
           }
           store8<T>(Y + off, v);
@@ -346,6 +366,24 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
 #pragma unroll
       for (int w = 0; w < NW; ++w) s += red[w * BN + tid];
       atomicAdd(&p.bab_q[(size_t)n_single * Cout + n0 + tid], s);
+    }
+    __syncthreads();
+  }
+  if (p.csum && single) {  // Σ_p y partials: the same reduction as sdot below
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      for (int o = CPR; o < 64; o <<= 1) pcs[e] += __shfl_xor(pcs[e], o, 64);
+    float* red = (float*)smem;
+    if (worker && lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[wid * BN + lane * 8 + e] = pcs[e];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < Cout) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s += red[w * BN + tid];
+      atomicAdd(&p.csum[(size_t)n_single * Cout + n0 + tid], s);
     }
     __syncthreads();
   }

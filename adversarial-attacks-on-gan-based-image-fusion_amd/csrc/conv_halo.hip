@@ -105,6 +105,8 @@ __device__ __forceinline__ void halo_epilogue(const ConvK& k, const f32x4 (&acc)
   T* __restrict__ Y = (T*)p.y;
   const bool bab = p.bab_demod != nullptr;
   float osc[FN][4], bia[FN][4], dmv[FN][4], bbv[FN][4], part[FN][4], partq[FN][4];
+  float msl[FN][4], asl[FN][4], pcs[FN][4];
+  const bool prelu = p.act_out == MIA_ACT_PRELU;
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int c = cl + 16 * j;
@@ -112,10 +114,13 @@ __device__ __forceinline__ void halo_epilogue(const ConvK& k, const f32x4 (&acc)
     for (int e = 0; e < 4; ++e) {
       osc[j][e] = 1.f;
       bia[j][e] = dmv[j][e] = bbv[j][e] = part[j][e] = partq[j][e] = 0.f;
+      msl[j][e] = asl[j][e] = pcs[j][e] = 0.f;
     }
     if (c < Cout) {  // c ≡ 0 mod 4 and Cout ≡ 0 mod 8: the whole quad is in range
       if (p.out_scale) ld4f(p.out_scale + (size_t)n * k.cout_mod + c, osc[j]);
       if (p.bias) ld4f(p.bias + c, bia[j]);
+      if (p.mask_slope) ld4f(p.mask_slope + c, msl[j]);
+      if (prelu) ld4f(p.act_slope + c, asl[j]);
       if (bab) {
         ld4f(p.bab_demod + (size_t)n * Cout + c, dmv[j]);
         if (p.bab_bias) ld4f(p.bab_bias + c, bbv[j]);
@@ -163,10 +168,15 @@ __device__ __forceinline__ void halo_epilogue(const ConvK& k, const f32x4 (&acc)
         if (MA) {
           if (MA != TA) load4<T>(MA + aoff, ma);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = ma[e] > 0.f ? v[e] : 0.f;
+          for (int e = 0; e < 4; ++e) v[e] = ma[e] > 0.f ? v[e] : msl[j][e] * v[e];
         }
+        if (prelu) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act_out);
+          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : asl[j][e] * v[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act_out);
+        }
         if (p.accumulate) {
           float yo[4];
           load4<T>(Y + off, yo);
@@ -181,6 +191,10 @@ __device__ __forceinline__ void halo_epilogue(const ConvK& k, const f32x4 (&acc)
             partq[j][e] += gp * (xv[e] / gr - bnz - bbv[j][e]);
             v[e] = gp * dmv[j][e];
           }
+        }
+        if (p.csum) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pcs[j][e] += v[e];
         }
         if constexpr (WIDE) {
 #pragma unroll
@@ -215,21 +229,23 @@ __device__ __forceinline__ void halo_epilogue(const ConvK& k, const f32x4 (&acc)
       }
     }
   }
-  if (p.sdot || bab) {
+  if (p.sdot || bab || p.csum) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int c = cl + 16 * j;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        float a = part[j][e], b = partq[j][e];
+        float a = part[j][e], b = partq[j][e], cs = pcs[j][e];
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {
           a += __shfl_xor(a, o, 64);
           b += __shfl_xor(b, o, 64);
+          cs += __shfl_xor(cs, o, 64);
         }
         if (px == 0 && c < Cout) {
           if (p.sdot) atomicAdd(&p.sdot[(size_t)n * Cout + c + e], a);
           if (bab) atomicAdd(&p.bab_q[(size_t)n * Cout + c + e], b);
+          if (p.csum) atomicAdd(&p.csum[(size_t)n * Cout + c + e], cs);
         }
       }
     }
@@ -724,6 +740,7 @@ static int launch_halo_tile_(ConvK& k, hipStream_t st) {
 static int epi_mask(const ConvK& k) {
   const mia_conv_args& a = k.a;
   if ((a.sdot || a.bab_demod) && a.act_aux != MIA_ACT_NONE) return -1;
+  if (a.mask_slope || a.act_out == MIA_ACT_PRELU || a.csum) return -1;  // encoder features
   int f = 0;
   if (a.out_scale) f |= epi::OSC;
   if (a.noise) f |= epi::NOISE;

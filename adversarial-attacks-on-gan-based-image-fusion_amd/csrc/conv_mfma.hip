@@ -314,6 +314,8 @@ static int run_conv(ConvK& k, int dtype, hipStream_t st) {
                                  !a.shuffle_out),
                 "bab_demod needs aux_x (stored activations, act_aux NONE), bab_q and y");
   MIA_CHECK_ARG(!a.tap_a || a.tap_t, "tap_a needs tap_t");
+  MIA_CHECK_ARG(a.act_out != MIA_ACT_PRELU || a.act_slope, "MIA_ACT_PRELU needs act_slope");
+  MIA_CHECK_ARG(!a.csum || (a.y && !a.shuffle_out), "csum needs y (un-shuffled)");
   MIA_CHECK_ARG(!a.shuffle_out || !(a.tap_a || a.mask_a || a.sdot),
                 "aux inputs need un-shuffled output");
   MIA_CHECK_ARG((int64_t)a.N * a.H * a.W * a.Cin < (1LL << 31), "input too large for 32-bit offsets");
@@ -326,9 +328,11 @@ static int run_conv(ConvK& k, int dtype, hipStream_t st) {
     MIA_CHECK_ARG(G.kpad == kpad_for(G.kh * G.kw * a.Cin, dtype), "Kpad must be mia_conv_kpad()");
     MIA_CHECK_ARG(G.ho > 0 && G.wo > 0, "empty output grid");
     MIA_CHECK_ARG((int64_t)a.N * G.ho * G.wo < (1LL << 31), "too many pixels");
-    MIA_CHECK_ARG(!(a.sdot || a.tap_a || a.mask_a || a.bab_demod) ||
-                      (k.ng == 1 && G.ho * G.wo == k.HT * k.WT),
-                  "aux operands need one group with an identity output placement");
+    MIA_CHECK_ARG(!(a.sdot || a.bab_demod) || (k.ng == 1 && G.ho * G.wo == k.HT * k.WT),
+                  "sdot / bab need one group with an identity output placement");
+    MIA_CHECK_ARG(G.ay * (G.ho - 1) + G.by < k.HT && G.ax * (G.wo - 1) + G.bx < k.WT &&
+                      G.by >= 0 && G.bx >= 0,
+                  "output placement outside the output grid");
   }
   int lc = 0;
   while ((1 << lc) < a.Cin) ++lc;
@@ -370,6 +374,45 @@ extern "C" int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream) {
   k.cout_mod = a.shuffle_out ? a.Cout / 4 : a.Cout;
   k.ystride = a.y_cstride > 0 ? a.y_cstride : k.cout_mod;
   MIA_CHECK_ARG(k.ystride >= k.cout_mod, "y_cstride < Cout");
+  return run_conv(k, dtype, (hipStream_t)stream);
+}
+
+extern "C" int mia_conv2d_kpad(int taps, int cin, int dtype) { return kpad_for(taps * cin, dtype); }
+
+extern "C" int mia_conv2d(const mia_conv_args* args, int stride, const mia_conv_group* groups,
+                          int ngroups, int out_h, int out_w, int dtype, void* stream) {
+  MIA_CHECK_ARG(args != nullptr && groups != nullptr, "null args");
+  MIA_CHECK_ARG(ngroups >= 1 && ngroups <= 4, "1..4 groups");
+  MIA_CHECK_ARG(stride == 1 || stride == 2, "stride 1 or 2");
+  MIA_CHECK_ARG(out_h > 0 && out_w > 0, "empty output");
+  MIA_CHECK_ARG(!args->shuffle_out, "shuffle_out is a mia_conv3x3 feature");
+  const mia_conv_args& a = *args;
+  ConvK k = {};
+  k.a = a;
+  k.stride = stride;
+  k.ng = ngroups;
+  k.HT = out_h;
+  k.WT = out_w;
+  k.cout_mod = a.Cout;
+  k.ystride = a.y_cstride > 0 ? a.y_cstride : a.Cout;
+  MIA_CHECK_ARG(k.ystride >= a.Cout, "y_cstride < Cout");
+  for (int g = 0; g < ngroups; ++g) {
+    const mia_conv_group& s = groups[g];
+    ConvGroup& G = k.g[g];
+    G.w = s.w;
+    G.kh = s.kh;
+    G.kw = s.kw;
+    G.kpad = kpad_for(s.kh * s.kw * a.Cin, dtype);
+    G.pad_y = s.pad_y;
+    G.pad_x = s.pad_x;
+    G.ho = s.ho;
+    G.wo = s.wo;
+    G.ay = s.ay;
+    G.by = s.by;
+    G.ax = s.ax;
+    G.bx = s.bx;
+    G.m = a.N * s.ho * s.wo;
+  }
   return run_conv(k, dtype, (hipStream_t)stream);
 }
 

@@ -216,7 +216,8 @@ bool conv_thin_eligible(const ConvK& k, int dtype) {
       G.pad_x != 1 || G.ho != a.H || G.wo != a.W || G.ay != 1 || G.ax != 1 || G.by != 0 ||
       G.bx != 0 || a.shuffle_out || a.W % 16 != 0 || k.HT != a.H || k.WT != a.W ||
       k.ystride != a.Cout || a.act_in != MIA_ACT_NONE || a.in_scale || a.out_scale || a.noise ||
-      a.tap_a || a.mask_a || a.sdot || a.bab_demod || a.accumulate || !a.y)
+      a.tap_a || a.mask_a || a.sdot || a.bab_demod || a.accumulate || !a.y || a.csum ||
+      a.act_out == MIA_ACT_PRELU)
     return false;
   if (a.Cin == 8 && a.Cout == 64 && G.kpad >= 96) return true;
   if (a.Cin == 64 && a.Cout == 8 && !a.bias && a.act_out == MIA_ACT_NONE) return true;

@@ -118,3 +118,42 @@ def upconv_phases(w):
                             acc += BLUR_F[jy] * BLUR_F[jx] * w[:, :, ky, kx]
                     v[py, px, :, :, ty, tx] = acc
     return v.reshape(4 * cout, cin, 3, 3)
+
+
+# ---- e4e encoder: strided convolutions ------------------------------------------------------------
+# Input gradient of a stride-2, pad-1 3×3 conv (out[o] = Σ_k in[2o + k − 1]·W[k] per axis) as four
+# sub-pixel phase GEMMs over the output gradient g: gin[2i] = g[i]·W[1];
+# gin[2i+1] = g[i]·W[2] + g[i+1]·W[0]. Phase p of an axis is a window conv with kh = 1 + p taps,
+# pad 0, tap t ↔ kernel index S2_KMAP[p][t], placed at output row 2i + p.
+S2_KMAP = ((1,), (2, 0))
+
+
+def s2_dgrad_phases(w, dtype):
+    """w: (Cout, Cin, 3, 3) of the forward stride-2 conv → [(matrix [Cin][Kpad], py, px)] for
+    phases p = 2·py + px, K index = (ty·kw + tx)·Cout + co (mia_conv2d groups)."""
+    cout, cin = w.shape[:2]
+    w = w.double()
+    bk = 32 if dtype == torch.float32 else 64
+    out = []
+    for ph in range(4):
+        py, px = ph >> 1, ph & 1
+        ky, kx = S2_KMAP[py], S2_KMAP[px]
+        m = torch.zeros(cin, len(ky), len(kx), cout, dtype=torch.float64)
+        for ty, a in enumerate(ky):
+            for tx, b in enumerate(kx):
+                m[:, ty, tx, :] = w[:, :, a, b].t()
+        k = len(ky) * len(kx) * cout
+        full = torch.zeros(cin, (k + bk - 1) // bk * bk, dtype=torch.float64)
+        full[:, :k] = m.reshape(cin, -1)
+        out.append((full.to(dtype), py, px))
+    return out
+
+
+def conv1x1_matrix(w, dtype):
+    """(Cout, Cin[, 1, 1]) → [Cout][Kpad] (K = Cin, zero-padded to the K-step)."""
+    w = w.reshape(w.shape[0], -1).double()
+    cout, cin = w.shape
+    bk = 32 if dtype == torch.float32 else 64
+    full = torch.zeros(cout, (cin + bk - 1) // bk * bk, dtype=torch.float64)
+    full[:, :cin] = w
+    return full.to(dtype)

@@ -18,10 +18,12 @@ import math
 
 import torch
 
+from .e4e import E4EEncoder
 from .encoder import SyntheticEncoder
 from .stylegan2 import SynthesisNet
 from .vgg import CPAD, VGGNet
-from .weights import (LR_MLP, N_MLP, STYLE_DIM, make_encoder_weights, make_generator_weights,
+from .weights import (LR_MLP, N_MLP, STYLE_DIM, make_e4e_weights, make_encoder_weights,
+                      make_generator_weights,
                       make_vgg_weights)
 from .workspace import Workspace
 from . import ops
@@ -114,12 +116,18 @@ class Decoder:
 
 
 class Encoder:
-    def __init__(self, params, size, device="cuda"):
-        self.impl = SyntheticEncoder(params, size, device=device)
+    """``net.encoder``: e4e ``Encoder4Editing(50, 'ir_se')`` (params from make_e4e_weights or an
+    e4e checkpoint's ``encoder.*`` state dict + ``latent_avg``) or the linear stand-in."""
+
+    def __init__(self, params, size, device="cuda", dtype=torch.float32):
+        if params.get("kind") == "e4e":
+            self.impl = E4EEncoder(params, size, dtype=dtype, device=device)
+        else:
+            self.impl = SyntheticEncoder(params, size, device=device)
         self._ws = Workspace(torch.device(device))
 
     def __call__(self, x):
-        x = x.to(self.impl.w.device, torch.float32).contiguous()
+        x = x.to(self.impl.latent_avg.device, torch.float32).contiguous()
         return self.impl.forward(x, self._ws).clone()
 
 
@@ -173,11 +181,19 @@ def get_latents(net, x, is_cars=False):
 
 
 def build_net(size=256, seed=0, dtype=torch.float32, device="cuda", vgg_seed=1234,
-              with_vgg=True):
-    """Seeded synthetic pSp bundle (+ VGG) — no checkpoints exist offline."""
+              with_vgg=True, encoder="linear"):
+    """Seeded synthetic pSp bundle (+ VGG) — no checkpoints exist offline.
+    ``encoder``: "e4e" (IR-SE50 Encoder4Editing, the reference's encoder) or "linear" (the
+    SURVEY.md §7 stand-in)."""
     gp = make_generator_weights(size, seed=seed)
-    ep = make_encoder_weights(size, seed=seed + 1)
-    net = PSPNet(Encoder(ep, size, device=device), Decoder(gp, size, dtype=dtype, device=device),
+    if encoder == "e4e":
+        ep = make_e4e_weights(size, seed=seed + 1)
+    elif encoder == "linear":
+        ep = make_encoder_weights(size, seed=seed + 1)
+    else:
+        raise ValueError("encoder: 'e4e' or 'linear'")
+    net = PSPNet(Encoder(ep, size, device=device, dtype=dtype),
+                 Decoder(gp, size, dtype=dtype, device=device),
                  ep["latent_avg"].to(device), ep["start_from_latent_avg"])
     net.params = dict(generator=gp, encoder=ep)
     if with_vgg:

@@ -6,7 +6,7 @@ import ctypes
 import torch
 
 from . import _lib
-from ._lib import ACT_LRELU_S2, ACT_NONE, ACT_RELU, ConvArgs, call  # noqa: F401
+from ._lib import ACT_LRELU_S2, ACT_NONE, ACT_PRELU, ACT_RELU, ConvArgs, call  # noqa: F401
 
 DTYPES = {torch.float32: _lib.MIA_F32, torch.float16: _lib.MIA_F16, torch.bfloat16: _lib.MIA_BF16}
 VEC = {torch.float32: 4, torch.float16: 8, torch.bfloat16: 8}
@@ -613,3 +613,167 @@ def truncate(w, mean, psi, out):
 def zero_(t):
     call("mia_memset", ptr(t), 0, t.numel() * t.element_size(), stream())
     return t
+
+
+# ---- general-geometry conv and the e4e encoder kernels (csrc/encoder.hip) ----------------------
+def conv2d_kpad(taps, cin, dtype):
+    bk = 32 if dtype == torch.float32 else 64
+    return (taps * cin + bk - 1) // bk * bk
+
+
+def conv2d(x, groups, y, out_hw, *, cout, stride=1, bias=None, act_out=ACT_NONE, act_slope=None,
+           mask_a=None, mask_slope=None, csum=None, accumulate=False, out_scale=None, flops=None):
+    """mia_conv2d: 1..4 problems over x (N,H,W,Cin) sharing one epilogue. ``groups``: list of
+    dict(w, kh, kw, pad=(py,px), ho, wo, a=(ay,ax), b=(by,bx)); w is [Cout][conv2d_kpad(kh·kw,
+    Cin)]. y: (N, out_h, out_w, Cout). mask_a lives on y's pixel grid."""
+    N, H, W, Cin = x.shape
+    T = x.dtype
+    oh, ow = out_hw
+    if Cin % VEC[T]:
+        raise ValueError("Cin must be a multiple of the 16-byte vector")
+    if not 1 <= len(groups) <= 4:
+        raise ValueError("1..4 groups")
+    _need(y, (N, oh, ow, cout), T, "y")
+    f32 = torch.float32
+    _numel_ok(bias, cout, f32, "bias")
+    _numel_ok(act_slope, cout, f32, "act_slope")
+    _numel_ok(mask_slope, cout, f32, "mask_slope")
+    _numel_ok(csum, N * cout, f32, "csum")
+    _numel_ok(out_scale, N * cout, f32, "out_scale")
+    if mask_a is not None:
+        _need(mask_a, (N, oh, ow, cout), T, "mask_a")
+    if act_out == ACT_PRELU and act_slope is None:
+        raise ValueError("ACT_PRELU needs act_slope")
+    garr = (_lib.ConvGroup * len(groups))()
+    keep = []
+    mac = 0
+    for i, g in enumerate(groups):
+        kh, kw = g["kh"], g["kw"]
+        _need(g["w"], (cout, conv2d_kpad(kh * kw, Cin, T)), T, f"w[{i}]")
+        py, px = g.get("pad", (0, 0))
+        ay, ax = g.get("a", (1, 1))
+        by, bx = g.get("b", (0, 0))
+        ho, wo = g["ho"], g["wo"]
+        if ho <= 0 or wo <= 0 or ay * (ho - 1) + by >= oh or ax * (wo - 1) + bx >= ow:
+            raise ValueError(f"group {i}: placement outside the output grid")
+        garr[i] = _lib.ConvGroup(ptr(g["w"]).value, kh, kw, py, px, ho, wo, ay, by, ax, bx)
+        keep.append(g["w"])
+        mac += N * ho * wo * kh * kw * Cin * cout
+    a = ConvArgs()
+    a.x, a.y = ptr(x), ptr(y)
+    a.N, a.H, a.W, a.Cin, a.Cout = N, H, W, Cin, cout
+    a.bias, a.out_scale = ptr(bias), ptr(out_scale)
+    a.act_out, a.act_slope = act_out, ptr(act_slope)
+    a.mask_a, a.mask_slope, a.csum = ptr(mask_a), ptr(mask_slope), ptr(csum)
+    a.accumulate = int(bool(accumulate))
+    prof = PROFILE
+    if prof is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    call("mia_conv2d", ctypes.byref(a), int(stride), garr, len(groups), oh, ow, dt(T), stream())
+    if prof is not None:
+        e1.record()
+        prof.append((e0, e1, flops if flops is not None else 2 * mac))
+    return y
+
+
+def se_fwd(csum, w1, w2, u, s, hw):
+    N, C = csum.shape
+    Cr = w1.shape[0]
+    _need(w1, (Cr, C), torch.float32, "w1")
+    _need(w2, (C, Cr), torch.float32, "w2")
+    _need(u, (N, Cr), torch.float32, "u")
+    _need(s, (N, C), torch.float32, "s")
+    call("mia_se_fwd", ptr(csum), ptr(w1), ptr(w2), ptr(u), ptr(s), N, C, Cr, 1.0 / hw, stream())
+    return s
+
+
+def se_apply(r, s, sc, ss, out, g=None, b=None, xb=None):
+    """out = r·s + sc (sc read at stride ss), xb = out·g + b (either output may be None)."""
+    N, H, W, C = r.shape
+    _numel_ok(s, N * C, torch.float32, "s")
+    if sc is not None:
+        _need(sc, (N, H * ss, W * ss, C), r.dtype, "sc")
+    if out is not None:
+        _need(out, r.shape, r.dtype, "out")
+    if xb is not None:
+        _need(xb, r.shape, r.dtype, "xb")
+        _numel_ok(g, C, torch.float32, "g")
+        _numel_ok(b, C, torch.float32, "b")
+    call("mia_se_apply", ptr(r), ptr(s), ptr(sc), int(ss), ptr(out), ptr(g), ptr(b), ptr(xb), N,
+         H, W, C, dt(r), stream())
+    return out if out is not None else xb
+
+
+def chan_dot(a, b, gs, accumulate=False):
+    N, H, W, C = a.shape
+    _need(b, a.shape, a.dtype, "b")
+    _need(gs, (N, C), torch.float32, "gs")
+    call("mia_chan_dot", ptr(a), ptr(b), ptr(gs), N, H * W, C, int(bool(accumulate)), dt(a),
+         stream())
+    return gs
+
+
+def se_bwd(gs, s, u, w1, w2, gavg, hw):
+    N, C = s.shape
+    Cr = w1.shape[0]
+    _need(gs, (N, C), torch.float32, "gs")
+    _need(u, (N, Cr), torch.float32, "u")
+    _need(gavg, (N, C), torch.float32, "gavg")
+    call("mia_se_bwd", ptr(gs), ptr(s), ptr(u), ptr(w1), ptr(w2), ptr(gavg), N, C, Cr, 1.0 / hw,
+         stream())
+    return gavg
+
+
+def se_grad_scale(g_out, s, gavg, g_r, gamma=None):
+    N, H, W, C = g_out.shape
+    _need(g_r, g_out.shape, g_out.dtype, "g_r")
+    _numel_ok(gamma, C, torch.float32, "gamma")
+    call("mia_se_grad_scale", ptr(g_out), ptr(s), ptr(gavg), ptr(gamma), ptr(g_r), N, H * W, C,
+         dt(g_out), stream())
+    return g_r
+
+
+def prelu_bwd_scale(g_a, a, slope, g, gamma=None):
+    C = g_a.shape[-1]
+    _need(a, g_a.shape, g_a.dtype, "a")
+    _need(g, g_a.shape, g_a.dtype, "g")
+    _numel_ok(slope, C, torch.float32, "slope")
+    _numel_ok(gamma, C, torch.float32, "gamma")
+    call("mia_prelu_bwd_scale", ptr(g_a), ptr(a), ptr(slope), ptr(gamma), ptr(g),
+         g_a.numel() // C, C, dt(g_a), stream())
+    return g
+
+
+def subsample_add(g, gx):
+    N, H, W, C = g.shape
+    _need(gx, (N, 2 * H, 2 * W, C), g.dtype, "gx")
+    call("mia_subsample_add", ptr(g), ptr(gx), N, H, W, C, dt(g), stream())
+    return gx
+
+
+def bilinear_fwd(x, y, accumulate=False):
+    N, Hi, Wi, C = x.shape
+    _, Ho, Wo, C2 = y.shape
+    if y.shape[0] != N or C2 != C or y.dtype != x.dtype:
+        raise ValueError("bilinear_fwd: shape/dtype mismatch")
+    call("mia_bilinear_fwd", ptr(x), ptr(y), N, Hi, Wi, Ho, Wo, C, int(bool(accumulate)), dt(x),
+         stream())
+    return y
+
+
+def bilinear_bwd(gy, gx, accumulate=False):
+    N, Ho, Wo, C = gy.shape
+    _, Hi, Wi, C2 = gx.shape
+    if gx.shape[0] != N or C2 != C or gx.dtype != gy.dtype:
+        raise ValueError("bilinear_bwd: shape/dtype mismatch")
+    call("mia_bilinear_bwd", ptr(gy), ptr(gx), N, Hi, Wi, Ho, Wo, C, int(bool(accumulate)),
+         dt(gy), stream())
+    return gx
+
+
+def cast(x, y, scale=1.0):
+    if x.numel() != y.numel():
+        raise ValueError("cast: size mismatch")
+    call("mia_cast", ptr(x), dt(x), ptr(y), dt(y), x.numel(), float(scale), stream())
+    return y

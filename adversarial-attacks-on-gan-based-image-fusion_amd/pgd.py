@@ -75,9 +75,9 @@ class AttackEngine:
         self.x0 = x0
         self.t = t
         self.lat_t = ws.get("ref.lat_t", (N, self.G.n_latent, STYLE_DIM), torch.float32)
-        self.lat_t.copy_(self.E.forward(t, ws))
+        self.lat_t.copy_(self._encode(t, "ref.in")[0])
         self.lat_o = ws.get("ref.lat_o", (N, self.G.n_latent, STYLE_DIM), torch.float32)
-        self.lat_o.copy_(self.E.forward(x0, ws))
+        self.lat_o.copy_(self._encode(x0, "ref.in")[0])
         self.taps_t, self.taps_o = [], []
         for img, dst, nm in ((t, self.taps_t, "t"), (x0, self.taps_o, "o")):
             a = self.V.forward(self._vgg_input(img, "ref.in"), ws, "")
@@ -85,6 +85,14 @@ class AttackEngine:
                 keep = ws.get(f"ref.tap{nm}{k}", tap.shape, self.dtype)
                 keep.copy_(tap)
                 dst.append(keep)
+
+    def _encode(self, img, name):
+        """E(img'). The e4e encoder reads the VGG input tensor x' (N,R,R,8) (both networks see
+        avg_pool2d(img, S/256), attack_main2.py:597,622); returns (lat, x' or None)."""
+        if getattr(self.E, "input_nhwc", False):
+            xin = self._vgg_input(img, name)
+            return self.E.forward_nhwc(xin, self.ws), xin
+        return self.E.forward(img, self.ws), None
 
     def _loss_terms(self, which, out, *tensors):
         """out[n] += the per-image objective terms of one stage (unscaled weights, MSE means)."""
@@ -110,8 +118,7 @@ class AttackEngine:
         returns them; both are scaled by loss_scale. ``loss`` (fp32 [N], zeroed by the caller)
         receives the per-image objective at x from the same forward pass (no host sync)."""
         ws, G, V, E = self.ws, self.G, self.V, self.E
-        N = x.shape[0]
-        lat = E.forward(x, ws)
+        lat, xin = self._encode(x, "in.x")
         rec = G.forward(lat, ws)
         self.rec = rec
         if loss is not None:
@@ -124,7 +131,7 @@ class AttackEngine:
         g_img = ws.get("g.img", rec.shape, torch.float32)
         ops.image_grad(rec, self.t, g_rv, g_img, self.pf, self.c_img_rec)
         # input path: VGG(x') vs VGG(x0')
-        a = V.forward(self._vgg_input(x, "in.x"), ws, "")
+        a = V.forward(xin if xin is not None else self._vgg_input(x, "in.x"), ws, "")
         if loss is not None:
             self._loss_terms("x", loss, x, a)
         g_xv = V.backward(a, self.taps_o, self.c_vgg_x, ws, "x")
@@ -133,8 +140,10 @@ class AttackEngine:
         ops.mse_grad_f32(lat, self.lat_t, g_lat, self.c_lat_t)
         ops.mse_grad_f32(lat, self.lat_o, g_lat, self.c_lat_o, accumulate=True)
         G.backward(g_img, g_lat, ws)
-        g_enc = E.backward(g_lat, ws)
-        return g_xv, g_enc
+        if xin is not None:  # e4e: ∂L/∂x' joins the VGG input-path gradient (same x')
+            E.backward_nhwc(g_lat, ws, g_xv, accumulate=True)
+            return g_xv, None
+        return g_xv, E.backward(g_lat, ws)
 
     def step(self, x, a, e):
         g_xv, g_enc = self.gradient(x)
@@ -153,12 +162,12 @@ class AttackEngine:
     def objective(self, x, out):
         """Per-image objective at x into out (fp32 [N], +=): forward passes only."""
         ws, G, V, E = self.ws, self.G, self.V, self.E
-        lat = E.forward(x, ws)
+        lat, xin = self._encode(x, "in.x")
         rec = G.forward(lat, ws)
         self._loss_terms("lat", out, lat)
         a = V.forward(self._vgg_input(rec, "in.rec"), ws, "")
         self._loss_terms("rec", out, rec, a)
-        a = V.forward(self._vgg_input(x, "in.x"), ws, "")
+        a = V.forward(xin if xin is not None else self._vgg_input(x, "in.x"), ws, "")
         self._loss_terms("x", out, x, a)
         return out
 
@@ -332,7 +341,10 @@ def fgsm(net, imgs, eps, **kw):
     return attack(net, imgs, eps, 1, alpha=eps, random_start=False, **kw)
 
 
-def algorithmic_flops_per_image_step(synth, vgg):
-    """G fwd ×3 (fwd, dgrad, style-grad) + VGG ×4 (two calls, fwd + dgrad)."""
-    return 3 * synth.flops_fwd_per_image + 4 * vgg.flops_fwd_per_image
+def algorithmic_flops_per_image_step(synth, vgg, encoder=None):
+    """G fwd ×3 (fwd, dgrad, style-grad) + VGG ×4 (two calls, fwd + dgrad)
+    + the e4e encoder ×2 (fwd + input gradient) when it is the real one (the linear stand-in's
+    FLOPs are excluded, §8d)."""
+    enc = 2 * getattr(encoder, "flops_fwd_per_image", 0) if encoder is not None else 0
+    return 3 * synth.flops_fwd_per_image + 4 * vgg.flops_fwd_per_image + enc
 

@@ -14,8 +14,9 @@ Names follow the state-dict keys of the modules the reference calls:
   decoder with ``input_is_latent=True``, ``attack_main2.py:619``).
 * VGG16 trunk (``code/vgg.py:12-39``): positional list of 13 convs, loaded like
   ``VGGBase.load_pretrained_layers`` (``code/vgg.py:66-76``).
-* Encoder: a deterministic linear stand-in for e4e behind the ``net.encoder`` slot
-  (SURVEY.md §2 row 8, §7 step 1).
+* Encoder: e4e ``Encoder4Editing(50, 'ir_se')`` (``code/utils/model_utils.py:24``; state-dict keys
+  of that module: ``input_layer.*``, ``body.{i}.*``, ``styles.{i}.*``, ``latlayer{1,2}.*``), or the
+  deterministic linear stand-in of SURVEY.md §7 step 1 (``enc.*``).
 """
 import math
 
@@ -154,3 +155,77 @@ def make_encoder_weights(size, seed=0, start_from_latent_avg=True):
         "latent_avg": 0.1 * torch.randn(nl, STYLE_DIM, generator=g),
         "start_from_latent_avg": bool(start_from_latent_avg),
     }
+
+
+# ---- e4e: Encoder4Editing(50, 'ir_se') ------------------------------------------------------------
+E4E_STAGES = [(64, 64, 3), (64, 128, 4), (128, 256, 14), (256, 512, 3)]  # get_blocks(50)
+E4E_SE_REDUCTION = 16
+E4E_COARSE, E4E_MIDDLE = 3, 7  # Encoder4Editing.coarse_ind / middle_ind
+
+
+def e4e_units():
+    """bottleneck_IR_SE units of the IR-SE50 body in order: (in_channel, depth, stride)
+    (get_block: the first unit of a stage has stride 2, the others 1)."""
+    units = []
+    for cin, depth, n in E4E_STAGES:
+        units.append((cin, depth, 2))
+        units += [(depth, depth, 1)] * (n - 1)
+    return units
+
+
+def e4e_style_spatial(i):
+    """GradualStyleBlock spatial size of style i: 16 (coarse, from c3), 32 (middle, from p2) or 64
+    (fine, from p1)."""
+    return 16 if i < E4E_COARSE else (32 if i < E4E_MIDDLE else 64)
+
+
+def make_e4e_weights(size, seed=0, start_from_latent_avg=True):
+    """Seeded Encoder4Editing(50, 'ir_se') state dict (eval-mode BatchNorm running statistics
+    included) for a generator of output size ``size`` (style_count = n_latent). Scales keep the
+    24-unit residual stack O(1): He-normal convs, BatchNorm γ of the residual branch ≈ 0.3,
+    PReLU slopes ≈ 0.25 (PyTorch's init; kept > 0)."""
+    g = torch.Generator().manual_seed(int(seed))
+    p = {}
+
+    def bn(prefix, c, gamma=1.0):
+        p[prefix + ".weight"] = gamma * (1.0 + 0.1 * torch.randn(c, generator=g))
+        p[prefix + ".bias"] = 0.1 * torch.randn(c, generator=g)
+        p[prefix + ".running_mean"] = 0.1 * torch.randn(c, generator=g)
+        p[prefix + ".running_var"] = 0.5 + torch.rand(c, generator=g)
+
+    def conv(name, cout, cin, k, gain=2.0):
+        p[name] = torch.randn(cout, cin, k, k, generator=g) * math.sqrt(gain / (cin * k * k))
+
+    def prelu(name, c):
+        p[name] = (0.25 + 0.05 * torch.randn(c, generator=g)).clamp_min(0.05)
+
+    conv("input_layer.0.weight", 64, 3, 3)
+    bn("input_layer.1", 64)
+    prelu("input_layer.2.weight", 64)
+    for i, (cin, depth, stride) in enumerate(e4e_units()):
+        pre = f"body.{i}"
+        if cin != depth:
+            conv(pre + ".shortcut_layer.0.weight", depth, cin, 1, gain=1.0)
+            bn(pre + ".shortcut_layer.1", depth)
+        bn(pre + ".res_layer.0", cin)
+        conv(pre + ".res_layer.1.weight", depth, cin, 3)
+        prelu(pre + ".res_layer.2.weight", depth)
+        conv(pre + ".res_layer.3.weight", depth, depth, 3)
+        bn(pre + ".res_layer.4", depth, gamma=0.3)
+        cr = depth // E4E_SE_REDUCTION
+        conv(pre + ".res_layer.5.fc1.weight", cr, depth, 1, gain=1.0)
+        conv(pre + ".res_layer.5.fc2.weight", depth, cr, 1, gain=1.0)
+    for i in range(n_latent_for(size)):
+        sp = e4e_style_spatial(i)
+        for j in range(int(math.log2(sp))):
+            conv(f"styles.{i}.convs.{2 * j}.weight", STYLE_DIM, STYLE_DIM, 3)
+            p[f"styles.{i}.convs.{2 * j}.bias"] = 0.05 * torch.randn(STYLE_DIM, generator=g)
+        p[f"styles.{i}.linear.weight"] = torch.randn(STYLE_DIM, STYLE_DIM, generator=g)
+        p[f"styles.{i}.linear.bias"] = 0.1 * torch.randn(STYLE_DIM, generator=g)
+    for name, cin in (("latlayer1", 256), ("latlayer2", 128)):
+        conv(name + ".weight", STYLE_DIM, cin, 1, gain=1.0)
+        p[name + ".bias"] = 0.05 * torch.randn(STYLE_DIM, generator=g)
+    p["latent_avg"] = 0.1 * torch.randn(n_latent_for(size), STYLE_DIM, generator=g)
+    p["start_from_latent_avg"] = bool(start_from_latent_avg)
+    p["kind"] = "e4e"
+    return p

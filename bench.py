@@ -5,7 +5,8 @@ all-gather when N>1) over this rank's batch of 128 synthetic 256² image pairs (
 batch 1024 over 8 GPUs = 128 per GPU; weak scaling). Inputs are resident in HBM before the timed
 region. Rank 0 prints ONE JSON line.
 
-    python bench.py [--gpus N --steps K --warmup W --batch B --dtype fp16|bf16|fp32]
+    python bench.py [--gpus N --steps K --warmup W --batch B --dtype fp16|bf16|fp32
+                     --encoder e4e|linear]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
@@ -23,11 +24,12 @@ sys.path.insert(0, ROOT)
 import gfa_import  # noqa: E402,F401
 from gfa_amd import ops, pgd  # noqa: E402
 from gfa_amd.dist import gather_shards  # noqa: E402
+from gfa_amd.e4e import E4EEncoder  # noqa: E402
 from gfa_amd.encoder import SyntheticEncoder  # noqa: E402
 from gfa_amd.stylegan2 import SynthesisNet  # noqa: E402
 from gfa_amd.vgg import VGGNet  # noqa: E402
-from gfa_amd.weights import (make_encoder_weights, make_generator_weights,  # noqa: E402
-                             make_vgg_weights)
+from gfa_amd.weights import (make_e4e_weights, make_encoder_weights,  # noqa: E402
+                             make_generator_weights, make_vgg_weights)
 
 METRIC = "attacked images/sec, PGD-20 L∞ ε=8/255 at 256², 1/2/4/8 MI355X"  # BASELINE.json
 DT = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
@@ -48,10 +50,17 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-steps", type=int, default=10)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--encoder", default="linear", choices=["e4e", "linear"],
+                    help="e4e = Encoder4Editing(50,'ir_se') (the reference's net.encoder); linear = "
+                         "the SURVEY.md §7 stand-in")
     return ap.parse_args()
 
 
-def cpu_baseline(size, pgd_steps, sample_steps):
+def encoder_weights(kind, size):
+    return make_e4e_weights(size, seed=1) if kind == "e4e" else make_encoder_weights(size, seed=1)
+
+
+def cpu_baseline(size, pgd_steps, sample_steps, encoder):
     """The oracle (CPU restatement, fp32, all host cores) on a bounded sample: one 256² image,
     `sample_steps` PGD iterations, extrapolated to a PGD-`pgd_steps` attack."""
     from oracle import attack_ref, vgg_ref
@@ -60,7 +69,7 @@ def cpu_baseline(size, pgd_steps, sample_steps):
     cores = max(1, min(cores, len(os.sched_getaffinity(0))))
     torch.set_num_threads(cores)
     gp = make_generator_weights(size, seed=0)
-    ep = make_encoder_weights(size, seed=1)
+    ep = encoder_weights(encoder, size)
     vp = vgg_ref.load_positional(make_vgg_weights(1234))
     g = torch.Generator().manual_seed(123)
     x0 = torch.rand(1, 3, size, size, generator=g) * 2 - 1
@@ -80,14 +89,16 @@ def cpu_baseline(size, pgd_steps, sample_steps):
                       f"torch.set_num_threads({cores})"}
 
 
-def pmc_traffic(dtype, batch, size, pgd_steps):
+def pmc_traffic(dtype, batch, size, pgd_steps, encoder="linear"):
     """HBM bytes per conv_kernel launch from the newest committed PMC profile of this exact
     workload (profiles/rNN_bench_<dtype>_b<batch>.json, written by profiles/summarize_rocprof.py
     from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench; FETCH_SIZE ×2 per the
     gfx950 correction). PMC counters cannot be read from inside the timed process, hence a file."""
     if size != 256 or pgd_steps != 20:
         return None, None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_bench_{dtype}_b{batch}.json")))
+    suffix = "_e4e" if encoder == "e4e" else ""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles",
+                                          f"r*_bench_{dtype}_b{batch}{suffix}.json")))
     for f in reversed(files):
         with open(f) as fh:
             d = json.load(fh)
@@ -112,9 +123,11 @@ def main():
     T = DT[args.dtype]
     S, B = args.size, args.batch
     gp = make_generator_weights(S, seed=0)
-    ep = make_encoder_weights(S, seed=1)
+    ep = encoder_weights(args.encoder, S)
     vs = make_vgg_weights(1234)
-    eng = pgd.AttackEngine(SyntheticEncoder(ep, S, device=dev),
+    enc = (E4EEncoder(ep, S, dtype=T, device=dev) if args.encoder == "e4e"
+           else SyntheticEncoder(ep, S, device=dev))
+    eng = pgd.AttackEngine(enc,
                            SynthesisNet(gp, S, dtype=T, device=dev),
                            VGGNet(vs, dtype=T, device=dev))
     g = torch.Generator().manual_seed(1000 + rank)
@@ -152,7 +165,7 @@ def main():
         elapsed = tt.item()
     ms = elapsed / args.steps * 1e3
     value = n_total * args.steps / elapsed
-    flops_img_step = pgd.algorithmic_flops_per_image_step(eng.G, eng.V)
+    flops_img_step = pgd.algorithmic_flops_per_image_step(eng.G, eng.V, eng.E)
     out = {
         "metric": METRIC if (S, args.pgd_steps) == (256, 20) else
                   f"attacked images/sec, PGD-{args.pgd_steps} L∞ ε=8/255 at {S}², "
@@ -161,11 +174,13 @@ def main():
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": DT_NAME[args.dtype],
         "data": f"synthetic: seeded U(-1,1) image/target pairs, seeded random-init StyleGAN2 "
-                f"({S}², cm=2), VGG16 trunk and linear encoder (no checkpoints offline)",
+                f"({S}², cm=2), VGG16 trunk and "
+                + ("e4e Encoder4Editing(50,'ir_se')" if args.encoder == "e4e"
+                   else "linear stand-in encoder") + " (no checkpoints offline)",
         "config": {"workload": f"PGD-{args.pgd_steps} L∞ eps=8/255 alpha=2/255 at {S}², "
                                f"{B} images/GPU (BASELINE config #4 per-GPU share), "
                                f"RCCL all-gather of outputs when N>1",
-                   "images_per_gpu": B, "global_batch": n_total, "size": S,
+                   "encoder": args.encoder, "images_per_gpu": B, "global_batch": n_total, "size": S,
                    "pgd_steps": args.pgd_steps, "parallelism": f"dp{world}",
                    "algorithmic_gflop_per_image_step": flops_img_step / 1e9,
                    "effective_tflops": flops_img_step * B * args.pgd_steps * world
@@ -179,18 +194,21 @@ def main():
         n = len(prof)
         ach = tot_fl / (tot_ms * 1e-3) / 1e12
         peak = PEAK_TFLOPS[args.dtype]
-        traffic, src = pmc_traffic(args.dtype, B, S, args.pgd_steps)
+        traffic, src = pmc_traffic(args.dtype, B, S, args.pgd_steps, args.encoder)
         out["roofline"] = {
             "kernel": "3x3 conv: every conv API call of the step (mia::conv_halo_kernel, "
                       "mia::upconv_halo_kernel + its edge launch, mia::conv_kernel, "
-                      "mia::conv_thin_*: StyledConv fwd, up-conv, dgrads, VGG fwd/dgrad)",
+                      "mia::conv_thin_*: StyledConv fwd, up-conv, dgrads, VGG fwd/dgrad"
+                      + (", e4e convs and their input gradients)" if args.encoder == "e4e"
+                         else ")"),
             "bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
             "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": src,
             "launches": n, "avg_launch_us": tot_ms / n * 1e3,
             "algorithmic_gflop_per_launch": tot_fl / n / 1e9,
             "share_of_step_time": tot_ms / (elapsed * 1e3)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(S, args.pgd_steps, args.cpu_sample_steps)
+        out["cpu_baseline"] = cpu_baseline(S, args.pgd_steps, args.cpu_sample_steps,
+                                           args.encoder)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

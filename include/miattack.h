@@ -36,6 +36,7 @@ extern "C" {
 #define MIA_ACT_NONE 0
 #define MIA_ACT_RELU 1
 #define MIA_ACT_LRELU_S2 2 /* leaky_relu(v, 0.2) * sqrt(2)  (FusedLeakyReLU) */
+#define MIA_ACT_PRELU 3    /* v > 0 ? v : act_slope[co]·v  (PReLU / LeakyReLU; conv act_out only) */
 
 int mia_version(void);
 const char* mia_last_error_string(void);
@@ -88,9 +89,37 @@ typedef struct mia_conv_args {
   float bab_noise_w;
   const float* bab_bias;  /* [Cout] or NULL */
   float* bab_q;           /* [N][Cout] fp32, accumulated with atomics */
+  /* encoder (IR-SE50 / e4e) epilogue features, applied in the order of the list above:
+   *   mask_slope: the mask step becomes v = mask_a > 0 ? v : mask_slope[co]·v (PReLU backward)
+   *   act_slope:  per-channel slope of act_out = MIA_ACT_PRELU
+   *   csum:       csum[n][co] += Σ_p y (the stored value; SE average pool) */
+  const float* mask_slope; /* [Cout] or NULL (→ 0: ReLU mask) */
+  const float* act_slope;  /* [Cout], required by MIA_ACT_PRELU */
+  float* csum;             /* [N][Cout] fp32, accumulated with atomics, or NULL */
 } mia_conv_args;
 
 int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream);
+
+/*
+ * General form of the same implicit-GEMM conv: 1..4 problems ("groups") over one input x
+ * (args->H × args->W) that share the epilogue, each with its own weights [Cout][Kpad]
+ * (K = kh·kw·Cin tap-major, Kpad = mia_conv2d_kpad(kh·kw, Cin, dtype)), tap window, padding and
+ * output placement: group output (y, x) ∈ [0,ho)×[0,wo) reads input
+ * (stride·y + ty − pad_y, stride·x + tx − pad_x) and lands at (ay·y + by, ax·x + bx) of the
+ * (N, out_h, out_w, y_cstride) output. Aux operands (mask_a, tap_*, aux_x) are indexed at the
+ * placed output pixel with channel stride Cout. args->w and args->Kpad are ignored.
+ * Replaces the encoder's strided convolutions and their input gradients (e4e / IR-SE50,
+ * un-vendored Encoder4Editing behind net.encoder, code/utils/model_utils.py:24,
+ * code/attack/attack_main2.py:597,622): stride-2 3×3 (bottleneck conv2, GradualStyleBlock),
+ * 1×1 stride-1/2 (FPN lateral, shortcut), and the 4-phase sub-pixel adjoint of a stride-2 conv.
+ */
+typedef struct mia_conv_group {
+  const void* w;
+  int kh, kw, pad_y, pad_x, ho, wo, ay, by, ax, bx;
+} mia_conv_group;
+int mia_conv2d_kpad(int taps, int cin, int dtype);
+int mia_conv2d(const mia_conv_args* args, int stride, const mia_conv_group* groups, int ngroups,
+               int out_h, int out_w, int dtype, void* stream);
 
 /* ---- named entry points (thin wrappers over mia_conv3x3) ------------------------------- */
 /* ModulatedConv2d + NoiseInjection + FusedLeakyReLU bias, forward [ext]
@@ -294,6 +323,44 @@ int mia_truncate(const float* w, const float* mean, float psi, float* out, int r
                  void* stream);
 /* dst[i*bytes .. ] = src for i < count (broadcast the constant input over the batch). */
 int mia_repeat(const void* src, void* dst, int64_t bytes, int count, void* stream);
+
+/* ---- e4e encoder (Encoder4Editing(50, 'ir_se'), un-vendored; code/utils/model_utils.py:24) --
+ * NHWC dtype feature maps, fp32 per-(n,c) vectors. Eval-mode BatchNorm is a per-channel affine
+ * y = x·g + b folded on the host. SEModule(C, 16) of bottleneck_IR_SE:
+ *   mia_se_fwd:  avg = csum/hw; u = relu(W1·avg) (N,C/16); s = sigmoid(W2·u) (N,C)
+ *                W1 [C/16][C], W2 [C][C/16] fp32.
+ *   mia_se_apply: out = r·s[n][c] + sc  (sc: NHWC (N, H·ss, W·ss, C) read at (ss·y, ss·x), ss = 1
+ *                 or 2 = MaxPool2d(1, 2) shortcut; NULL → none; s NULL → 1); xb = out·g[c] + b[c]
+ *                 (the next unit's BatchNorm, optional); out may be NULL when only xb is wanted.
+ *   mia_chan_dot: gs[n][c] (+)= Σ_p a·b  (fp32 out)
+ *   mia_se_bwd:  from gs = ∂L/∂s: gz = gs·s(1−s); gu = (W2ᵀ gz)·[u > 0]; gavg = W1ᵀ gu / hw
+ *   mia_se_grad_scale: g_r = gamma[c]·(g_out·s[n][c] + gavg[n][c])  (gamma NULL → 1)
+ *   mia_prelu_bwd_scale: g = g_a·(a > 0 ? 1 : slope[c])·gamma[c]  (gamma NULL → 1)
+ *   mia_cast: y = scale·x converted between dtypes (x, y: flat, n elements)
+ *   mia_subsample_add: gx[n][2y][2x][c] += g[n][y][x][c]   (MaxPool2d(1,2) adjoint)
+ *   mia_bilinear_fwd/bwd: F.interpolate(mode='bilinear', align_corners=True) (N,Hi,Wi,C) →
+ *                 (N,Ho,Wo,C) and its adjoint (gather form, no atomics); accumulate adds to out. */
+int mia_se_fwd(const float* csum, const float* w1, const float* w2, float* u, float* s, int N,
+               int C, int Cr, float inv_hw, void* stream);
+int mia_se_apply(const void* r, const float* s, const void* sc, int ss, void* out,
+                 const float* g, const float* b, void* xb, int N, int H, int W, int C, int dtype,
+                 void* stream);
+int mia_chan_dot(const void* a, const void* b, float* gs, int N, int HW, int C, int accumulate,
+                 int dtype, void* stream);
+int mia_se_bwd(const float* gs, const float* s, const float* u, const float* w1, const float* w2,
+               float* gavg, int N, int C, int Cr, float inv_hw, void* stream);
+int mia_se_grad_scale(const void* g_out, const float* s, const float* gavg, const float* gamma,
+                      void* g_r, int N, int HW, int C, int dtype, void* stream);
+int mia_prelu_bwd_scale(const void* g_a, const void* a, const float* slope, const float* gamma,
+                        void* g, int64_t pixels, int C, int dtype, void* stream);
+int mia_subsample_add(const void* g, void* gx, int N, int H, int W, int C, int dtype,
+                      void* stream);
+int mia_cast(const void* x, int xdtype, void* y, int ydtype, int64_t n, float scale,
+             void* stream);
+int mia_bilinear_fwd(const void* x, void* y, int N, int Hi, int Wi, int Ho, int Wo, int C,
+                     int accumulate, int dtype, void* stream);
+int mia_bilinear_bwd(const void* gy, void* gx, int N, int Hi, int Wi, int Ho, int Wo, int C,
+                     int accumulate, int dtype, void* stream);
 int mia_memset(void* dst, int value, int64_t bytes, void* stream);
 
 #ifdef __cplusplus

@@ -37,8 +37,8 @@ class Refs:
             self.x0, self.t = x0, t
             self.x0p = F.avg_pool2d(x0, pf) if pf > 1 else x0
             self.tp = F.avg_pool2d(t, pf) if pf > 1 else t
-            self.lat_t = encoder_ref.encode(ep, self.tp)
-            self.lat_o = encoder_ref.encode(ep, self.x0p)
+            self.lat_t = encoder_ref.apply(ep, self.tp, size)
+            self.lat_o = encoder_ref.apply(ep, self.x0p, size)
             self.taps_t = vgg_ref.vgg_forward(vp, self.tp)
             self.taps_o = vgg_ref.vgg_forward(vp, self.x0p)
 
@@ -46,7 +46,7 @@ class Refs:
 def objective(gp, vp, ep, x, refs, size, weights=LOSS_WEIGHTS, per_image=False):
     pf = max(1, size // 256)
     xp = F.avg_pool2d(x, pf) if pf > 1 else x
-    lat = encoder_ref.encode(ep, xp)
+    lat = encoder_ref.apply(ep, xp, size)
     rec = stylegan2_ref.synthesis(gp, lat, size)
     recp = F.avg_pool2d(rec, pf) if pf > 1 else rec
     taps_rec = vgg_ref.vgg_forward(vp, recp)

@@ -1,0 +1,279 @@
+"""e4e encoder (Encoder4Editing(50, 'ir_se')) on the GPU: the new kernels
+against fp64 torch references of the same op, the whole encoder (forward and input gradient)
+against the CPU oracle (oracle/encoder_ref.py, parity unpinned: the module is un-vendored), and
+the attack gradient with the e4e encoder against autograd through the oracle objective."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from gfa_amd import e4e, layouts, ops, pgd
+from gfa_amd.vgg import CPAD, VGGNet
+from gfa_amd.weights import make_e4e_weights, make_generator_weights, make_vgg_weights
+from gfa_amd.workspace import Workspace
+from oracle import attack_ref, encoder_ref, vgg_ref
+
+pytestmark = pytest.mark.gpu
+
+TOL = {torch.float32: 2e-5, torch.float16: 2e-2}
+
+
+def rel_err(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def rnd(shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(shape, generator=g, dtype=torch.float64) * scale
+
+
+def nhwc(t, dtype, dev):
+    return t.permute(0, 2, 3, 1).contiguous().to(dtype).to(dev)
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).double().cpu()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("H,cin,cout", [(16, 64, 128), (32, 128, 64), (2, 512, 512), (8, 64, 64)])
+def test_conv2d_stride2_fwd_and_phase_dgrad(cuda, dtype, H, cin, cout):
+    """Stride-2 3×3 conv (bias + LeakyReLU epilogue) and its 4-phase sub-pixel input gradient with
+    the slope mask of the layer below, vs F.conv2d and autograd."""
+    N = 2
+    x = rnd((N, cin, H, H), 1)
+    w = rnd((cout, cin, 3, 3), 2, math.sqrt(2 / (9 * cin)))
+    b = rnd((cout,), 3, 0.1)
+    ho = (H - 1) // 2 + 1
+    slope = torch.full((cout,), 0.01, device=cuda)
+    y = torch.empty(N, ho, ho, cout, dtype=dtype, device=cuda)
+    ops.conv2d(nhwc(x, dtype, cuda), [dict(w=layouts.fwd_matrix(w, dtype).to(cuda), kh=3, kw=3,
+                                           pad=(1, 1), ho=ho, wo=ho)],
+               y, (ho, ho), cout=cout, stride=2, bias=b.float().to(cuda),
+               act_out=ops.ACT_PRELU, act_slope=slope)
+    ref = F.leaky_relu(F.conv2d(x, w, b, stride=2, padding=1), 0.01)
+    assert rel_err(nchw(y), ref) < TOL[dtype]
+    # adjoint, masked by a stored activation of the layer below (slope 0.25)
+    g = rnd((N, cout, ho, ho), 4)
+    a_below = rnd((N, cin, H, H), 5)
+    sl = torch.full((cin,), 0.25, device=cuda)
+    gx = torch.empty(N, H, H, cin, dtype=dtype, device=cuda)
+    groups = e4e._phase_groups([(m.to(cuda), py, px) for m, py, px in
+                                layouts.s2_dgrad_phases(w, dtype)], H)
+    ops.conv2d(nhwc(g, dtype, cuda), groups, gx, (H, H), cout=cin,
+               mask_a=nhwc(a_below, dtype, cuda), mask_slope=sl)
+    xx = x.clone().requires_grad_(True)
+    (gref,) = torch.autograd.grad(F.conv2d(xx, w, stride=2, padding=1), xx, g)
+    gref = torch.where(a_below.to(dtype).double() > 0, gref, 0.25 * gref)
+    assert rel_err(nchw(gx), gref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_conv2d_1x1_stride2_and_placed_adjoint(cuda, dtype):
+    N, H, cin, cout = 2, 32, 64, 128
+    x = rnd((N, cin, H, H), 6)
+    w = rnd((cout, cin, 1, 1), 7, 0.1)
+    b = rnd((cout,), 8, 0.1)
+    ho = H // 2
+    y = torch.empty(N, ho, ho, cout, dtype=dtype, device=cuda)
+    ops.conv2d(nhwc(x, dtype, cuda), [dict(w=layouts.conv1x1_matrix(w, dtype).to(cuda), kh=1,
+                                           kw=1, ho=ho, wo=ho)],
+               y, (ho, ho), cout=cout, stride=2, bias=b.float().to(cuda))
+    assert rel_err(nchw(y), F.conv2d(x, w, b, stride=2)) < TOL[dtype]
+    g = rnd((N, cout, ho, ho), 9)
+    base = rnd((N, cin, H, H), 10)
+    gx = nhwc(base, dtype, cuda)
+    ops.conv2d(nhwc(g, dtype, cuda), [dict(w=layouts.conv1x1_matrix(w.reshape(cout, cin).t(), dtype)
+                                           .to(cuda), kh=1, kw=1, ho=ho, wo=ho, a=(2, 2))],
+               gx, (H, H), cout=cin, accumulate=True)
+    xx = x.clone().requires_grad_(True)
+    (gref,) = torch.autograd.grad(F.conv2d(xx, w, stride=2), xx, g)
+    assert rel_err(nchw(gx), gref + base.to(dtype).double()) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("H,cin,cout", [(32, 128, 128), (16, 64, 64)])
+def test_conv_prelu_epilogue_and_channel_sum(cuda, dtype, H, cin, cout):
+    """Stride-1 3×3 (halo kernel at Cout = 128, generic at 64) with a per-channel PReLU epilogue
+    and the Σ_p channel sum (SE average pool)."""
+    N = 3
+    x = rnd((N, cin, H, H), 11)
+    w = rnd((cout, cin, 3, 3), 12, math.sqrt(2 / (9 * cin)))
+    b = rnd((cout,), 13, 0.1)
+    slope = rnd((cout,), 14, 0.05).abs() + 0.1
+    y = torch.empty(N, H, H, cout, dtype=dtype, device=cuda)
+    cs = torch.zeros(N, cout, device=cuda)
+    ops.conv2d(nhwc(x, dtype, cuda), [dict(w=layouts.fwd_matrix(w, dtype).to(cuda), kh=3, kw=3,
+                                           pad=(1, 1), ho=H, wo=H)],
+               y, (H, H), cout=cout, bias=b.float().to(cuda), act_out=ops.ACT_PRELU,
+               act_slope=slope.float().to(cuda), csum=cs)
+    ref = F.prelu(F.conv2d(x, w, b, padding=1), slope)
+    assert rel_err(nchw(y), ref) < TOL[dtype]
+    assert rel_err(cs, ref.sum(dim=(2, 3))) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_se_kernels_vs_autograd(cuda, dtype):
+    N, H, C = 3, 16, 256
+    Cr = C // 16
+    r = rnd((N, C, H, H), 20)
+    sc = rnd((N, C, 2 * H, 2 * H), 21)
+    w1 = rnd((Cr, C), 22, 1 / math.sqrt(C))
+    w2 = rnd((C, Cr), 23, 1 / math.sqrt(Cr))
+    gnext, bnext = rnd((C,), 24, 0.1) + 1, rnd((C,), 25, 0.1)
+    rd, scd = nhwc(r, dtype, cuda), nhwc(sc, dtype, cuda)
+    r64, sc64 = rd.double().cpu().permute(0, 3, 1, 2), scd.double().cpu().permute(0, 3, 1, 2)
+    cs = r64.sum(dim=(2, 3)).float().to(cuda)
+    u = torch.empty(N, Cr, device=cuda)
+    s = torch.empty(N, C, device=cuda)
+    ops.se_fwd(cs, w1.float().to(cuda), w2.float().to(cuda), u, s, H * H)
+    rr = r64.clone().requires_grad_(True)
+    s_ref = torch.sigmoid(F.relu(rr.mean(dim=(2, 3)) @ w1.t()) @ w2.t())
+    assert rel_err(s, s_ref) < 1e-5
+    out = torch.empty_like(rd)
+    xb = torch.empty_like(rd)
+    ops.se_apply(rd, s, scd, 2, out, gnext.float().to(cuda), bnext.float().to(cuda), xb)
+    out_ref = r64 * s.double().cpu()[:, :, None, None] + sc64[:, :, ::2, ::2]
+    assert rel_err(nchw(out), out_ref) < TOL[dtype]
+    assert rel_err(nchw(xb), out_ref * gnext[None, :, None, None] + bnext[None, :, None, None]) \
+        < TOL[dtype]
+    # backward of out = r·SE(r) w.r.t. r, through chan_dot / se_bwd / se_grad_scale
+    go = rnd((N, C, H, H), 26)
+    god = nhwc(go, dtype, cuda)
+    go64 = god.double().cpu().permute(0, 3, 1, 2)
+    (gref,) = torch.autograd.grad(rr * s_ref[:, :, None, None], rr, go64)
+    gs = ops.chan_dot(god, rd, torch.empty(N, C, device=cuda))
+    assert rel_err(gs, (go64 * r64).sum(dim=(2, 3))) < 1e-5
+    gavg = ops.se_bwd(gs, s, u, w1.float().to(cuda), w2.float().to(cuda),
+                      torch.empty(N, C, device=cuda), H * H)
+    gr = ops.se_grad_scale(god, s, gavg, torch.empty_like(rd))
+    assert rel_err(nchw(gr), gref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("hi,ho", [(16, 32), (32, 64), (4, 9)])
+def test_bilinear_align_corners_fwd_bwd(cuda, dtype, hi, ho):
+    N, C = 2, 64
+    x = rnd((N, C, hi, hi), 30)
+    base = rnd((N, C, ho, ho), 31)
+    y = nhwc(base, dtype, cuda)
+    ops.bilinear_fwd(nhwc(x, dtype, cuda), y, accumulate=True)
+    xx = x.clone().requires_grad_(True)
+    up = F.interpolate(xx, size=(ho, ho), mode="bilinear", align_corners=True)
+    assert rel_err(nchw(y), up.detach() + base) < TOL[dtype]
+    g = rnd((N, C, ho, ho), 32)
+    (gref,) = torch.autograd.grad(up, xx, g)
+    gx = torch.empty(N, hi, hi, C, dtype=dtype, device=cuda)
+    ops.bilinear_bwd(nhwc(g, dtype, cuda), gx)
+    assert rel_err(nchw(gx), gref) < TOL[dtype]
+
+
+def test_prelu_bwd_subsample_cast(cuda):
+    N, H, C = 2, 8, 64
+    ga, a = rnd((N, H, H, C), 40), rnd((N, H, H, C), 41)
+    slope = rnd((C,), 42, 0.1).abs() + 0.05
+    gamma = rnd((C,), 43, 0.1) + 1
+    out = torch.empty(N, H, H, C, device=cuda)
+    ops.prelu_bwd_scale(ga.float().to(cuda), a.float().to(cuda), slope.float().to(cuda), out,
+                        gamma.float().to(cuda))
+    assert rel_err(out, torch.where(a > 0, ga, slope * ga) * gamma) < 1e-6
+    g = rnd((N, H, H, C), 44)
+    gx0 = rnd((N, 2 * H, 2 * H, C), 45)
+    gx = gx0.float().to(cuda)
+    ops.subsample_add(g.float().to(cuda), gx)
+    want = gx0.clone()
+    want[:, ::2, ::2] += g
+    assert rel_err(gx, want) < 1e-6
+    h = torch.empty(N, H, H, C, dtype=torch.float16, device=cuda)
+    ops.cast(g.float().to(cuda), h, 2.0)
+    assert rel_err(h, 2 * g) < 1e-3
+
+
+def _e4e_setup(dtype, cuda, N=2, R=256, seed=3):
+    p = make_e4e_weights(256, seed=seed)
+    enc = e4e.E4EEncoder(p, 256, dtype=dtype, device=cuda)
+    x = rnd((N, 3, R, R), 50).clamp(-1, 1) * 0.9
+    xin = torch.zeros(N, R, R, CPAD, dtype=dtype, device=cuda)
+    xin[..., :3] = x.permute(0, 2, 3, 1).to(dtype).to(cuda)
+    p64 = {k: (v.double() if torch.is_tensor(v) else v) for k, v in p.items()}
+    return enc, xin, xin[..., :3].permute(0, 3, 1, 2).double().cpu(), p64
+
+
+def _grad_close(got, ref, nrm_tol, agree_tol):
+    """The encoder's LeakyReLU(0.01) / PReLU masks make ∇x' non-smooth: a 1e-6 relative change of
+    a feature map flips a few near-zero masks deep in a style head (1×1…4² maps, each spanning the
+    whole receptive field) and moves ∇x' by ~1e-3 in norm — the fp64 oracle itself, re-evaluated
+    at our fp32 features, differs from itself by 1.5e-3. So the full gradient is compared in norm
+    and in sign; exactness is checked mask-for-mask by test_e4e_style_head_gradient_exact."""
+    nrm = ((got - ref).norm() / ref.norm()).item()
+    big = ref.abs() > 1e-2 * ref.abs().max()
+    agree = (torch.sign(got[big]) == torch.sign(ref[big])).float().mean().item()
+    assert nrm < nrm_tol and agree > agree_tol, (nrm, agree)
+
+
+@pytest.mark.parametrize("dtype,tol,gtol,agree", [(torch.float32, 1e-4, 3e-2, 0.995),
+                                                  (torch.float16, 3e-2, 0.25, 0.95)])
+def test_e4e_forward_and_input_gradient_vs_oracle(cuda, dtype, tol, gtol, agree):
+    enc, xin, x64, p64 = _e4e_setup(dtype, cuda)
+    ws = Workspace(cuda)
+    lat = enc.forward_nhwc(xin, ws)
+    xx = x64.clone().requires_grad_(True)
+    ref = encoder_ref.e4e_encode(p64, xx, 14)
+    assert tuple(lat.shape) == (2, 14, 512)
+    assert rel_err(lat, ref) < tol
+    gl = rnd((2, 14, 512), 51)
+    (gref,) = torch.autograd.grad(ref, xx, gl)
+    gx = torch.zeros_like(xin)
+    enc.backward_nhwc(gl.float().to(cuda), ws, gx, accumulate=True)
+    got = nchw(gx[..., :3].contiguous())
+    assert torch.isfinite(got).all()
+    _grad_close(got, gref, gtol, agree)
+    assert gx[..., 3:].abs().max().item() == 0.0
+    assert enc.flops_fwd_per_image > 100e9
+
+
+def test_e4e_style_head_gradient_exact(cuda):
+    """Teacher-forced: a style head's backward (EqualLinear, 6 stride-2 convs with LeakyReLU
+    masks, accumulation into ∂p1) vs autograd through the oracle head evaluated at OUR p1, for a
+    latent gradient on one row (fp32: no mask flips at this size, so exact to fp32 rounding)."""
+    enc, xin, _, p64 = _e4e_setup(torch.float32, cuda)
+    ws = Workspace(cuda)
+    enc.forward_nhwc(xin, ws)
+    p1 = nchw(enc._feats["p1"]).requires_grad_(True)
+    for i in (7, 13):
+        out = encoder_ref.gradual_style_block(p64, f"styles.{i}", p1, 64)
+        gl = torch.zeros(2, 14, 512, dtype=torch.float64)
+        gl[:, i] = rnd((2, 512), 60 + i)
+        (gref,) = torch.autograd.grad(out, p1, gl[:, i])
+        enc.debug = {}
+        enc.backward_nhwc(gl.float().to(cuda), ws, torch.zeros_like(xin))
+        got = nchw(enc.debug["heads.p1"])
+        enc.debug = None
+        assert ((got - gref).norm() / gref.norm()).item() < 1e-4
+
+
+def test_attack_gradient_with_e4e_vs_oracle(cuda):
+    """∇_x L of the full objective with the real encoder architecture (fp32, 256², one image)."""
+    size = 256
+    gp = make_generator_weights(size, seed=0)
+    ep = make_e4e_weights(size, seed=1)
+    vs = make_vgg_weights(1234)
+    from gfa_amd.stylegan2 import SynthesisNet
+    eng = pgd.AttackEngine(e4e.E4EEncoder(ep, size, dtype=torch.float32, device=cuda),
+                           SynthesisNet(gp, size, dtype=torch.float32, device=cuda),
+                           VGGNet(vs, dtype=torch.float32, device=cuda))
+    g = torch.Generator().manual_seed(7)
+    x0 = torch.rand(1, 3, size, size, generator=g) * 2 - 1
+    t = torch.rand(1, 3, size, size, generator=g) * 2 - 1
+    x = (x0 + 0.03 * (torch.rand(x0.shape, generator=g) * 2 - 1)).clamp(-1, 1)
+    eng.prepare(x0.to(cuda), t.to(cuda))
+    gd = eng.full_gradient(x.to(cuda)).cpu().double()
+    gp64 = {k: v.double() for k, v in gp.items()}
+    vp64 = {k: (w.double(), b.double()) for k, (w, b) in vgg_ref.load_positional(vs).items()}
+    ep64 = {k: (v.double() if torch.is_tensor(v) else v) for k, v in ep.items()}
+    refs = attack_ref.Refs(gp64, vp64, ep64, x0.double(), t.double(), size)
+    L, gr = attack_ref.loss_grad(gp64, vp64, ep64, x.double(), refs, size)
+    _grad_close(gd, gr, 3e-2, 0.995)  # mask-flip sensitivity: see _grad_close
+    assert rel_err(eng.loss(x.to(cuda)).double(), L) < 1e-4

@@ -81,6 +81,7 @@ def test_library_exports_every_header_symbol():
 
 
 @pytest.mark.parametrize("cname,pyname", [("mia_conv_args", "ConvArgs"),
+                                          ("mia_conv_group", "ConvGroup"),
                                           ("mia_gemm_seg", "GemmSeg"),
                                           ("mia_gemm_group", "GemmGroup")])
 def test_abi_struct_layout_matches_c(tmp_path, cname, pyname):
@@ -184,3 +185,50 @@ def test_upconv_subpixel_matrices_equal_conv_transpose():
     md = layouts.upconv_dgrad_matrix(W, torch.float64)
     cols = F.unfold(gT, 3, stride=2).view(2, cout, 9, R * R).transpose(1, 2).reshape(2, 9 * cout, -1)
     assert torch.allclose((md[:, :9 * cout] @ cols).view(2, cin, R, R), gx, atol=1e-12)
+
+
+def _emulate_conv2d(x, groups, out_hw, cout, stride=1):
+    """CPU restatement of mia_conv2d's group semantics (include/miattack.h) on NHWC fp64."""
+    N, H, W, Cin = x.shape
+    y = torch.zeros(N, out_hw[0], out_hw[1], cout, dtype=torch.float64)
+    for g in groups:
+        kh, kw = g["kh"], g["kw"]
+        py, px = g.get("pad", (0, 0))
+        ay, ax = g.get("a", (1, 1))
+        by, bx = g.get("b", (0, 0))
+        wm = g["w"].double()[:, :kh * kw * Cin].reshape(cout, kh, kw, Cin)
+        for i in range(g["ho"]):
+            for j in range(g["wo"]):
+                acc = torch.zeros(N, cout, dtype=torch.float64)
+                for ty in range(kh):
+                    for tx in range(kw):
+                        yy, xx = stride * i + ty - py, stride * j + tx - px
+                        if 0 <= yy < H and 0 <= xx < W:
+                            acc += x[:, yy, xx, :] @ wm[:, ty, tx, :].t()
+                y[:, ay * i + by, ax * j + bx, :] = acc
+    return y
+
+
+@pytest.mark.parametrize("H", [8, 7, 2, 1])
+def test_stride2_dgrad_phase_layout_is_the_adjoint(H):
+    """layouts.s2_dgrad_phases + e4e._phase_groups (the 4-phase sub-pixel input gradient of a
+    stride-2, pad-1 3×3 conv) equal autograd of F.conv2d, by a CPU emulation of the kernel's
+    group semantics — including odd sizes and the 2→1 / 1→1 tail of a GradualStyleBlock."""
+    import torch.nn.functional as F
+    from gfa_amd import e4e, layouts
+    g = torch.Generator().manual_seed(0)
+    cin, cout = 3, 5
+    w = torch.randn(cout, cin, 3, 3, generator=g, dtype=torch.float64)
+    x = torch.randn(2, cin, H, H, generator=g, dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(x, w, stride=2, padding=1)
+    gy = torch.randn(y.shape, generator=g, dtype=torch.float64)
+    (gx,) = torch.autograd.grad(y, x, gy)
+    groups = e4e._phase_groups(layouts.s2_dgrad_phases(w, torch.float32), H)
+    got = _emulate_conv2d(gy.permute(0, 2, 3, 1), groups, (H, H), cin)
+    assert torch.allclose(got.permute(0, 3, 1, 2), gx, atol=1e-5)
+    # the forward through the same emulation (fwd_matrix layout, stride 2)
+    ho = (H - 1) // 2 + 1
+    fwd = _emulate_conv2d(x.detach().permute(0, 2, 3, 1),
+                          [dict(w=layouts.fwd_matrix(w, torch.float64), kh=3, kw=3, pad=(1, 1),
+                                ho=ho, wo=ho)], (ho, ho), cout, stride=2)
+    assert torch.allclose(fwd.permute(0, 3, 1, 2), y.detach(), atol=1e-10)

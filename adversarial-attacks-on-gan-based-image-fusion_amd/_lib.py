@@ -122,6 +122,8 @@ SIGNATURES = {
     "mia_conv2d_kpad": (c_int, [c_int, c_int, c_int]),
     "mia_conv2d": (c_int, [ctypes.POINTER(ConvArgs), c_int, ctypes.POINTER(ConvGroup), c_int,
                            c_int, c_int, c_int, P]),
+    "mia_conv_s2_dgrad_halo": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, c_int,
+                                       P]),
     "mia_se_fwd": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
     "mia_se_apply": (c_int, [P, P, P, c_int, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_chan_dot": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P]),

@@ -22,6 +22,13 @@
 //     epilogue exchanges fragment pairs (v_permlane16_swap) for 16-byte stores into T.
 // The phase positions on the last row / column of T's phase grids (y = R or x = R; they exist for
 // the even phases only) go to the generic kernel as four one-row / one-column groups.
+//
+// DG (input-gradient mode): the same kernel computes the input gradient of a stride-2, pad-1 3×3
+// conv (the e4e encoder's strided convs): gin[2i] = g[i]·W[1], gin[2i+1] = g[i]·W[2] + g[i+1]·W[0]
+// per axis — the transposed conv mirrored: offsets (0, +1) instead of (0, −1), output phase
+// 1 − p, weights flipped (layouts.s2_dgrad_halo_matrix). Every output row 2i + q of an input
+// patch lies inside the output, so no edge launch; the epilogue applies the slope mask of the
+// layer below (PReLU / LeakyReLU backward) and optionally accumulates.
 #include "conv_common.h"
 
 namespace mia {
@@ -51,12 +58,14 @@ __device__ __forceinline__ constexpr int up_phase(int st, int slot) {
 struct UpK {
   const void* x;
   const void* w;  // packed [Cin/64][5][2][Cout][64]
-  void* t;        // (N, 2R+1, 2R+1, Cout)
+  void* t;        // (N, 2R+1, 2R+1, Cout); DG: (N, 2R, 2R, Cout)
   const float* style;
-  int N, R, Cin, Cout, act_in, nbn, nblk;
+  const void* mask_a;       // DG: (N, 2R, 2R, Cout) or NULL
+  const float* mask_slope;  // DG: [Cout] or NULL (→ 0)
+  int N, R, Cin, Cout, act_in, nbn, nblk, accumulate;
 };
 
-template <typename T, bool PRO>
+template <typename T, bool PRO, bool DG>
 __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
   typedef HaloUp TL;
   typedef typename Vec<T>::type VT;
@@ -102,7 +111,7 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
     } else {
       const int hr = (hw + HWAVES * j) * 8 + (lane >> 3);
       const int hy = hr / HSIDE, hx = hr - (hr / HSIDE) * HSIDE;
-      const int y = y0 + hy - 1, x = x0 + hx - 1;
+      const int y = y0 + hy - (DG ? 0 : 1), x = x0 + hx - (DG ? 0 : 1);
       if (hr < HROWS && y >= 0 && y < R && x >= 0 && x < R)
         src[j] = X + ((size_t)(n * R + y) * R + x) * Cin + ((lane & 7) ^ fsw(hr)) * VEC;
     }
@@ -165,7 +174,8 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
         VT af[FM];
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
-          const int hr = (wm * FM + i + 1 - jy) * HSIDE + frow + 1 - jx;
+          const int hr = DG ? (wm * FM + i + jy) * HSIDE + frow + jx
+                            : (wm * FM + i + 1 - jy) * HSIDE + frow + 1 - jx;
           af[i] = *(const VT*)(ha + hr * ROWB + ((ch ^ fsw(hr)) << 4));
         }
         if constexpr (PRO) {
@@ -210,14 +220,21 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
 
   // ---- epilogue: phase (py, px) of input position (y, x) → T(2y+py, 2x+px) ----------------------
   T* __restrict__ Y = (T*)k.t;
-  const int TS = 2 * R + 1, lrow = lane >> 4;
+  const int TS = DG ? 2 * R : 2 * R + 1, lrow = lane >> 4;
   typedef T t2 __attribute__((ext_vector_type(2)));
+  float msl[8];
+  if constexpr (DG) {
+    const int c = n0 + wn * FN * 16 + 16 * (lrow & 1) + 8 * (lrow >> 1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) msl[e] = k.mask_slope ? k.mask_slope[c + e] : 0.f;
+  }
 #pragma unroll
   for (int ph = 0; ph < 4; ++ph) {
     const int py = ph >> 1, px = ph & 1;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const int ty = 2 * (y0 + wm * FM + i) + py, tx = 2 * (x0 + frow) + px;
+      const int ty = 2 * (y0 + wm * FM + i) + (DG ? 1 - py : py);
+      const int tx = 2 * (x0 + frow) + (DG ? 1 - px : px);
       unsigned a[2], b[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -231,12 +248,36 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
       }
       // lane row lrow now holds channels [16·(lrow & 1) + 8·(lrow >> 1), +8) of the wave's 32
       const int c = n0 + wn * FN * 16 + 16 * (lrow & 1) + 8 * (lrow >> 1);
-      *(uint4*)(Y + ((size_t)(n * TS + ty) * TS + tx) * Cout + c) = make_uint4(a[0], a[1], b[0], b[1]);
+      const size_t off = ((size_t)(n * TS + ty) * TS + tx) * Cout + c;
+      if constexpr (DG) {
+        if (k.mask_a || k.accumulate) {  // 8 channels of this lane: mask, accumulate, repack
+          typedef typename Vec<T>::type VT8;
+          VT8 v = __builtin_bit_cast(VT8, make_uint4(a[0], a[1], b[0], b[1]));
+          float f[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) f[e] = (float)v[e];
+          if (k.mask_a) {
+            const VT8 m = *(const VT8*)((const T*)k.mask_a + off);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = (float)m[e] > 0.f ? f[e] : msl[e] * f[e];
+          }
+          if (k.accumulate) {
+            const VT8 o = *(const VT8*)(Y + off);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] += (float)o[e];
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = (T)f[e];
+          *(VT8*)(Y + off) = v;
+          continue;
+        }
+      }
+      *(uint4*)(Y + off) = make_uint4(a[0], a[1], b[0], b[1]);
     }
   }
 }
 
-template <typename T, bool PRO>
+template <typename T, bool PRO, bool DG = false>
 static int launch_upconv_halo(UpK& k, hipStream_t st) {
   typedef HaloUp TL;
   k.nbn = k.Cout / TL::BN;
@@ -244,7 +285,7 @@ static int launch_upconv_halo(UpK& k, hipStream_t st) {
   size_t lds = 2 * (size_t)TL::HBUF + (size_t)TL::STAGES * TL::BSTAGE;
   if (PRO) lds += (size_t)k.Cin * sizeof(T);
   if (lds > 160 * 1024) return set_error("upconv_halo: LDS budget exceeded");
-  auto fn = upconv_halo_kernel<T, PRO>;
+  auto fn = upconv_halo_kernel<T, PRO, DG>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -271,10 +312,44 @@ int launch_upconv_halo(const void* x, const void* w_up, void* t, int N, int R, i
   const bool pro = style != nullptr || act_in != MIA_ACT_NONE;
   MIA_DISPATCH_DTYPE(dtype, T, {
     if constexpr (sizeof(T) == 2) {
-      return pro ? launch_upconv_halo<T, true>(k, st) : launch_upconv_halo<T, false>(k, st);
+      return pro ? launch_upconv_halo<T, true, false>(k, st)
+                 : launch_upconv_halo<T, false, false>(k, st);
     }
   });
   return set_error("upconv_halo: 2-byte types only");
 }
 
+bool s2_dgrad_halo_eligible(int dtype, int R, int Cg, int Cx) {
+  const char* e = getenv("MIA_S2DG_HALO");  // tuning / A-B switch: 0 = generic phase GEMMs
+  if (e && atoi(e) == 0) return false;
+  return dtype != MIA_F32 && R % 16 == 0 && Cg % 64 == 0 && Cx % HaloUp::BN == 0 &&
+         (int64_t)4 * R * R < (1LL << 31);
+}
+
+int launch_s2_dgrad_halo(const void* g, const void* w, void* gx, int N, int R, int Cg, int Cx,
+                         const void* mask_a, const float* mask_slope, int accumulate, int dtype,
+                         hipStream_t st) {
+  UpK k = {};
+  k.x = g; k.w = w; k.t = gx; k.mask_a = mask_a; k.mask_slope = mask_slope;
+  k.N = N; k.R = R; k.Cin = Cg; k.Cout = Cx; k.accumulate = accumulate;
+  MIA_DISPATCH_DTYPE(dtype, T, {
+    if constexpr (sizeof(T) == 2) return launch_upconv_halo<T, false, true>(k, st);
+  });
+  return set_error("s2_dgrad_halo: 2-byte types only");
+}
+
 }  // namespace mia
+
+using namespace mia;
+
+extern "C" int mia_conv_s2_dgrad_halo(const void* g, const void* w_halo, void* gx, int N, int R,
+                                      int Cg, int Cx, const void* mask_a, const float* mask_slope,
+                                      int accumulate, int dtype, void* stream) {
+  MIA_CHECK_ARG(g && w_halo && gx && N > 0, "bad args");
+  MIA_CHECK_ARG(s2_dgrad_halo_eligible(dtype, R, Cg, Cx),
+                "needs fp16/bf16, R % 16 == 0, Cg % 64 == 0, Cx % 64 == 0 "
+                "(use mia_conv2d phase groups otherwise)");
+  MIA_CHECK_ARG((int64_t)N * R * R * Cg < (1LL << 31), "input too large for 32-bit offsets");
+  return launch_s2_dgrad_halo(g, w_halo, gx, N, R, Cg, Cx, mask_a, mask_slope, accumulate, dtype,
+                              (hipStream_t)stream);
+}

@@ -116,6 +116,8 @@ class E4EEncoder:
                 U["w2d"] = mt(layouts.dgrad_matrix(w2, T))
             else:
                 U["w2d"] = [(mt(m), py, px) for m, py, px in layouts.s2_dgrad_phases(w2, T)]
+                U["w2dh"] = mt(layouts.s2_dgrad_halo_matrix(w2, T)) if T != torch.float32 \
+                    else None
             U["se_w1"] = dd(p[pre + ".res_layer.5.fc1.weight"].reshape(U["cr"], depth))
             U["se_w2"] = dd(p[pre + ".res_layer.5.fc2.weight"].reshape(depth, U["cr"]))
             if cin != depth:
@@ -140,13 +142,18 @@ class E4EEncoder:
         for i in range(self.n_latent):
             sp = e4e_style_spatial(i)
             convs = []
+            src = "c3" if i < E4E_COARSE else ("p2" if i < E4E_MIDDLE else "p1")
+            h = self.R // {"c3": 16, "p2": 8, "p1": 4}[src]  # head input resolution
             for j in range(int(math.log2(sp))):
                 w = p[f"styles.{i}.convs.{2 * j}.weight"].double()
+                ho = _s2_out(h)
+                halo = ops.s2_dgrad_halo_ok(T, ho, STYLE_DIM, STYLE_DIM) and 2 * ho == h
                 convs.append(dict(w=mt(layouts.fwd_matrix(w, T)),
                                   wd=[(mt(m), py, px) for m, py, px in
                                       layouts.s2_dgrad_phases(w, T)],
+                                  wdh=mt(layouts.s2_dgrad_halo_matrix(w, T)) if halo else None,
                                   b=dd(p[f"styles.{i}.convs.{2 * j}.bias"])))
-            src = "c3" if i < E4E_COARSE else ("p2" if i < E4E_MIDDLE else "p1")
+                h = ho
             self.heads.append(dict(convs=convs, src=src,
                                    lw=dd(p[f"styles.{i}.linear.weight"].double() * inv),
                                    lb=dd(p[f"styles.{i}.linear.bias"])))
@@ -287,6 +294,19 @@ class E4EEncoder:
         self._plans[key] = plan
         return plan
 
+    @staticmethod
+    def _s2_dgrad(g, phases, w_halo, y, mask, slope, accumulate):
+        """Input gradient of a stride-2 3×3 conv into y: one halo-tiled launch where it applies
+        (fp16/bf16, g side a multiple of 16, y exactly twice g), else the 4 phase GEMMs."""
+        R, h = g.shape[1], y.shape[1]
+        if w_halo is not None and h == 2 * R and ops.s2_dgrad_halo_ok(g.dtype, R, g.shape[-1],
+                                                                      y.shape[-1]):
+            ops.s2_dgrad_halo(g, w_halo, y, mask_a=mask, mask_slope=slope if mask is not None
+                              else None, accumulate=accumulate)
+        else:
+            ops.conv2d(g, _phase_groups(phases, h), y, (h, h), cout=y.shape[-1], mask_a=mask,
+                       mask_slope=slope if mask is not None else None, accumulate=accumulate)
+
     # ------------------------------------------------------------------------------------------
     def backward_nhwc(self, g_lat, ws, g_xin, accumulate=True):
         """Adds (or writes) ∂L/∂x' for ∂L/∂lat = g_lat (N, n_latent, 512) fp32 into g_xin."""
@@ -310,13 +330,12 @@ class E4EEncoder:
                 cv = hd["convs"][j]
                 if j > 0:
                     y = self._buf(ws, f"ghh{i}_{j - 1}", acts[j - 1].shape)
-                    ops.conv2d(g, _phase_groups(cv["wd"], y.shape[1]), y, y.shape[1:3], cout=D,
-                               mask_a=acts[j - 1], mask_slope=self.slope001)
+                    mask, acc = acts[j - 1], False
                 else:
                     y = gfeat[hd["src"]]
-                    ops.conv2d(g, _phase_groups(cv["wd"], y.shape[1]), y, y.shape[1:3], cout=D,
-                               accumulate=hd["src"] in seen)
+                    mask, acc = None, hd["src"] in seen
                     seen.add(hd["src"])
+                self._s2_dgrad(g, cv["wd"], cv["wdh"], y, mask, self.slope001, acc)
                 g = y
         dbg = getattr(self, "debug", None)  # tests: dict to receive intermediate gradients
         if dbg is not None:
@@ -344,8 +363,11 @@ class E4EEncoder:
                               self._buf(ws, "gavg", (N, d), f32), u["_hw"])
             g_r = ops.se_grad_scale(Gc, u["_s"], gavg, self._buf(ws, f"g_r{d}", Gc.shape))
             gp1 = self._buf(ws, f"gp1_{h}_{d}", (N, h, h, d))
-            groups = ([_g3(u["w2d"], h)] if s == 1 else _phase_groups(u["w2d"], h))
-            ops.conv2d(g_r, groups, gp1, (h, h), cout=d, mask_a=u["_a1"], mask_slope=u["slope"])
+            if s == 1:
+                ops.conv2d(g_r, [_g3(u["w2d"], h)], gp1, (h, h), cout=d, mask_a=u["_a1"],
+                           mask_slope=u["slope"])
+            else:
+                self._s2_dgrad(g_r, u["w2d"], u["w2dh"], gp1, u["_a1"], u["slope"], False)
             if cin == d and s == 1:  # identity shortcut: ∂x = γ1·dgrad + ∂out, in place
                 tgt, acc = Gc, True
             elif i == 0:

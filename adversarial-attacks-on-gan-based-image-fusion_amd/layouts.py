@@ -157,3 +157,11 @@ def conv1x1_matrix(w, dtype):
     full = torch.zeros(cout, (cin + bk - 1) // bk * bk, dtype=torch.float64)
     full[:, :cin] = w
     return full.to(dtype)
+
+
+def s2_dgrad_halo_matrix(w, dtype):
+    """Packed weights of mia_conv_s2_dgrad_halo for the forward stride-2 conv w (Cout, Cin, 3, 3):
+    the halo up-conv layout of the channel-transposed, spatially flipped kernel (the input
+    gradient is the transposed conv mirrored: offsets +j, output phase 1 − p, kernel index
+    2 − (p + 2j)). (Cout/64, 5, 2, Cin, 64)."""
+    return upconv_halo_matrix(w.double().transpose(0, 1).flip(2, 3), dtype)

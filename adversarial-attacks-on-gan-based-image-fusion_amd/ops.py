@@ -777,3 +777,31 @@ def cast(x, y, scale=1.0):
         raise ValueError("cast: size mismatch")
     call("mia_cast", ptr(x), dt(x), ptr(y), dt(y), x.numel(), float(scale), stream())
     return y
+
+
+def s2_dgrad_halo(g, w_halo, gx, mask_a=None, mask_slope=None, accumulate=False, flops=None):
+    """mia_conv_s2_dgrad_halo: gx (N,2R,2R,Cx) ← input gradient of a stride-2 3×3 conv from
+    g (N,R,R,Cg) (+ slope mask, + accumulate)."""
+    N, R, R2, Cg = g.shape
+    Cx = gx.shape[-1]
+    T = g.dtype
+    if R != R2:
+        raise ValueError("square inputs only")
+    _need(w_halo, (Cg // 64, 5, 2, Cx, 64), T, "w_halo")
+    _need(gx, (N, 2 * R, 2 * R, Cx), T, "gx")
+    if mask_a is not None:
+        _need(mask_a, gx.shape, T, "mask_a")
+    _numel_ok(mask_slope, Cx, torch.float32, "mask_slope")
+    _prof_call("mia_conv_s2_dgrad_halo",
+               flops if flops is not None else 2 * N * R * R * 9 * Cg * Cx,
+               ptr(g), ptr(w_halo), ptr(gx), N, R, Cg, Cx, ptr(mask_a), ptr(mask_slope),
+               int(bool(accumulate)), dt(T), stream())
+    return gx
+
+
+def s2_dgrad_halo_ok(dtype, R, Cg, Cx):
+    """Host mirror of s2_dgrad_halo_eligible (csrc/conv_upconv.hip)."""
+    import os
+    if os.environ.get("MIA_S2DG_HALO") == "0":
+        return False
+    return dtype != torch.float32 and R % 16 == 0 and Cg % 64 == 0 and Cx % 64 == 0

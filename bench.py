@@ -2,8 +2,9 @@
 
 One "step" = one complete PGD-20 attack (target precompute + 20 iterations + the final RCCL
 all-gather when N>1) over this rank's batch of 128 synthetic 256² image pairs (BASELINE config #4:
-batch 1024 over 8 GPUs = 128 per GPU; weak scaling). Inputs are resident in HBM before the timed
-region. Rank 0 prints ONE JSON line.
+batch 1024 over 8 GPUs = 128 per GPU; weak scaling) through the reference's networks: the e4e
+encoder (IR-SE50 Encoder4Editing), the StyleGAN2 synthesis and the VGG16 trunk, random-init.
+Inputs are resident in HBM before the timed region. Rank 0 prints ONE JSON line.
 
     python bench.py [--gpus N --steps K --warmup W --batch B --dtype fp16|bf16|fp32
                      --encoder e4e|linear]
@@ -50,9 +51,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-steps", type=int, default=10)
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--encoder", default="linear", choices=["e4e", "linear"],
-                    help="e4e = Encoder4Editing(50,'ir_se') (the reference's net.encoder); linear = "
-                         "the SURVEY.md §7 stand-in")
+    ap.add_argument("--encoder", default="e4e", choices=["e4e", "linear"],
+                    help="e4e = Encoder4Editing(50,'ir_se'), the reference's net.encoder "
+                         "(code/utils/model_utils.py:24; default); linear = the SURVEY.md §7 "
+                         "stand-in (rounds before the e4e encoder existed)")
     return ap.parse_args()
 
 

@@ -113,6 +113,15 @@ int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream);
  * code/attack/attack_main2.py:597,622): stride-2 3×3 (bottleneck conv2, GradualStyleBlock),
  * 1×1 stride-1/2 (FPN lateral, shortcut), and the 4-phase sub-pixel adjoint of a stride-2 conv.
  */
+/* Input gradient of a stride-2, pad-1 3×3 conv as ONE halo-tiled launch (the halo up-conv kernel
+ * mirrored; fp16/bf16, R % 16 == 0, Cg % 64 == 0, Cx % 64 == 0): g (N,R,R,Cg) → gx (N,2R,2R,Cx),
+ * gx = mask(Σ ...) (+ gx if accumulate), mask as mia_conv_args.mask_a / mask_slope.
+ * w_halo = layouts.s2_dgrad_halo_matrix(W): [Cg/64][5][2][Cx][64]. Replaces the same e4e strided
+ * conv backward as the mia_conv2d phase groups (bottleneck conv2, GradualStyleBlock convs). */
+int mia_conv_s2_dgrad_halo(const void* g, const void* w_halo, void* gx, int N, int R, int Cg,
+                           int Cx, const void* mask_a, const float* mask_slope, int accumulate,
+                           int dtype, void* stream);
+
 typedef struct mia_conv_group {
   const void* w;
   int kh, kw, pad_y, pad_x, ho, wo, ay, by, ax, bx;

@@ -70,6 +70,33 @@ def test_conv2d_stride2_fwd_and_phase_dgrad(cuda, dtype, H, cin, cout):
     assert rel_err(nchw(gx), gref) < TOL[dtype]
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("R,cg,cx", [(16, 64, 64), (32, 512, 512), (16, 128, 256)])
+def test_s2_dgrad_halo_vs_autograd(cuda, dtype, R, cg, cx):
+    """The halo up-conv kernel in input-gradient mode (mia_conv_s2_dgrad_halo): stride-2 conv
+    adjoint with the slope mask and accumulate, vs autograd, and vs the 4-phase GEMM path."""
+    N = 2
+    w = rnd((cg, cx, 3, 3), 70, math.sqrt(2 / (9 * cx)))  # forward conv: cx → cg, stride 2
+    g = rnd((N, cg, R, R), 71)
+    a_below = rnd((N, cx, 2 * R, 2 * R), 72)
+    base = rnd((N, cx, 2 * R, 2 * R), 73)
+    sl = torch.full((cx,), 0.25, device=cuda)
+    gx = nhwc(base, dtype, cuda)
+    ops.s2_dgrad_halo(nhwc(g, dtype, cuda), layouts.s2_dgrad_halo_matrix(w, dtype).to(cuda), gx,
+                      mask_a=nhwc(a_below, dtype, cuda), mask_slope=sl, accumulate=True)
+    xx = torch.zeros(N, cx, 2 * R, 2 * R, dtype=torch.float64, requires_grad=True)
+    (gref,) = torch.autograd.grad(F.conv2d(xx, w, stride=2, padding=1), xx, g)
+    gref = torch.where(a_below.to(dtype).double() > 0, gref, 0.25 * gref) + base.to(dtype).double()
+    tol = 2e-2 if dtype == torch.float16 else 1e-1
+    assert rel_err(nchw(gx), gref) < tol
+    gx2 = nhwc(base, dtype, cuda)
+    groups = e4e._phase_groups([(m.to(cuda), py, px) for m, py, px in
+                                layouts.s2_dgrad_phases(w, dtype)], 2 * R)
+    ops.conv2d(nhwc(g, dtype, cuda), groups, gx2, (2 * R, 2 * R), cout=cx,
+               mask_a=nhwc(a_below, dtype, cuda), mask_slope=sl, accumulate=True)
+    assert rel_err(gx, gx2) < tol / 4
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 def test_conv2d_1x1_stride2_and_placed_adjoint(cuda, dtype):
     N, H, cin, cout = 2, 32, 64, 128

@@ -232,3 +232,35 @@ def test_stride2_dgrad_phase_layout_is_the_adjoint(H):
                           [dict(w=layouts.fwd_matrix(w, torch.float64), kh=3, kw=3, pad=(1, 1),
                                 ho=ho, wo=ho)], (ho, ho), cout, stride=2)
     assert torch.allclose(fwd.permute(0, 3, 1, 2), y.detach(), atol=1e-10)
+
+
+@pytest.mark.parametrize("R", [2, 3])
+def test_s2_dgrad_halo_packing_is_the_adjoint(R):
+    """layouts.s2_dgrad_halo_matrix under the DG-mode semantics of the halo up-conv kernel
+    (offsets +j over the UPCONV_HALO_STEPS table, output phase 1 − p) equals autograd of a
+    stride-2 pad-1 conv — a CPU emulation of csrc/conv_upconv.hip's K-step loop."""
+    import torch.nn.functional as F
+    from gfa_amd import layouts
+    g0 = torch.Generator().manual_seed(1)
+    cin, cout, N = 64, 128, 2  # forward conv: cin → cout; the gradient runs cout (Cg) → cin (Cx)
+    w = torch.randn(cout, cin, 3, 3, generator=g0, dtype=torch.float64)
+    x = torch.randn(N, cin, 2 * R, 2 * R, generator=g0, dtype=torch.float64, requires_grad=True)
+    y = F.conv2d(x, w, stride=2, padding=1)
+    gy = torch.randn(y.shape, generator=g0, dtype=torch.float64)
+    (gx,) = torch.autograd.grad(y, x, gy)
+    pk = layouts.s2_dgrad_halo_matrix(w, torch.float64)  # (Cg/64, 5, 2, Cx, 64)
+    g = torch.zeros(N, R + 1, R + 1, cout, dtype=torch.float64)
+    g[:, :R, :R] = gy.permute(0, 2, 3, 1)
+    acc = torch.zeros(4, N, R, R, cin, dtype=torch.float64)
+    for st, ((jy, jx), phases) in enumerate(layouts.UPCONV_HALO_STEPS):
+        gs = g[:, jy:jy + R, jx:jx + R]
+        for slot, ph in enumerate(phases):
+            if ph is None:
+                continue
+            wm = pk[:, st, slot].permute(1, 0, 2).reshape(cin, cout)  # [Cx][Cg]
+            acc[ph] += gs @ wm.t()
+    out = torch.zeros(N, 2 * R, 2 * R, cin, dtype=torch.float64)
+    for ph in range(4):
+        py, px = ph >> 1, ph & 1
+        out[:, 1 - py::2, 1 - px::2] = acc[ph]
+    assert torch.allclose(out.permute(0, 3, 1, 2), gx, atol=1e-9)

@@ -6,11 +6,12 @@
 set -euo pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-ARGS="--steps 2 --warmup 1 --no-cpu-baseline"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace \
-  -o run -- python3 bench.py $ARGS > gpurun_out/prof_trace.log 2>&1
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch \
-  -o run -- python3 bench.py $ARGS > gpurun_out/prof_fetch.log 2>&1
-timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write \
-  -o run -- python3 bench.py $ARGS > gpurun_out/prof_write.log 2>&1
-find gpurun_out/prof_trace gpurun_out/prof_fetch gpurun_out/prof_write -name "*.csv" | head -20
+ARGS="--steps 2 --warmup 1 --no-cpu-baseline ${EXTRA:-}"  # EXTRA="--encoder e4e", TAG=_e4e
+T=${TAG:-}
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_trace$T \
+  -o run -- python3 bench.py $ARGS > gpurun_out/prof_trace$T.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/prof_fetch$T \
+  -o run -- python3 bench.py $ARGS > gpurun_out/prof_fetch$T.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/prof_write$T \
+  -o run -- python3 bench.py $ARGS > gpurun_out/prof_write$T.log 2>&1
+find gpurun_out/prof_trace$T gpurun_out/prof_fetch$T gpurun_out/prof_write$T -name "*.csv" | head -20

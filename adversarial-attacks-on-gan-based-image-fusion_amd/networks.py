@@ -201,3 +201,35 @@ def build_net(size=256, seed=0, dtype=torch.float32, device="cuda", vgg_seed=123
         net.vgg = VGGBase(vs, dtype=dtype, device=device)
         net.params["vgg"] = vs
     return net
+
+
+def psp_params_from_checkpoint(ckpt):
+    """Generator and e4e encoder parameter dicts from a pSp / e4e checkpoint (a path or an already
+    loaded dict), as ``utils/model_utils.py:7-35`` + pSp.load_weights split it: ``state_dict``
+    keys ``encoder.*`` / ``decoder.*``, ``latent_avg``, ``opts``. Loaded with
+    ``torch.load(weights_only=True)`` (nothing in the file is executed)."""
+    if not isinstance(ckpt, dict):
+        ckpt = torch.load(ckpt, map_location="cpu", weights_only=True)
+    sd = ckpt["state_dict"]
+    enc = {k[len("encoder."):]: v for k, v in sd.items() if k.startswith("encoder.")}
+    dec = {k[len("decoder."):]: v for k, v in sd.items() if k.startswith("decoder.")}
+    if not enc or not dec:
+        raise ValueError("checkpoint state_dict needs encoder.* and decoder.* keys")
+    opts = ckpt.get("opts", {}) or {}
+    enc["latent_avg"] = ckpt["latent_avg"].reshape(-1, STYLE_DIM).float()
+    enc["start_from_latent_avg"] = bool(opts.get("start_from_latent_avg", True))
+    enc["kind"] = "e4e"
+    return dec, enc, opts
+
+
+def build_net_from_checkpoint(ckpt, size=None, dtype=torch.float32, device="cuda", vgg=None):
+    """``setup_model(checkpoint_path)`` (utils/model_utils.py:7-18) on the device kernels: the
+    e4e encoder + StyleGAN2 decoder of one checkpoint (+ an optional VGG state dict)."""
+    dec, enc, opts = psp_params_from_checkpoint(ckpt)
+    size = int(size or opts.get("stylegan_size", 1024))
+    net = PSPNet(Encoder(enc, size, device=device, dtype=dtype),
+                 Decoder(dec, size, dtype=dtype, device=device),
+                 enc["latent_avg"].to(device), enc["start_from_latent_avg"])
+    if vgg is not None:
+        net.vgg = VGGBase(vgg, dtype=dtype, device=device)
+    return net

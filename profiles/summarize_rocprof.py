@@ -19,12 +19,16 @@ from collections import defaultdict
 # every kernel a conv API call of the attack launches (ops.conv3x3 / upconv_fwd / upconv_dgrad):
 # the implicit-GEMM tiles, the halo tiles, the halo up-conv and the thin-channel VGG input layer
 CONV = re.compile(r"conv_(halo_)?kernel|upconv_halo_kernel|conv_thin_(in|out)_kernel")
+# (e4e: mia_conv2d launches conv_kernel / conv_halo_kernel; mia_conv_s2_dgrad_halo launches the
+# up-conv halo kernel in DG mode)
 # mia_upconv_fwd_halo is ONE API call that launches TWO kernels (upconv_halo_kernel for the
 # interior + a generic conv_kernel for the last row / column), so the per-call average that
 # bench.py's HIP events measure divides by launches − upconv_halo launches
-PAIRED = re.compile(r"upconv_halo_kernel")
+# (only the up-conv form pairs: its input-gradient mode, template flag DG = 1, is one launch)
+PAIRED = re.compile(r"upconv_halo_kernelI\w+?Lb[01]ELb0E")
 # names of the bool template parameters of the elementwise kernels (csrc/pointwise.hip)
 KFLAGS = {"blur4_strip_kernel": ("fwd", "noise"), "torgb_bwd_kernel": ("front",),
+          "upconv_halo_kernel": ("pro", "dgrad"),
           "maxpool2_bwd_kernel": ("tap",)}
 
 
@@ -34,7 +38,7 @@ def short(name):
         base = re.sub(r"^\d+", "", m.group(1))
         tile = re.search(r"TileILi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)", name)
         halo = re.search(r"HaloTileILi(\d+)ELi(\d+)ELi(\d+)E", name)
-        flags = re.findall(r"ELb([01])", name)
+        flags = re.findall(r"(?:E|_)Lb([01])", name)
         extra = ""
         if halo:
             bn, ph, stg = map(int, halo.groups())

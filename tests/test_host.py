@@ -264,3 +264,24 @@ def test_s2_dgrad_halo_packing_is_the_adjoint(R):
         py, px = ph >> 1, ph & 1
         out[:, 1 - py::2, 1 - px::2] = acc[ph]
     assert torch.allclose(out.permute(0, 3, 1, 2), gx, atol=1e-9)
+
+
+def test_psp_checkpoint_split(tmp_path):
+    """A pSp/e4e checkpoint (state_dict with encoder.* / decoder.* keys, latent_avg, opts) saved
+    by torch.save loads with weights_only=True and splits into the generator and e4e dicts."""
+    from gfa_amd import networks
+    from gfa_amd.weights import make_e4e_weights, make_generator_weights
+    gp = make_generator_weights(32, seed=0)
+    ep = make_e4e_weights(32, seed=1)
+    sd = {f"decoder.{k}": v for k, v in gp.items()}
+    sd.update({f"encoder.{k}": v for k, v in ep.items() if torch.is_tensor(v) and k != "latent_avg"})
+    sd["encoder.input_layer.1.num_batches_tracked"] = torch.tensor(5)
+    path = tmp_path / "e4e_test.pt"
+    torch.save({"state_dict": sd, "latent_avg": ep["latent_avg"],
+                "opts": {"stylegan_size": 32, "start_from_latent_avg": True}}, path)
+    dec, enc, opts = networks.psp_params_from_checkpoint(str(path))
+    assert set(dec) == set(gp) and opts["stylegan_size"] == 32
+    assert enc["kind"] == "e4e" and torch.equal(enc["latent_avg"], ep["latent_avg"])
+    assert torch.equal(enc["body.3.shortcut_layer.0.weight"], ep["body.3.shortcut_layer.0.weight"])
+    with pytest.raises(ValueError):
+        networks.psp_params_from_checkpoint({"state_dict": {}, "latent_avg": ep["latent_avg"]})

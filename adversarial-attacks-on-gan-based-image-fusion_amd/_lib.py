@@ -113,6 +113,7 @@ SIGNATURES = {
     "mia_gemm_f32": (c_int, [c_int, c_int, c_int, c_float, P, c_int64, c_int64, P, c_int64,
                              c_int64, c_float, P, c_int64, c_int64, P, P]),
     "mia_gemm_f32_grouped": (c_int, [ctypes.POINTER(GemmGroup), c_int, P]),
+    "mia_sum_slices": (c_int, [P, P, c_int, c_int, c_int, P]),
     "mia_style_demod": (c_int, [P, P, P, c_int, c_int, c_int, c_float, P]),
     "mia_demod_bwd": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
     "mia_pixel_norm": (c_int, [P, P, c_int, c_int, c_float, P]),

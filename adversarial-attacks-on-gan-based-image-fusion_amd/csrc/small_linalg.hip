@@ -31,7 +31,7 @@ int check_launch(const char* what) {
 // share one W+ latent row in the style-affine backward). Every block owns one TM×TM tile of one
 // group; TM = 64 (4×4 per thread) or 32 (2×2 per thread) is picked on the host so that a launch
 // has enough blocks to cover the 256 CUs (the attack's GEMMs have M = batch ≤ 128).
-constexpr int GK = 16;
+constexpr int GK = 32;
 constexpr int kMaxGroups = 12;
 
 struct GemmSeg {
@@ -54,9 +54,13 @@ struct GemmBatch {
   GemmGroup g[kMaxGroups];
 };
 
+// The K loop is software-pipelined: the operand elements of K-step s+1 are loaded into
+// registers before the FMAs of step s, so each step waits on one LDS round trip, not on a
+// global-load latency (the style GEMMs have K = 512 … 1024 and only a few tiles per group).
 template <int TM>
 __global__ __launch_bounds__(256) void sgemm_grouped_kernel(const GemmBatch b) {
-  constexpr int R = TM / 16;  // per-thread micro-tile R×R
+  constexpr int R = TM / 16;         // per-thread micro-tile R×R
+  constexpr int EPT = GK * TM / 256;  // operand elements per thread per K-step
   __shared__ float As[GK][TM + 1];
   __shared__ float Bs[GK][TM + 1];
   int gi = 0;
@@ -68,38 +72,56 @@ __global__ __launch_bounds__(256) void sgemm_grouped_kernel(const GemmBatch b) {
   const int m0 = (t / G.ntn) * TM, n0 = (t % G.ntn) * TM;
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
   float acc[R][R] = {};
-#pragma unroll 1
-  for (int sgi = 0; sgi < G.nseg; ++sgi) {
-    const GemmSeg S = G.seg[sgi];
+  const int steps0 = (G.seg[0].K + GK - 1) / GK;
+  const int nsteps = steps0 + (G.nseg > 1 ? (G.seg[1].K + GK - 1) / GK : 0);
+  float ra[EPT], rb[EPT];
+  // consecutive threads walk the operand's contiguous dimension (coalesced loads)
+  auto load = [&](int s) {
+    const GemmSeg& S = s < steps0 ? G.seg[0] : G.seg[1];
+    const int k0 = (s < steps0 ? s : s - steps0) * GK;
     const bool a_kfast = S.sak == 1, b_kfast = S.sbk == 1;
-#pragma unroll 1
-    for (int k0 = 0; k0 < S.K; k0 += GK) {
-      // consecutive threads walk the operand's contiguous dimension (coalesced loads)
-      for (int i = threadIdx.x; i < GK * TM; i += 256) {
-        const int kk = a_kfast ? i % GK : i / TM, mm = a_kfast ? i / GK : i % TM;
-        const int gm = m0 + mm, gk = k0 + kk;
-        As[kk][mm] = (gm < G.M && gk < S.K) ? S.A[gm * S.sam + gk * S.sak] : 0.f;
-      }
-      for (int i = threadIdx.x; i < GK * TM; i += 256) {
-        const int kk = b_kfast ? i % GK : i / TM, nn = b_kfast ? i / GK : i % TM;
-        const int gn = n0 + nn, gk = k0 + kk;
-        Bs[kk][nn] = (gn < G.N && gk < S.K) ? S.B[gk * S.sbk + gn * S.sbn] : 0.f;
-      }
-      __syncthreads();
 #pragma unroll
-      for (int kk = 0; kk < GK; ++kk) {
-        float a[R], bb[R];
-#pragma unroll
-        for (int i = 0; i < R; ++i) a[i] = As[kk][ty * R + i];
-#pragma unroll
-        for (int j = 0; j < R; ++j) bb[j] = Bs[kk][tx * R + j];
-#pragma unroll
-        for (int i = 0; i < R; ++i)
-#pragma unroll
-          for (int j = 0; j < R; ++j) acc[i][j] += a[i] * bb[j];
-      }
-      __syncthreads();
+    for (int e = 0; e < EPT; ++e) {
+      const int i = threadIdx.x + e * 256;
+      int kk = a_kfast ? i % GK : i / TM, mm = a_kfast ? i / GK : i % TM;
+      int gm = m0 + mm, gk = k0 + kk;
+      ra[e] = (gm < G.M && gk < S.K) ? S.A[gm * S.sam + gk * S.sak] : 0.f;
+      kk = b_kfast ? i % GK : i / TM;
+      const int nn = b_kfast ? i / GK : i % TM;
+      const int gn = n0 + nn;
+      gk = k0 + kk;
+      rb[e] = (gn < G.N && gk < S.K) ? S.B[gk * S.sbk + gn * S.sbn] : 0.f;
     }
+  };
+  auto store = [&](int s) {
+    const GemmSeg& S = s < steps0 ? G.seg[0] : G.seg[1];
+    const bool a_kfast = S.sak == 1, b_kfast = S.sbk == 1;
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const int i = threadIdx.x + e * 256;
+      As[a_kfast ? i % GK : i / TM][a_kfast ? i / GK : i % TM] = ra[e];
+      Bs[b_kfast ? i % GK : i / TM][b_kfast ? i / GK : i % TM] = rb[e];
+    }
+  };
+  load(0);
+#pragma unroll 1
+  for (int s = 0; s < nsteps; ++s) {
+    store(s);
+    __syncthreads();
+    if (s + 1 < nsteps) load(s + 1);
+#pragma unroll
+    for (int kk = 0; kk < GK; ++kk) {
+      float a[R], bb[R];
+#pragma unroll
+      for (int i = 0; i < R; ++i) a[i] = As[kk][ty * R + i];
+#pragma unroll
+      for (int j = 0; j < R; ++j) bb[j] = Bs[kk][tx * R + j];
+#pragma unroll
+      for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int j = 0; j < R; ++j) acc[i][j] += a[i] * bb[j];
+    }
+    __syncthreads();
   }
 #pragma unroll
   for (int i = 0; i < R; ++i)
@@ -113,6 +135,19 @@ __global__ __launch_bounds__(256) void sgemm_grouped_kernel(const GemmBatch b) {
         G.C[gm * G.scm + gn * G.scn] = v;
       }
     }
+}
+
+// y[n][d] = Σ_s x[n][s][d]  (e4e: the latent gradient rows that all read style 0)
+__global__ __launch_bounds__(256) void sum_slices_kernel(const float* __restrict__ x, float* y,
+                                                         int S, int D, int64_t total) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t n = i / D;
+    const int d = (int)(i - n * D);
+    const float* p = x + n * S * D + d;
+    float a = 0.f;
+    for (int s = 0; s < S; ++s) a += p[(int64_t)s * D];
+    y[i] = a;
+  }
 }
 
 static int run_gemm_groups(const mia_gemm_group* groups, int ngroups, hipStream_t st) {
@@ -228,4 +263,13 @@ extern "C" int mia_demod_bwd(const float* q, const float* demod, const float* ws
   hipLaunchKernelGGL(demod_bwd_kernel, grid, dim3(256), Cout * sizeof(float), (hipStream_t)stream,
                      q, demod, wsq, s, gs, Cin, Cout, scale2);
   return check_launch("demod_bwd");
+}
+
+extern "C" int mia_sum_slices(const float* x, float* y, int N, int S, int D, void* stream) {
+  MIA_CHECK_ARG(x && y && N > 0 && S > 0 && D > 0, "bad args");
+  const int64_t total = (int64_t)N * D;
+  const int grid = (int)std::min<int64_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(sum_slices_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, y, S, D,
+                     total);
+  return check_launch("sum_slices");
 }

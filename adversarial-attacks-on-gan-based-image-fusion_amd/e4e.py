@@ -158,10 +158,9 @@ class E4EEncoder:
                                    lw=dd(p[f"styles.{i}.linear.weight"].double() * inv),
                                    lb=dd(p[f"styles.{i}.linear.bias"])))
         # w = w0 + delta_i: the linear biases of rows i ≥ 1 include style 0's; the backward of
-        # style 0 sums every row, i.e. one K = n_latent·512 product with its weight tiled
+        # style 0 reads the sum of every row (mia_sum_slices)
         b0l = self.heads[0]["lb"]
         self.lin_bias = [b0l] + [(h["lb"] + b0l).contiguous() for h in self.heads[1:]]
-        self.w0_tiled = self.heads[0]["lw"].repeat(self.n_latent, 1).contiguous()
         self.flops_fwd_per_image = self._count_flops()
         self._plans = {}
 
@@ -287,7 +286,8 @@ class E4EEncoder:
                 plan.add(lat[:, i, :], S * D, 1, N, D, segs, bias=self.lin_bias[i])
         else:  # ∂f_i = ∂lat[:, i]·W_i (i ≥ 1); ∂f_0 = Σ_i ∂lat[:, i]·W_0
             gf = [self._buf(ws, f"gf{i}", (N, D), f32) for i in range(S)]
-            plan.add(gf[0], D, 1, N, D, [(lat, S * D, 1, self.w0_tiled, D, 1, S * D)])
+            gsum = self._buf(ws, "gsum", (N, D), f32)  # Σ_i ∂lat[:, i] (backward_nhwc)
+            plan.add(gf[0], D, 1, N, D, [(gsum, D, 1, self.heads[0]["lw"], D, 1, D)])
             for i in range(1, S):
                 plan.add(gf[i], D, 1, N, D, [(lat[:, i, :], S * D, 1, self.heads[i]["lw"], D, 1,
                                               D)])
@@ -316,6 +316,7 @@ class E4EEncoder:
         f32 = torch.float32
         D = STYLE_DIM
         feats = self._feats
+        ops.sum_slices(g_lat, self._buf(ws, "gsum", (N, D), f32))
         self._plan(ws, N, "bwd", g_lat).run()
         gfeat = {k: self._buf(ws, "g" + k, feats[k].shape) for k in ("c3", "p2", "p1")}
         seen = set()

@@ -805,3 +805,13 @@ def s2_dgrad_halo_ok(dtype, R, Cg, Cx):
     if os.environ.get("MIA_S2DG_HALO") == "0":
         return False
     return dtype != torch.float32 and R % 16 == 0 and Cg % 64 == 0 and Cx % 64 == 0
+
+
+def sum_slices(x, y):
+    """y (N, D) = Σ_s x[:, s, :] for x (N, S, D) fp32."""
+    N, S, D = x.shape
+    _need(y, (N, D), torch.float32, "y")
+    if x.dtype != torch.float32:
+        raise ValueError("sum_slices: fp32 required")
+    call("mia_sum_slices", ptr(x), ptr(y), N, S, D, stream())
+    return y

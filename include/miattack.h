@@ -318,6 +318,9 @@ typedef struct mia_gemm_group {
   mia_gemm_seg seg[2];
 } mia_gemm_group;
 int mia_gemm_f32_grouped(const mia_gemm_group* groups, int ngroups, void* stream);
+/* y[n][d] = Σ_s x[n][s][d] (fp32): e4e's latent-gradient rows that all read style 0
+ * (Encoder4Editing: w[:, i] = style_0(c3) + delta_i, so ∂style_0 = Σ_i ∂w[:, i]). */
+int mia_sum_slices(const float* x, float* y, int N, int S, int D, void* stream);
 /* demod[n][co] = rsqrt(scale2·Σ_ci s[n][ci]²·wsq[co][ci] + 1e-8)  (ModulatedConv2d demod [ext]) */
 int mia_style_demod(const float* s, const float* wsq, float* demod, int N, int Cin, int Cout,
                     float scale2, void* stream);

@@ -438,6 +438,9 @@ int launch_conv_halo(ConvK& k, int dtype, hipStream_t st);
 bool upconv_halo_eligible(int dtype, int R, int Cin, int Cout);
 int launch_upconv_halo(const void* x, const void* w_up, void* t, int N, int R, int Cin, int Cout,
                        int act_in, const float* style, int dtype, hipStream_t st);
+// 64 → 64-channel stride-1 layers, weights resident in VGPRs, persistent (conv_wres.hip)
+bool conv_wres_eligible(const ConvK& k, int dtype);
+int launch_conv_wres(ConvK& k, int dtype, hipStream_t st);
 // thin-channel layers: VGG conv1_1 forward and its input gradient (conv_thin.hip)
 bool conv_thin_eligible(const ConvK& k, int dtype);
 int launch_conv_thin(ConvK& k, int dtype, hipStream_t st);

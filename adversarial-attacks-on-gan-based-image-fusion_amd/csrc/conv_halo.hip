@@ -22,6 +22,7 @@
 #include <cstring>
 
 #include "conv_common.h"
+#include "halo_epilogue.h"
 
 namespace mia {
 
@@ -76,363 +77,6 @@ __device__ unsigned long long g_halo_dbg[HT_SLOTS][8];
 #define HT_STEP_STAMP(v)
 #define HT_STEPS 0
 #endif
-
-__device__ __forceinline__ void ld4f(const float* p, float (&v)[4]) {
-  const f32x4 a = *(const f32x4*)p;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) v[e] = a[e];
-}
-
-// Epilogue straight from the accumulators (REG kernels). Their MFMAs compute D = W·X̃ᵀ (output
-// channels × patch pixels), so for every fragment a lane holds 4 consecutive output channels of
-// one pixel: each per-element operation of conv_epilogue (same order, same semantics) runs in
-// registers with 8-/16-byte aux loads and stores and no LDS staging. The sdot / q reductions sum
-// a lane's pixels, then the 16 pixel lanes of a channel group by shuffles, then one atomic per
-// channel per wave.
-template <typename T, typename TL>
-__device__ __forceinline__ void halo_epilogue(const ConvK& k, const f32x4 (&acc)[TL::FM][TL::FN],
-                                              int n, int y0, int x0, int n0, int wm, int wn,
-                                              int lane) {
-  constexpr int FM = TL::FM, FN = TL::FN;
-  const mia_conv_args& p = k.a;
-  const int H = p.H, W = p.W, Cout = p.Cout;
-  const int px = lane & 15;
-  const int cl = n0 + wn * FN * 16 + ((lane >> 4) << 2);  // first channel of fragment 0
-  const T* AX = (const T*)p.aux_x;
-  const T* TA = (const T*)p.tap_a;
-  const T* TT = (const T*)p.tap_t;
-  const T* MA = (const T*)p.mask_a;
-  T* __restrict__ Y = (T*)p.y;
-  const bool bab = p.bab_demod != nullptr;
-  float osc[FN][4], bia[FN][4], dmv[FN][4], bbv[FN][4], part[FN][4], partq[FN][4];
-  float msl[FN][4], asl[FN][4], pcs[FN][4];
-  const bool prelu = p.act_out == MIA_ACT_PRELU;
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int c = cl + 16 * j;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      osc[j][e] = 1.f;
-      bia[j][e] = dmv[j][e] = bbv[j][e] = part[j][e] = partq[j][e] = 0.f;
-      msl[j][e] = asl[j][e] = pcs[j][e] = 0.f;
-    }
-    if (c < Cout) {  // c ≡ 0 mod 4 and Cout ≡ 0 mod 8: the whole quad is in range
-      if (p.out_scale) ld4f(p.out_scale + (size_t)n * k.cout_mod + c, osc[j]);
-      if (p.bias) ld4f(p.bias + c, bia[j]);
-      if (p.mask_slope) ld4f(p.mask_slope + c, msl[j]);
-      if (prelu) ld4f(p.act_slope + c, asl[j]);
-      if (bab) {
-        ld4f(p.bab_demod + (size_t)n * Cout + c, dmv[j]);
-        if (p.bab_bias) ld4f(p.bab_bias + c, bbv[j]);
-      }
-    }
-  }
-  // 2-byte outputs: pairs of fragments are exchanged between lane rows (v_permlane16_swap) so
-  // that every lane stores 8 consecutive channels with ONE 16-byte store — the store tail is
-  // issue-bound per instruction (cdna_hip_programming.md T21), so half the instructions.
-  constexpr bool WIDE = sizeof(T) == 2 && FN % 2 == 0;
-  const int lrow = lane >> 4;
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int y = y0 + wm * FM + i, x = x0 + px;
-    const int m = (n * H + y) * W + x;  // output pixel (identity placement, HT = H, WT = W)
-    const float nz = p.noise ? p.noise_w * p.noise[y * W + x] : 0.f;
-    const float bnz = (bab && p.bab_noise) ? p.bab_noise_w * p.bab_noise[y * W + x] : 0.f;
-    float vo[FN][4];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int c = cl + 16 * j;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) vo[j][e] = 0.f;
-      if (c >= Cout) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      const size_t aoff = (size_t)m * Cout + c;
-      float xv[4];
-      if (p.sdot || bab) load4<T>(AX + aoff, xv);
-      if (p.sdot) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) part[j][e] += v[e] * apply_act(xv[e], p.act_aux);
-      }
-      if (Y) {
-        const size_t off = (size_t)m * k.ystride + c;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = v[e] * osc[j][e] + nz + bia[j][e];
-        float ma[4];
-        if (TA) {
-          float tt[4];
-          load4<T>(TA + aoff, ma);  // the tap tensor doubles as the mask when they coincide
-          load4<T>(TT + aoff, tt);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += p.tap_coef * (ma[e] - tt[e]);
-        }
-        if (MA) {
-          if (MA != TA) load4<T>(MA + aoff, ma);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = ma[e] > 0.f ? v[e] : msl[j][e] * v[e];
-        }
-        if (prelu) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : asl[j][e] * v[e];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act_out);
-        }
-        if (p.accumulate) {
-          float yo[4];
-          load4<T>(Y + off, yo);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += yo[e];
-        }
-        if (bab) {  // fused StyledConv backward front of the layer whose activation is aux_x
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float gr = lrelu_s2_grad(xv[e]);
-            const float gp = v[e] * gr;
-            partq[j][e] += gp * (xv[e] / gr - bnz - bbv[j][e]);
-            v[e] = gp * dmv[j][e];
-          }
-        }
-        if (p.csum) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) pcs[j][e] += v[e];
-        }
-        if constexpr (WIDE) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) vo[j][e] = v[e];
-        } else {
-          store4<T>(Y + off, v);
-        }
-      }
-    }
-    if constexpr (WIDE) {
-      if (Y) {
-        typedef T t2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-        for (int q = 0; q < FN / 2; ++q) {
-          // A = fragment 2q (this lane's 4 channels), B = fragment 2q+1; after the swap lane
-          // row r holds channels [8·(r>>1), +8) of fragment 2q + (r & 1)
-          unsigned a[2], b[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const t2 ta = {(T)vo[2 * q][2 * h], (T)vo[2 * q][2 * h + 1]};
-            const t2 tb = {(T)vo[2 * q + 1][2 * h], (T)vo[2 * q + 1][2 * h + 1]};
-            a[h] = __builtin_bit_cast(unsigned, ta);
-            b[h] = __builtin_bit_cast(unsigned, tb);
-            const auto r = __builtin_amdgcn_permlane16_swap(a[h], b[h], false, false);
-            a[h] = r[0];
-            b[h] = r[1];
-          }
-          const int c = n0 + wn * FN * 16 + 16 * (2 * q + (lrow & 1)) + 8 * (lrow >> 1);
-          if (c < Cout)
-            *(uint4*)(Y + (size_t)m * k.ystride + c) = make_uint4(a[0], a[1], b[0], b[1]);
-        }
-      }
-    }
-  }
-  if (p.sdot || bab || p.csum) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int c = cl + 16 * j;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float a = part[j][e], b = partq[j][e], cs = pcs[j][e];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          a += __shfl_xor(a, o, 64);
-          b += __shfl_xor(b, o, 64);
-          cs += __shfl_xor(cs, o, 64);
-        }
-        if (px == 0 && c < Cout) {
-          if (p.sdot) atomicAdd(&p.sdot[(size_t)n * Cout + c + e], a);
-          if (bab) atomicAdd(&p.bab_q[(size_t)n * Cout + c + e], b);
-          if (p.csum) atomicAdd(&p.csum[(size_t)n * Cout + c + e], cs);
-        }
-      }
-    }
-  }
-}
-
-// Epilogue feature mask (compile-time specialisations of halo_epilogue for the launches the
-// attack makes; any other combination runs the runtime-generic halo_epilogue).
-namespace epi {
-constexpr int OSC = 1, NOISE = 2, BIAS = 4, TAP = 8, MASK = 16, ACC = 32, SDOT = 64, BAB = 128;
-constexpr int RELU = MIA_ACT_RELU << 8, LRELU = MIA_ACT_LRELU_S2 << 8;
-}  // namespace epi
-
-template <typename T>
-struct Raw4 {  // 4 consecutive elements of T, loaded raw (8 or 16 bytes)
-  typedef T type __attribute__((ext_vector_type(4)));
-};
-
-// The same operations as halo_epilogue for one feature mask F, straight-line: every aux load of
-// the tile is issued first (one wait instead of one per fragment — a wait also drains the stores
-// issued before it), then the arithmetic and the 16-byte stores.
-template <typename T, typename TL, int F>
-__device__ __forceinline__ void halo_epilogue_f(const ConvK& k, const f32x4 (&acc)[TL::FM][TL::FN],
-                                                int n, int y0, int x0, int n0, int wm, int wn,
-                                                int lane) {
-  constexpr int FM = TL::FM, FN = TL::FN;
-  constexpr bool OSC = F & epi::OSC, NOISE = F & epi::NOISE, BIAS = F & epi::BIAS;
-  constexpr bool TAP = F & epi::TAP, MASK = F & epi::MASK, ACC = F & epi::ACC;
-  constexpr bool SDOT = F & epi::SDOT, BAB = F & epi::BAB;
-  constexpr int ACT = (F >> 8) & 3;
-  constexpr bool WIDE = sizeof(T) == 2 && FN % 2 == 0;
-  typedef typename Raw4<T>::type R4;
-  const mia_conv_args& p = k.a;
-  const int H = p.H, W = p.W, Cout = p.Cout;
-  const int px = lane & 15, lrow = lane >> 4;
-  const int cl = n0 + wn * FN * 16 + (lrow << 2);
-  T* __restrict__ Y = (T*)p.y;
-  const T* AX = (const T*)p.aux_x;
-  const T* TA = (const T*)p.tap_a;
-  const T* TT = (const T*)p.tap_t;
-  const T* MA = (const T*)p.mask_a;
-  const bool ma_is_ta = MA == TA;
-
-  float osc[FN][4], bia[FN][4], dmv[FN][4], bbv[FN][4];
-  bool cok[FN];
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int c = cl + 16 * j;
-    cok[j] = c < Cout;  // c ≡ 0 mod 4, Cout ≡ 0 mod 8: the whole quad is in range
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      osc[j][e] = 1.f;
-      bia[j][e] = dmv[j][e] = bbv[j][e] = 0.f;
-    }
-    if (cok[j]) {
-      if constexpr (OSC) ld4f(p.out_scale + (size_t)n * k.cout_mod + c, osc[j]);
-      if constexpr (BIAS) ld4f(p.bias + c, bia[j]);
-      if constexpr (BAB) {
-        ld4f(p.bab_demod + (size_t)n * Cout + c, dmv[j]);
-        if (p.bab_bias) ld4f(p.bab_bias + c, bbv[j]);
-      }
-    }
-  }
-  float part[FN][4], partq[FN][4];
-#pragma unroll
-  for (int j = 0; j < FN; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) part[j][e] = partq[j][e] = 0.f;
-  // rows in chunks of FMC (the aux loads of a chunk are hoisted together; chunks bound the live
-  // registers for tall wave tiles)
-  constexpr int FMC = FM < 4 ? FM : 4;
-#pragma unroll
-  for (int i0 = 0; i0 < FM; i0 += FMC) {
-  float nz[FMC], bnz[FMC];
-  R4 rx[FMC][FN], rta[FMC][FN], rtt[FMC][FN], rma[FMC][FN], ryo[FMC][FN];
-#pragma unroll
-  for (int i = 0; i < FMC; ++i) {
-    const int y = y0 + wm * FM + i0 + i, x = x0 + px;
-    const int m = (n * H + y) * W + x;
-    nz[i] = bnz[i] = 0.f;
-    if constexpr (NOISE) nz[i] = p.noise_w * p.noise[y * W + x];
-    if constexpr (BAB) {
-      if (p.bab_noise) bnz[i] = p.bab_noise_w * p.bab_noise[y * W + x];
-    }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      if (!cok[j]) continue;
-      const int c = cl + 16 * j;
-      const size_t aoff = (size_t)m * Cout + c;
-      if constexpr (SDOT || BAB) rx[i][j] = *(const R4*)(AX + aoff);
-      if constexpr (TAP) {
-        rta[i][j] = *(const R4*)(TA + aoff);
-        rtt[i][j] = *(const R4*)(TT + aoff);
-      }
-      if constexpr (MASK) {
-        if (!(TAP && ma_is_ta)) rma[i][j] = *(const R4*)(MA + aoff);
-      }
-      if constexpr (ACC) ryo[i][j] = *(const R4*)(Y + (size_t)m * k.ystride + c);
-    }
-  }
-
-#pragma unroll
-  for (int i = 0; i < FMC; ++i) {
-    const int m = (n * H + y0 + wm * FM + i0 + i) * W + x0 + px;
-    float vo[FN][4];
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) vo[j][e] = 0.f;
-      if (!cok[j]) continue;
-      float v[4] = {acc[i0 + i][j][0], acc[i0 + i][j][1], acc[i0 + i][j][2], acc[i0 + i][j][3]};
-      float xv[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) xv[e] = (SDOT || BAB) ? (float)rx[i][j][e] : 0.f;
-      if constexpr (SDOT) {  // act_aux NONE (the host picks the generic epilogue otherwise)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) part[j][e] += v[e] * xv[e];
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if constexpr (OSC) v[e] *= osc[j][e];
-        if constexpr (NOISE) v[e] += nz[i];
-        if constexpr (BIAS) v[e] += bia[j][e];
-        if constexpr (TAP) v[e] += p.tap_coef * ((float)rta[i][j][e] - (float)rtt[i][j][e]);
-        if constexpr (MASK) {
-          const float ma = (TAP && ma_is_ta) ? (float)rta[i][j][e] : (float)rma[i][j][e];
-          v[e] = ma > 0.f ? v[e] : 0.f;
-        }
-        if constexpr (ACT == MIA_ACT_RELU) v[e] = v[e] > 0.f ? v[e] : 0.f;
-        if constexpr (ACT == MIA_ACT_LRELU_S2) v[e] = lrelu_s2(v[e]);
-        if constexpr (ACC) v[e] += (float)ryo[i][j][e];
-        if constexpr (BAB) {
-          const float gr = lrelu_s2_grad(xv[e]);
-          const float gp = v[e] * gr;
-          partq[j][e] += gp * (xv[e] / gr - bnz[i] - bbv[j][e]);
-          v[e] = gp * dmv[j][e];
-        }
-        vo[j][e] = v[e];
-      }
-      if constexpr (!WIDE) {
-        if (Y) store4<T>(Y + (size_t)m * k.ystride + cl + 16 * j, v);
-      }
-    }
-    if constexpr (WIDE) {
-      if (Y) {
-        typedef T t2 __attribute__((ext_vector_type(2)));
-#pragma unroll
-        for (int q = 0; q < FN / 2; ++q) {
-          unsigned a[2], b[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const t2 ta = {(T)vo[2 * q][2 * h], (T)vo[2 * q][2 * h + 1]};
-            const t2 tb = {(T)vo[2 * q + 1][2 * h], (T)vo[2 * q + 1][2 * h + 1]};
-            const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, ta),
-                                                            __builtin_bit_cast(unsigned, tb),
-                                                            false, false);
-            a[h] = r[0];
-            b[h] = r[1];
-          }
-          const int c = n0 + wn * FN * 16 + 16 * (2 * q + (lrow & 1)) + 8 * (lrow >> 1);
-          if (c < Cout)
-            *(uint4*)(Y + (size_t)m * k.ystride + c) = make_uint4(a[0], a[1], b[0], b[1]);
-        }
-      }
-    }
-  }
-  }  // row chunks
-  if constexpr (SDOT || BAB) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int c = cl + 16 * j;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float a = part[j][e], b = partq[j][e];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          if constexpr (SDOT) a += __shfl_xor(a, o, 64);
-          if constexpr (BAB) b += __shfl_xor(b, o, 64);
-        }
-        if (px == 0 && c < Cout) {
-          if constexpr (SDOT) atomicAdd(&p.sdot[(size_t)n * Cout + c + e], a);
-          if constexpr (BAB) atomicAdd(&p.bab_q[(size_t)n * Cout + c + e], b);
-        }
-      }
-    }
-  }
-}
 
 // EPI: −2 = LDS-staged shared epilogue (conv_epilogue), −1 = register epilogue with runtime
 // features (halo_epilogue), ≥ 0 = register epilogue specialised for feature mask EPI.
@@ -736,23 +380,6 @@ static int launch_halo_tile_(ConvK& k, hipStream_t st) {
   return check_launch("conv_halo");
 }
 
-// Feature mask of a launch (−1: a combination without a specialisation, e.g. act_aux ≠ NONE).
-static int epi_mask(const ConvK& k) {
-  const mia_conv_args& a = k.a;
-  if ((a.sdot || a.bab_demod) && a.act_aux != MIA_ACT_NONE) return -1;
-  if (a.mask_slope || a.act_out == MIA_ACT_PRELU || a.csum) return -1;  // encoder features
-  int f = 0;
-  if (a.out_scale) f |= epi::OSC;
-  if (a.noise) f |= epi::NOISE;
-  if (a.bias) f |= epi::BIAS;
-  if (a.tap_a) f |= epi::TAP;
-  if (a.mask_a) f |= epi::MASK;
-  if (a.accumulate) f |= epi::ACC;
-  if (a.sdot) f |= epi::SDOT;
-  if (a.bab_demod) f |= epi::BAB;
-  return f | (a.act_out << 8);
-}
-
 template <typename T, typename TL, bool PRO, bool SPEC>
 static int launch_halo_tile(ConvK& k, hipStream_t st) {
   // tuning / A-B switch, read per launch: MIA_HALO_EPI=0 LDS-staged shared epilogue, 2 register
@@ -777,6 +404,11 @@ static int launch_halo_tile(ConvK& k, hipStream_t st) {
         case OSC | SDOT | BAB: return launch_halo_tile_<T, TL, PRO, OSC | SDOT | BAB>(k, st);
         case OSC | SDOT | ACC | BAB:
           return launch_halo_tile_<T, TL, PRO, OSC | SDOT | ACC | BAB>(k, st);
+        // e4e IR-SE50 body: conv1 fwd (PReLU), conv2 fwd (bias + SE pool), their input gradients
+        case PRELU: return launch_halo_tile_<T, TL, PRO, PRELU>(k, st);
+        case BIAS | CSUM: return launch_halo_tile_<T, TL, PRO, BIAS | CSUM>(k, st);
+        case MASK | MSL: return launch_halo_tile_<T, TL, PRO, MASK | MSL>(k, st);
+        case ACC: return launch_halo_tile_<T, TL, PRO, ACC>(k, st);
         default: break;
       }
     }

@@ -668,3 +668,71 @@ def test_upconv_halo_fwd(cuda, dtype, N, cin, cout, R, lrelu_in):
     assert not torch.isnan(t1).any(), "halo path left T positions unwritten"
     assert rel_err(nchw(t1), ref) < 3 * TOL[dtype]
     assert rel_err(t1.float(), t2.float()) < 2 * TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,H,W,C", [(2, 192, 192, 64), (1, 16, 16, 64), (3, 16, 48, 64),
+                                     (2, 32, 16, 128)])
+@pytest.mark.parametrize("mode", ["plain", "bias_relu", "tap_mask", "prelu", "bias_csum",
+                                  "mask_slope", "acc"])
+@pytest.mark.parametrize("spec", ["1", "0"])
+def test_conv2d_register_epilogue_paths(cuda, monkeypatch, dtype, N, H, W, C, mode, spec):
+    """Stride-1 C→C 3×3 convs with every epilogue feature set of the attack step (vgg.py, e4e
+    IR-SE50 body). spec=1: the specialised register epilogues — at C = 64 the weights-resident
+    persistent kernel (conv_wres.hip; 192² = 288 patches > one per CU exercises the persistent
+    loop and the halo prefetch), at C = 128 the halo kernel; spec=0: generic tile at 64
+    (MIA_CONV_WRES=0) and the runtime-feature halo epilogue at 128 (MIA_HALO_EPI=2)."""
+    monkeypatch.setenv("MIA_CONV_WRES", spec)
+    monkeypatch.setenv("MIA_HALO_EPI", "1" if spec == "1" else "2")
+    g = torch.Generator().manual_seed(N * 11 + H + W + C + len(mode))
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
+    xq, wq = x.to(dtype).double(), w.to(dtype).double()
+    kp = ops.conv2d_kpad(9, C, dtype)
+    wm = torch.zeros(C, kp)
+    wm[:, :9 * C] = w.permute(0, 2, 3, 1).reshape(C, 9 * C)
+    grp = [dict(w=wm.to(dtype).to(cuda), kh=3, kw=3, pad=(1, 1), ho=H, wo=W)]
+    conv = F.conv2d(xq, wq, padding=1)
+    y0 = torch.randn(N, C, H, W, generator=g)
+    y = nhwc(y0, dtype).to(cuda)
+    slope = torch.rand(C, generator=g) * 0.5 + 0.05
+    sl = slope.double().view(1, C, 1, 1)
+    kw, cs = {}, None
+    if mode == "plain":
+        ref = conv
+    elif mode == "bias_relu":
+        b = torch.randn(C, generator=g) * 0.1
+        ref = F.relu(conv + b.double().view(1, C, 1, 1))
+        kw = dict(bias=b.to(cuda), act_out=ops.ACT_RELU)
+    elif mode == "tap_mask":
+        a = torch.randn(N, C, H, W, generator=g).relu()
+        t = torch.randn(N, C, H, W, generator=g)
+        aq, tq = a.to(dtype).double(), t.to(dtype).double()
+        ref = (conv + 0.37 * (aq - tq)) * (aq > 0)
+        y3 = torch.empty_like(y)
+        ops.conv3x3(nhwc(x, dtype).to(cuda), layouts.fwd_matrix(w, dtype).to(cuda), y3, cout=C,
+                    tap_a=nhwc(a, dtype).to(cuda), tap_t=nhwc(t, dtype).to(cuda), tap_coef=0.37,
+                    mask_a=nhwc(a, dtype).to(cuda))
+    elif mode == "prelu":
+        ref = torch.where(conv > 0, conv, sl * conv)
+        kw = dict(act_out=ops.ACT_PRELU, act_slope=slope.to(cuda))
+    elif mode == "bias_csum":
+        b = torch.randn(C, generator=g) * 0.1
+        ref = conv + b.double().view(1, C, 1, 1)
+        cs = torch.zeros(N, C, device=cuda)
+        kw = dict(bias=b.to(cuda), csum=cs)
+    elif mode == "mask_slope":
+        m = torch.randn(N, C, H, W, generator=g)
+        ref = torch.where(m.to(dtype).double() > 0, conv, sl * conv)
+        kw = dict(mask_a=nhwc(m, dtype).to(cuda), mask_slope=slope.to(cuda))
+    else:
+        ref = conv + y0.to(dtype).double()
+        kw = dict(accumulate=True)
+    if mode == "tap_mask":
+        y = y3
+    else:
+        ops.conv2d(nhwc(x, dtype).to(cuda), grp, y, (H, W), cout=C, **kw)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(y), ref) < 2 * TOL[dtype]
+    if cs is not None:
+        assert rel_err(cs, ref.sum((2, 3))) < 2 * TOL[dtype]

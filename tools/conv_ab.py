@@ -36,7 +36,54 @@ SHAPES = [
     ("up 128²→256² 256→128", 128, 256, 128, "up"),
     ("up 64²→128² 512→256", 64, 512, 256, "up"),
     ("up 32²→64² 512→512", 32, 512, 512, "up"),
+    # e4e IR-SE50 body (mia_conv2d epilogue features)
+    ("e4e prelu 256² 64→64", 256, 64, 64, "prelu"),
+    ("e4e bias+csum 128² 64→64", 128, 64, 64, "csum"),
+    ("e4e mask+slope 128² 64→64", 128, 64, 64, "mslope"),
+    ("e4e acc 128² 64→64", 128, 64, 64, "acc"),
+    ("e4e prelu 64² 128→128", 64, 128, 128, "prelu"),
+    ("e4e bias+csum 32² 256→256", 32, 256, 256, "csum"),
+    ("e4e mask+slope 32² 256→256", 32, 256, 256, "mslope"),
+    ("e4e acc 32² 256→256", 32, 256, 256, "acc"),
 ]
+
+E4E_MODES = ("prelu", "csum", "mslope", "acc")
+
+
+def run_e4e(H, Cin, Cout, mode, N, iters, dtype, dev):
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(N, H, H, Cin, device=dev, generator=g).to(dtype)
+    kp = ops.conv2d_kpad(9, Cin, dtype)
+    w = (torch.randn(Cout, kp, device=dev, generator=g) / math.sqrt(9 * Cin)).to(dtype)
+    y = torch.empty(N, H, H, Cout, device=dev, dtype=dtype)
+    grp = [dict(w=w, kh=3, kw=3, pad=(1, 1), ho=H, wo=H)]
+    slope = torch.rand(Cout, device=dev, generator=g) * 0.5 + 0.05
+    kw = {}
+    if mode == "prelu":
+        kw = dict(act_out=ops.ACT_PRELU, act_slope=slope)
+    elif mode == "csum":
+        kw = dict(bias=torch.randn(Cout, device=dev, generator=g),
+                  csum=torch.zeros(N, Cout, device=dev))
+    elif mode == "mslope":
+        kw = dict(mask_a=torch.randn(N, H, H, Cout, device=dev, generator=g).to(dtype),
+                  mask_slope=slope)
+    elif mode == "acc":
+        kw = dict(accumulate=True)
+    call = lambda: ops.conv2d(x, grp, y, (H, H), cout=Cout, **kw)  # noqa: E731
+    y.zero_()
+    call()
+    torch.cuda.synchronize()
+    ref = y.float().clone()
+    if "csum" in kw:
+        ref = torch.cat([ref.flatten(), kw["csum"].flatten() / (H * H)])
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        call()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    return ms, 2.0 * N * H * H * 9 * Cin * Cout / (ms * 1e-3) / 1e12, ref
 
 
 def run_up(H, Cin, Cout, N, iters, dtype, dev):
@@ -65,6 +112,8 @@ def run_up(H, Cin, Cout, N, iters, dtype, dev):
 def run(name, H, Cin, Cout, mode, N, iters, dtype, dev):
     if mode == "up":
         return run_up(H, Cin, Cout, N, iters, dtype, dev)
+    if mode in E4E_MODES:
+        return run_e4e(H, Cin, Cout, mode, N, iters, dtype, dev)
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.randn(N, H, H, Cin, device=dev, generator=g).to(dtype)
     kp = ops.conv_kpad(Cin, dtype)

@@ -35,8 +35,19 @@
 
 namespace mia {
 
+// s_waitcnt leaving at most `steps` K-steps of DMA (PER vm instructions each) in flight
+template <int PER>
+__device__ __forceinline__ void wait_dma_steps(int steps) {
+  static_assert(3 * PER <= 63, "vmcnt field");
+  if (steps <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (steps == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+  else if (steps == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER) : "memory");
+}
+
 template <typename T, typename TL, bool PRO, bool SMALLC>
-__global__ __launch_bounds__(TL::NT, TL::NW == 4 ? 2 : 1) void conv_kernel(const ConvK k) {
+__global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? 2 : 1) void conv_kernel(
+    const ConvK k) {
   typedef typename Vec<T>::type VT;
   constexpr int VEC = Vec<T>::N;
   constexpr int BK = ROWB / (int)sizeof(T);
@@ -170,9 +181,9 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 ? 2 : 1) void conv_kernel(const
   if constexpr (STAGES == 2) {
     __syncthreads();
   } else {
-    // retire step 0 (step 1 may stay in flight), then make every wave's DMA visible
-    if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_INS + B_INS) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // retire step 0 (the later prologue steps may stay in flight), then make every wave's DMA
+    // visible
+    wait_dma_steps<A_INS + B_INS>(min(nk, STAGES - 1) - 1);
     __syncthreads();
   }
   const int frow = lane & 15, fq = lane >> 4;
@@ -213,9 +224,8 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 ? 2 : 1) void conv_kernel(const
     if constexpr (STAGES == 2) {
       __syncthreads();  // retires the DMA of step kb+1 (vmcnt(0)) and frees stage st
     } else {
-      // step kb+1 must have landed; step kb+2 (issued this iteration) may stay in flight
-      if (ahead < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_INS + B_INS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // step kb+1 must have landed; steps kb+2 … (issued up to this iteration) may stay in flight
+      wait_dma_steps<A_INS + B_INS>(min(STAGES - 2, nk - 2 - kb));
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS reads of stage st done
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);

@@ -32,11 +32,16 @@ adjoint in the PGD update. Stored for the backward: per unit a1 = PReLU(conv1), 
 the SE vectors u, s; the head activations; nothing else.
 """
 import math
+import os
 
 import torch
 
 from . import layouts, ops
 from .ops import ACT_PRELU
+
+# side streams for the style heads (GPU_MAX_HW_QUEUES is 4 on the box); MIA_HEAD_STREAMS
+# overrides it (A/B switch)
+HEAD_STREAMS = max(1, int(os.environ.get("MIA_HEAD_STREAMS", "4")))
 from .vgg import CPAD
 from .weights import (E4E_COARSE, E4E_MIDDLE, E4E_SE_REDUCTION, STYLE_DIM, e4e_style_spatial,
                       e4e_units, n_latent_for)
@@ -163,6 +168,15 @@ class E4EEncoder:
         self.lin_bias = [b0l] + [(h["lb"] + b0l).contiguous() for h in self.heads[1:]]
         self.flops_fwd_per_image = self._count_flops()
         self._plans = {}
+        self._side = None
+
+    def _side_streams(self):
+        """The 14 GradualStyleBlocks are independent chains of small stride-2 convs (8²…1²
+        outputs: a few tiles each, latency-bound on their K loop), so they run concurrently on
+        HEAD_STREAMS side streams forked from / joined into the caller's stream."""
+        if self._side is None:
+            self._side = [torch.cuda.Stream(device=self.device) for _ in range(HEAD_STREAMS)]
+        return self._side
 
     # ------------------------------------------------------------------------------------------
     def _count_flops(self):
@@ -250,21 +264,28 @@ class E4EEncoder:
                    bias=self.lat_b[1], accumulate=True)
         feats.update(p2=p2, p1=p1)
         self._feats = feats
+        main = torch.cuda.current_stream()
+        side = self._side_streams()
+        for st in side:
+            st.wait_stream(main)
         for i, hd in enumerate(self.heads):
             x = feats[hd["src"]]
             h = x.shape[1]
             acts = []
-            for j, cv in enumerate(hd["convs"]):
-                ho = _s2_out(h)
-                a = self._buf(ws, f"h{i}_{j}", (N, ho, ho, STYLE_DIM))
-                ops.conv2d(x, [_g3(cv["w"], ho)], a, (ho, ho), cout=STYLE_DIM, stride=2,
-                           bias=cv["b"], act_out=ACT_PRELU, act_slope=self.slope001)
-                acts.append(a)
-                x, h = a, ho
-            if h != 1:
-                raise ValueError("GradualStyleBlock must end at 1×1 (encoder input R = 256)")
-            hd["_acts"] = acts
-            ops.cast(x, self._buf(ws, f"f{i}", (N, STYLE_DIM), f32))
+            with torch.cuda.stream(side[i % len(side)]):
+                for j, cv in enumerate(hd["convs"]):
+                    ho = _s2_out(h)
+                    a = self._buf(ws, f"h{i}_{j}", (N, ho, ho, STYLE_DIM))
+                    ops.conv2d(x, [_g3(cv["w"], ho)], a, (ho, ho), cout=STYLE_DIM, stride=2,
+                               bias=cv["b"], act_out=ACT_PRELU, act_slope=self.slope001)
+                    acts.append(a)
+                    x, h = a, ho
+                if h != 1:
+                    raise ValueError("GradualStyleBlock must end at 1×1 (encoder input R = 256)")
+                hd["_acts"] = acts
+                ops.cast(x, self._buf(ws, f"f{i}", (N, STYLE_DIM), f32))
+        for st in side:
+            main.wait_stream(st)
         lat = ws.get(f"{tag}.lat", (N, self.n_latent, STYLE_DIM), f32)
         self._plan(ws, N, "fwd", lat).run()
         return lat
@@ -319,25 +340,43 @@ class E4EEncoder:
         ops.sum_slices(g_lat, self._buf(ws, "gsum", (N, D), f32))
         self._plan(ws, N, "bwd", g_lat).run()
         gfeat = {k: self._buf(ws, "g" + k, feats[k].shape) for k in ("c3", "p2", "p1")}
-        seen = set()
-        # style heads, fine first (their gradient feeds p1 → p2 → c3)
+        # style heads, fine first (their gradient feeds p1 → p2 → c3): every head's chain down to
+        # its first conv's output gradient runs concurrently on the side streams; the first convs
+        # (input gradients into the shared source-feature gradient, the later ones accumulating)
+        # run in the same head order on one side stream per source
+        main = torch.cuda.current_stream()
+        side = self._side_streams()
+        for st in side:
+            main_ev = main.record_event()
+            st.wait_event(main_ev)
+        heads_g, heads_ev = {}, {}
         for i in reversed(range(self.n_latent)):
             hd = self.heads[i]
             acts = hd["_acts"]
-            g = self._buf(ws, f"gh{i}", acts[-1].shape)
-            ops.cast(self._buf(ws, f"gf{i}", (N, D), f32), g)
-            ops.prelu_bwd_scale(g, acts[-1], self.slope001, g)
-            for j in reversed(range(len(hd["convs"]))):
-                cv = hd["convs"][j]
-                if j > 0:
+            st = side[i % len(side)]
+            with torch.cuda.stream(st):
+                g = self._buf(ws, f"gh{i}", acts[-1].shape)
+                ops.cast(self._buf(ws, f"gf{i}", (N, D), f32), g)
+                ops.prelu_bwd_scale(g, acts[-1], self.slope001, g)
+                for j in reversed(range(1, len(hd["convs"]))):
+                    cv = hd["convs"][j]
                     y = self._buf(ws, f"ghh{i}_{j - 1}", acts[j - 1].shape)
-                    mask, acc = acts[j - 1], False
-                else:
-                    y = gfeat[hd["src"]]
-                    mask, acc = None, hd["src"] in seen
-                    seen.add(hd["src"])
-                self._s2_dgrad(g, cv["wd"], cv["wdh"], y, mask, self.slope001, acc)
-                g = y
+                    self._s2_dgrad(g, cv["wd"], cv["wdh"], y, acts[j - 1], self.slope001, False)
+                    g = y
+                heads_g[i], heads_ev[i] = g, st.record_event()
+        src_stream = {src: side[k % len(side)] for k, src in enumerate(("c3", "p2", "p1"))}
+        seen = set()
+        for i in reversed(range(self.n_latent)):
+            hd = self.heads[i]
+            st = src_stream[hd["src"]]
+            st.wait_event(heads_ev[i])
+            with torch.cuda.stream(st):
+                cv = hd["convs"][0]
+                self._s2_dgrad(heads_g[i], cv["wd"], cv["wdh"], gfeat[hd["src"]], None,
+                               self.slope001, hd["src"] in seen)
+            seen.add(hd["src"])
+        for st in side:
+            main.wait_stream(st)
         dbg = getattr(self, "debug", None)  # tests: dict to receive intermediate gradients
         if dbg is not None:
             dbg.update({"heads." + k: v.clone() for k, v in gfeat.items()})

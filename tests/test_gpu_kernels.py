@@ -736,3 +736,41 @@ def test_conv2d_register_epilogue_paths(cuda, monkeypatch, dtype, N, H, W, C, mo
     assert rel_err(nchw(y), ref) < 2 * TOL[dtype]
     if cs is not None:
         assert rel_err(cs, ref.sum((2, 3))) < 2 * TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,H,C,k,stride", [(4, 2, 512, 3, 2), (3, 8, 512, 3, 2), (2, 16, 256, 3, 2),
+                                            (5, 4, 512, 1, 1), (2, 8, 128, 3, 1),
+                                            (3, 4, 128, 1, 1)])
+@pytest.mark.parametrize("mode", ["bias_prelu", "mask_slope_acc"])
+def test_conv2d_style_head_shapes(cuda, dtype, N, H, C, k, stride, mode):
+    """Generic-tile launches of the e4e style heads (stride-2 3×3, 8²…1² outputs, K up to 9·512,
+    a few tiles per launch) and short-K 1×1 layers, with the head epilogues (bias + PReLU) and
+    the backward ones (slope mask + accumulate), against torch fp64."""
+    g = torch.Generator().manual_seed(N * 13 + H + C + k + stride)
+    pad = k // 2
+    ho = (H + 2 * pad - k) // stride + 1
+    x = torch.randn(N, C, H, H, generator=g)
+    w = torch.randn(C, C, k, k, generator=g) / math.sqrt(k * k * C)
+    xq, wq = x.to(dtype).double(), w.to(dtype).double()
+    kp = ops.conv2d_kpad(k * k, C, dtype)
+    wm = torch.zeros(C, kp)
+    wm[:, :k * k * C] = w.permute(0, 2, 3, 1).reshape(C, k * k * C)
+    grp = [dict(w=wm.to(dtype).to(cuda), kh=k, kw=k, pad=(pad, pad), ho=ho, wo=ho)]
+    conv = F.conv2d(xq, wq, stride=stride, padding=pad)
+    slope = torch.rand(C, generator=g) * 0.5 + 0.05
+    sl = slope.double().view(1, C, 1, 1)
+    y0 = torch.randn(N, C, ho, ho, generator=g)
+    if mode == "bias_prelu":
+        b = torch.randn(C, generator=g) * 0.1
+        pre = conv + b.double().view(1, C, 1, 1)
+        ref = torch.where(pre > 0, pre, sl * pre)
+        kw = dict(bias=b.to(cuda), act_out=ops.ACT_PRELU, act_slope=slope.to(cuda))
+    else:
+        m = torch.randn(N, C, ho, ho, generator=g)
+        ref = torch.where(m.to(dtype).double() > 0, conv, sl * conv) + y0.to(dtype).double()
+        kw = dict(mask_a=nhwc(m, dtype).to(cuda), mask_slope=slope.to(cuda), accumulate=True)
+    y = nhwc(y0, dtype).to(cuda)
+    ops.conv2d(nhwc(x, dtype).to(cuda), grp, y, (ho, ho), cout=C, stride=stride, **kw)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(y), ref) < 2 * TOL[dtype]

@@ -45,22 +45,31 @@ SHAPES = [
     ("e4e bias+csum 32² 256→256", 32, 256, 256, "csum"),
     ("e4e mask+slope 32² 256→256", 32, 256, 256, "mslope"),
     ("e4e acc 32² 256→256", 32, 256, 256, "acc"),
+    # e4e GradualStyleBlock convs (stride 2, bias + LeakyReLU(0.01)); H = output side
+    ("head s2 →16² 512→512", 16, 512, 512, "head"),
+    ("head s2 →8² 512→512", 8, 512, 512, "head"),
+    ("head s2 →4² 512→512", 4, 512, 512, "head"),
+    ("head s2 →2² 512→512", 2, 512, 512, "head"),
+    ("head s2 →1² 512→512", 1, 512, 512, "head"),
 ]
 
-E4E_MODES = ("prelu", "csum", "mslope", "acc")
+E4E_MODES = ("prelu", "csum", "mslope", "acc", "head")
 
 
 def run_e4e(H, Cin, Cout, mode, N, iters, dtype, dev):
     g = torch.Generator(device=dev).manual_seed(0)
-    x = torch.randn(N, H, H, Cin, device=dev, generator=g).to(dtype)
+    s2 = 2 if mode == "head" else 1
+    x = torch.randn(N, H * s2, H * s2, Cin, device=dev, generator=g).to(dtype)
     kp = ops.conv2d_kpad(9, Cin, dtype)
     w = (torch.randn(Cout, kp, device=dev, generator=g) / math.sqrt(9 * Cin)).to(dtype)
     y = torch.empty(N, H, H, Cout, device=dev, dtype=dtype)
     grp = [dict(w=w, kh=3, kw=3, pad=(1, 1), ho=H, wo=H)]
     slope = torch.rand(Cout, device=dev, generator=g) * 0.5 + 0.05
     kw = {}
-    if mode == "prelu":
+    if mode in ("prelu", "head"):
         kw = dict(act_out=ops.ACT_PRELU, act_slope=slope)
+    if mode == "head":
+        kw.update(stride=2, bias=torch.randn(Cout, device=dev, generator=g))
     elif mode == "csum":
         kw = dict(bias=torch.randn(Cout, device=dev, generator=g),
                   csum=torch.zeros(N, Cout, device=dev))

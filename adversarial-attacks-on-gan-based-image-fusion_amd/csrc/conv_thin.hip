@@ -38,6 +38,7 @@ template <typename T, int COUT>
 __global__ __launch_bounds__(256) void conv_thin_in_kernel(const T* __restrict__ x,
                                                            const T* __restrict__ w, int kpad,
                                                            const float* __restrict__ bias, int act,
+                                                           const float* __restrict__ slope,
                                                            T* __restrict__ y, int N, int H, int W) {
   typedef typename Vec<T>::type VT;
   constexpr int FN = COUT / 16;
@@ -48,11 +49,14 @@ __global__ __launch_bounds__(256) void conv_thin_in_kernel(const T* __restrict__
   for (int j = 0; j < FN; ++j)
 #pragma unroll
     for (int m = 0; m < 3; ++m) wr[j][m] = *(const VT*)(w + (size_t)(16 * j + frow) * kpad + 8 * (4 * m + fq));
-  float bs[FN][4];
+  float bs[FN][4], sl[FN][4];  // bias; PReLU slope (act = MIA_ACT_PRELU: the e4e input layer)
 #pragma unroll
   for (int j = 0; j < FN; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bs[j][r] = bias ? bias[16 * j + 4 * fq + r] : 0.f;
+    for (int r = 0; r < 4; ++r) {
+      bs[j][r] = bias ? bias[16 * j + 4 * fq + r] : 0.f;
+      sl[j][r] = act == MIA_ACT_PRELU ? slope[16 * j + 4 * fq + r] : 0.f;
+    }
 
   const int gpr = W / 16, ngroups = N * H * gpr;
   for (int g = wave; g < ngroups; g += nwaves) {
@@ -88,8 +92,13 @@ __global__ __launch_bounds__(256) void conv_thin_in_kernel(const T* __restrict__
         for (int e = 0; e < 2; ++e) {
           va[e] = acc[2 * q][2 * h + e] + bs[2 * q][2 * h + e];
           vb[e] = acc[2 * q + 1][2 * h + e] + bs[2 * q + 1][2 * h + e];
-          va[e] = apply_act(va[e], act);
-          vb[e] = apply_act(vb[e], act);
+          if (act == MIA_ACT_PRELU) {
+            va[e] = va[e] > 0.f ? va[e] : sl[2 * q][2 * h + e] * va[e];
+            vb[e] = vb[e] > 0.f ? vb[e] : sl[2 * q + 1][2 * h + e] * vb[e];
+          } else {
+            va[e] = apply_act(va[e], act);
+            vb[e] = apply_act(vb[e], act);
+          }
         }
         const t2 ta = {(T)va[0], (T)va[1]};
         const t2 tb = {(T)vb[0], (T)vb[1]};
@@ -106,7 +115,7 @@ __global__ __launch_bounds__(256) void conv_thin_in_kernel(const T* __restrict__
   }
 }
 
-// ---- input gradient, CIN = 64 channels → 8 output channels (store), no epilogue ---------------
+// ---- input gradient, CIN = 64 channels → 8 output channels (store, or accumulate into y) -------
 // Every input pixel feeds 9 taps, so the pixel operand is staged per wave in LDS: a work item is
 // RS = 2 output rows × 16 pixels; its (RS+2) × 18 input pixels (72 rows of 128 B, 9 LDS-DMA pieces
 // of 1 KB, bank-swizzled through the source chunk as in conv_halo.hip) are DMA'd once, then read
@@ -122,8 +131,8 @@ constexpr int THIN_WBUF = THIN_PIECES * 1024;
 template <typename T, int COUT>
 __global__ __launch_bounds__(256) void conv_thin_out_kernel(const T* __restrict__ g,
                                                             const T* __restrict__ w, int kpad,
-                                                            T* __restrict__ y, int N, int H,
-                                                            int W) {
+                                                            T* __restrict__ y, int accumulate,
+                                                            int N, int H, int W) {
   typedef typename Vec<T>::type VT;
   constexpr int CIN = 64, S = 18;
   static_assert(COUT == 8, "");
@@ -186,7 +195,14 @@ __global__ __launch_bounds__(256) void conv_thin_out_kernel(const T* __restrict_
       const int yy = y0 + ry;
       if (fq < COUT / 4 && yy < H) {
         float v[4] = {acc[0], acc[1], acc[2], acc[3]};
-        store4<T>(y + ((size_t)(n * H + yy) * W + x0 + frow) * COUT + 4 * fq, v);
+        T* yp = y + ((size_t)(n * H + yy) * W + x0 + frow) * COUT + 4 * fq;
+        if (accumulate) {  // the e4e input layer's gradient adds into the VGG input-path gradient
+          float yo[4];
+          load4<T>(yp, yo);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += yo[e];
+        }
+        store4<T>(yp, v);
       }
     }
   }
@@ -205,8 +221,8 @@ static int grid_for(int64_t groups, int waves_per_cu = 32) {
 }
 
 // Eligible launches (checked by run_conv): 2-byte type, one group, stride 1, 3×3 pad 1, identity
-// output placement, W % 16 == 0, and either (Cin 8 → Cout 64, epilogue = bias/act only) or
-// (Cin 64 → Cout 8, no epilogue).
+// output placement, W % 16 == 0, and either (Cin 8 → Cout 64, epilogue = bias + ReLU / PReLU: the
+// VGG and e4e input layers) or (Cin 64 → Cout 8, plain or accumulating: their input gradients).
 bool conv_thin_eligible(const ConvK& k, int dtype) {
   const char* e = getenv("MIA_CONV_THIN");  // tuning / A-B switch: 0 disables the thin kernels
   if (e && atoi(e) == 0) return false;
@@ -216,10 +232,9 @@ bool conv_thin_eligible(const ConvK& k, int dtype) {
       G.pad_x != 1 || G.ho != a.H || G.wo != a.W || G.ay != 1 || G.ax != 1 || G.by != 0 ||
       G.bx != 0 || a.shuffle_out || a.W % 16 != 0 || k.HT != a.H || k.WT != a.W ||
       k.ystride != a.Cout || a.act_in != MIA_ACT_NONE || a.in_scale || a.out_scale || a.noise ||
-      a.tap_a || a.mask_a || a.sdot || a.bab_demod || a.accumulate || !a.y || a.csum ||
-      a.act_out == MIA_ACT_PRELU)
+      a.tap_a || a.mask_a || a.sdot || a.bab_demod || !a.y || a.csum)
     return false;
-  if (a.Cin == 8 && a.Cout == 64 && G.kpad >= 96) return true;
+  if (a.Cin == 8 && a.Cout == 64 && G.kpad >= 96 && !a.accumulate) return true;
   if (a.Cin == 64 && a.Cout == 8 && !a.bias && a.act_out == MIA_ACT_NONE) return true;
   return false;
 }
@@ -232,13 +247,13 @@ int launch_conv_thin(ConvK& k, int dtype, hipStream_t st) {
       if (a.Cin == 8) {
         hipLaunchKernelGGL((conv_thin_in_kernel<T, 64>), dim3(grid), dim3(256), 0, st,
                            (const T*)a.x, (const T*)k.g[0].w, k.g[0].kpad, a.bias, a.act_out,
-                           (T*)a.y, a.N, a.H, a.W);
+                           a.act_slope, (T*)a.y, a.N, a.H, a.W);
       } else {
         const int64_t items = (int64_t)a.N * ((a.H + THIN_RS - 1) / THIN_RS) * (a.W / 16);
         const int lds = 4 * 2 * THIN_WBUF;
         hipLaunchKernelGGL((conv_thin_out_kernel<T, 8>), dim3(grid_for(items, 16)), dim3(256),
                            lds, st, (const T*)a.x, (const T*)k.g[0].w, k.g[0].kpad, (T*)a.y,
-                           a.N, a.H, a.W);
+                           a.accumulate, a.N, a.H, a.W);
       }
       return check_launch("conv_thin");
     }

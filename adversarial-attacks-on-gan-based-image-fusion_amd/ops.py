@@ -60,6 +60,13 @@ def conv_kpad(cin, dtype):
 # conv3x3 call is bracketed by HIP events on the launch stream and (start, end, algorithmic
 # FLOPs) is appended. None (default) = no events.
 PROFILE = None
+# Tuning aid (tools/layer_table.py): when a list, one label per PROFILE entry (API + shape).
+PROFILE_TAGS = None
+
+
+def _tag(label):
+    if PROFILE_TAGS is not None:
+        PROFILE_TAGS.append(label)
 
 
 def conv3x3(x, w, y, *, cout, act_in=ACT_NONE, in_scale=None, out_scale=None, bias=None,
@@ -124,6 +131,9 @@ def conv3x3(x, w, y, *, cout, act_in=ACT_NONE, in_scale=None, out_scale=None, bi
     if prof is not None:
         e1.record()
         prof.append((e0, e1, flops if flops is not None else 2 * N * H * W * 9 * Cin * cout))
+        _tag(f"conv3x3 {H}x{W} {Cin}->{cout}" + (" mod" if in_scale is not None else "")
+             + (" bab" if bab is not None else "") + (" sdot" if sdot is not None else "")
+             + (" tap" if tap_a is not None else "") + (" shuf" if shuffle_out else ""))
     return y
 
 
@@ -136,6 +146,7 @@ def _prof_call(name, flops, *args):
     if prof is not None:
         e1.record()
         prof.append((e0, e1, flops))
+        _tag(f"{name} {args[4:8] if name != 'mia_conv_s2_dgrad_halo' else ''}")
 
 
 def upconv_kpad(cin, phase, dtype):
@@ -674,6 +685,8 @@ def conv2d(x, groups, y, out_hw, *, cout, stride=1, bias=None, act_out=ACT_NONE,
     if prof is not None:
         e1.record()
         prof.append((e0, e1, flops if flops is not None else 2 * mac))
+        _tag(f"conv2d {H}x{W} {Cin}->{cout} s{stride} g{len(groups)} k{groups[0]['kh']}"
+             + (" mask" if mask_a is not None else "") + (" acc" if accumulate else ""))
     return y
 
 

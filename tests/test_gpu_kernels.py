@@ -607,11 +607,15 @@ def test_fused_backward_front_epilogue(cuda, dtype, N, H, Cin, Cout, up):
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 17, 16), (3, 16, 64)])
 @pytest.mark.parametrize("thin", ["1", "0"])
-def test_conv_thin_vgg_input_layer(cuda, monkeypatch, dtype, N, H, W, thin):
+@pytest.mark.parametrize("e4e", [False, True])
+def test_conv_thin_vgg_input_layer(cuda, monkeypatch, dtype, N, H, W, thin, e4e):
     """VGG conv1_1 forward (8-channel padded image → 64, bias, ReLU) and its input gradient
     (64 → 8 channels, 3 real) on the thin-channel kernels (conv_thin.hip; MIA_CONV_THIN=0 = the
-    implicit-GEMM tiles), against torch fp64 on the same rounded operands."""
+    implicit-GEMM tiles), against torch fp64 on the same rounded operands. e4e: the encoder's
+    input layer — bias + PReLU forward, gradient accumulated into an existing one (mia_conv2d)."""
     monkeypatch.setenv("MIA_CONV_THIN", thin)
+    if e4e:
+        return _thin_e4e_input_layer(cuda, dtype, N, H, W)
     g = torch.Generator().manual_seed(N * 100 + H + W)
     x = torch.zeros(N, 8, H, W)
     x[:, :3] = torch.rand(N, 3, H, W, generator=g) * 2 - 1
@@ -774,3 +778,41 @@ def test_conv2d_style_head_shapes(cuda, dtype, N, H, C, k, stride, mode):
     ops.conv2d(nhwc(x, dtype).to(cuda), grp, y, (ho, ho), cout=C, stride=stride, **kw)
     torch.cuda.synchronize()
     assert rel_err(nchw(y), ref) < 2 * TOL[dtype]
+
+
+def _thin_e4e_input_layer(cuda, dtype, N, H, W):
+    g = torch.Generator().manual_seed(N * 101 + H + W)
+    x = torch.zeros(N, 8, H, W)
+    x[:, :3] = torch.rand(N, 3, H, W, generator=g) * 2 - 1
+    wp = torch.zeros(64, 8, 3, 3)
+    wp[:, :3] = torch.randn(64, 3, 3, 3, generator=g) / math.sqrt(27)
+    b = torch.randn(64, generator=g) * 0.1
+    slope = torch.rand(64, generator=g) * 0.5 + 0.05
+    xq, wq = x.to(dtype).double(), wp.to(dtype).double()
+    pre = F.conv2d(xq, wq, b.double(), padding=1)
+    ref = torch.where(pre > 0, pre, slope.double().view(1, 64, 1, 1) * pre)
+    kp = ops.conv2d_kpad(9, 8, dtype)
+    wm = torch.zeros(64, kp)
+    wm[:, :72] = wp.permute(0, 2, 3, 1).reshape(64, 72)
+    y = torch.empty(N, H, W, 64, dtype=dtype, device=cuda)
+    ops.conv2d(nhwc(x, dtype).to(cuda), [dict(w=wm.to(dtype).to(cuda), kh=3, kw=3, pad=(1, 1),
+                                              ho=H, wo=W)], y, (H, W), cout=64, bias=b.to(cuda),
+               act_out=ops.ACT_PRELU, act_slope=slope.to(cuda))
+    # input gradient: g (64 ch) → 8 channels, accumulated onto gx0
+    gout = torch.randn(N, 64, H, W, generator=g)
+    gx0 = torch.randn(N, 8, H, W, generator=g)
+    gq = gout.to(dtype).double()
+    xx = torch.zeros(N, 8, H, W, dtype=torch.float64, requires_grad=True)
+    (gx_ref,) = torch.autograd.grad((F.conv2d(xx, wq, padding=1) * gq).sum(), xx)
+    gx_ref = gx_ref + gx0.to(dtype).double()
+    wd = wp.flip(2, 3).transpose(0, 1)  # (8, 64, 3, 3): the flipped, transposed kernel
+    kd = ops.conv2d_kpad(9, 64, dtype)
+    wdm = torch.zeros(8, kd)
+    wdm[:, :576] = wd.permute(0, 2, 3, 1).reshape(8, 576)
+    gx = nhwc(gx0, dtype).to(cuda)
+    ops.conv2d(nhwc(gout, dtype).to(cuda), [dict(w=wdm.to(dtype).to(cuda), kh=3, kw=3, pad=(1, 1),
+                                                 ho=H, wo=W)], gx, (H, W), cout=8,
+               accumulate=True)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(y), ref) < 2 * TOL[dtype]
+    assert rel_err(nchw(gx), gx_ref) < 2 * TOL[dtype]

@@ -46,7 +46,7 @@ __device__ __forceinline__ void wait_dma_steps(int steps) {
 }
 
 template <typename T, typename TL, bool PRO, bool SMALLC>
-__global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? 2 : 1) void conv_kernel(
+__global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 128 ? 4 : 2) : 1) void conv_kernel(
     const ConvK k) {
   typedef typename Vec<T>::type VT;
   constexpr int VEC = Vec<T>::N;
@@ -277,6 +277,7 @@ static int launch_tile(ConvK& k, hipStream_t st) {
 typedef Tile<2, 2, 4, 2, 2> Tile128x64;
 typedef Tile<2, 2, 4, 4, 2> Tile128x128;
 typedef Tile<4, 2, 4, 4, 3> Tile256x128;
+typedef Tile<2, 2, 2, 2, 2> Tile64x64;
 
 template <typename T, bool PRO, bool SMALLC>
 static int launch_bn(ConvK& k, hipStream_t st) {
@@ -288,6 +289,15 @@ static int launch_bn(ConvK& k, hipStream_t st) {
   const char* e = getenv("MIA_CONV_TILE");
   const int force = e ? atoi(e) : 0;
   if (k.a.Cout <= 64) return launch_tile<T, Tile128x64, PRO, SMALLC>(k, st);
+  // Launches with fewer 128x128 tiles than half the CUs (the e4e style heads at 4²…1² outputs,
+  // K = 9·512) run one block per CU and serialise each wave's LDS reads, MFMAs and the step
+  // barrier; 64x64 tiles put 4× the blocks (and waves) on the chip. MIA_CONV_SMALLTILE=0
+  // disables (A/B switch, read per launch).
+  const char* es = getenv("MIA_CONV_SMALLTILE");
+  int64_t tiles = 0;
+  for (int g = 0; g < k.ng; ++g) tiles += (k.g[g].m + 127) / 128;
+  tiles *= (k.a.Cout + 127) / 128;
+  if (!(es && atoi(es) == 0) && tiles < 128) return launch_tile<T, Tile64x64, PRO, SMALLC>(k, st);
   const int64_t big_blocks = (m / 256) * ((k.a.Cout + 127) / 128);
   if (force == 2 && big_blocks >= 512) return launch_tile<T, Tile256x128, PRO, SMALLC>(k, st);
   return launch_tile<T, Tile128x128, PRO, SMALLC>(k, st);

@@ -289,15 +289,16 @@ static int launch_bn(ConvK& k, hipStream_t st) {
   const char* e = getenv("MIA_CONV_TILE");
   const int force = e ? atoi(e) : 0;
   if (k.a.Cout <= 64) return launch_tile<T, Tile128x64, PRO, SMALLC>(k, st);
-  // Launches with fewer 128x128 tiles than half the CUs (the e4e style heads at 4²…1² outputs,
+  // Launches with fewer 128x128 tiles than 2 per CU (the e4e style heads at 8²…1² outputs,
   // K = 9·512) run one block per CU and serialise each wave's LDS reads, MFMAs and the step
-  // barrier; 64x64 tiles put 4× the blocks (and waves) on the chip. MIA_CONV_SMALLTILE=0
-  // disables (A/B switch, read per launch).
+  // barrier; 64x64 tiles put 4× the blocks (and waves) on the chip. MIA_CONV_SMALLTILE = the
+  // 128x128-tile count below which this applies (A/B switch, read per launch; 0 disables).
   const char* es = getenv("MIA_CONV_SMALLTILE");
   int64_t tiles = 0;
   for (int g = 0; g < k.ng; ++g) tiles += (k.g[g].m + 127) / 128;
   tiles *= (k.a.Cout + 127) / 128;
-  if (!(es && atoi(es) == 0) && tiles < 128) return launch_tile<T, Tile64x64, PRO, SMALLC>(k, st);
+  const int64_t small_below = es ? atoi(es) : 512;
+  if (tiles < small_below) return launch_tile<T, Tile64x64, PRO, SMALLC>(k, st);
   const int64_t big_blocks = (m / 256) * ((k.a.Cout + 127) / 128);
   if (force == 2 && big_blocks >= 512) return launch_tile<T, Tile256x128, PRO, SMALLC>(k, st);
   return launch_tile<T, Tile128x128, PRO, SMALLC>(k, st);

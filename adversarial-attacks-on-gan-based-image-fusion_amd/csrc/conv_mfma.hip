@@ -298,7 +298,9 @@ static int launch_bn(ConvK& k, hipStream_t st) {
   for (int g = 0; g < k.ng; ++g) tiles += (k.g[g].m + 127) / 128;
   tiles *= (k.a.Cout + 127) / 128;
   const int64_t small_below = es ? atoi(es) : 512;
-  if (tiles < small_below) return launch_tile<T, Tile64x64, PRO, SMALLC>(k, st);
+  // (2-byte types only: in fp32, the reference-precision path, a small image keeps one tile per
+  // image row block, so its sdot / csum sums stay single-atomic and run-to-run deterministic)
+  if (sizeof(T) == 2 && tiles < small_below) return launch_tile<T, Tile64x64, PRO, SMALLC>(k, st);
   const int64_t big_blocks = (m / 256) * ((k.a.Cout + 127) / 128);
   if (force == 2 && big_blocks >= 512) return launch_tile<T, Tile256x128, PRO, SMALLC>(k, st);
   return launch_tile<T, Tile128x128, PRO, SMALLC>(k, st);

@@ -195,7 +195,10 @@ def test_adam_mode_matches_oracle(cuda):
 @pytest.mark.parametrize("c", [1e-4, 10.0])
 def test_cw_mode_matches_oracle(cuda, c):
     """norm='l2_cw' (torchattacks C&W composed with the objective) vs the oracle restatement:
-    tanh space, Adam on w, best-L2 selection with success = objective below the clean image's."""
+    tanh space, Adam on w, best-L2 selection with success = objective below the clean image's.
+    At c = 1e-4 the success test is a near-tie: it needs the fp32 path to be run-to-run
+    deterministic (one sdot atomic per (image, channel) at 32², conv_mfma.hip keeps the 128-row
+    tiles in fp32), else a whole image may select a different iterate."""
     size, N, steps, lr = 32, 2, 4, 0.01
     eng, x0, t, (gp, vp, ep) = _engine(size, torch.float32, N, cuda, seed=6)
     adv = eng.run_cw(x0.to(cuda), t.to(cuda), steps, c=c, lr=lr).cpu()

@@ -77,13 +77,15 @@ def read_pmc(path, counter):
     return per
 
 
-def busy_union_ns(trace_path):
+def busy_union_ns(trace_path, pattern=None):
     """GPU-busy time of a kernel trace: the union of the dispatch intervals (the e4e style heads
-    run on side streams, so kernel durations overlap and their sum exceeds the busy time)."""
+    run on side streams, so kernel durations overlap and their sum exceeds the busy time).
+    pattern: only the kernels whose name it matches (the conv kernels: conv-busy time)."""
     iv = []
     with open(trace_path) as f:
         for r in csv.DictReader(f):
-            iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+            if pattern is None or pattern.search(r["Kernel_Name"]):
+                iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
     iv.sort()
     busy, (cs, ce) = 0, iv[0]
     for s0, e0 in iv[1:]:
@@ -119,10 +121,16 @@ def main():
     trace = a.stats.replace("kernel_stats.csv", "kernel_trace.csv")
     if trace != a.stats and os.path.exists(trace):
         busy = busy_union_ns(trace)
+        cbusy = busy_union_ns(trace, CONV)
         out["gpu_busy_ms_per_step_incl_setup"] = busy / 1e6 / a.steps
+        out["conv_kernel"]["busy_ms"] = cbusy / 1e6
+        out["conv_kernel"]["avg_busy_us_per_call"] = cbusy / conv_calls / 1e3
         lines += [f"GPU busy (union of dispatch intervals, incl. the one-off setup before the first "
                   f"step) {busy / 1e6 / a.steps:.1f} ms per step: kernels of the style-head side "
-                  f"streams overlap, so per-kernel times below sum to more than the busy time.", ""]
+                  f"streams overlap, so per-kernel times below sum to more than the busy time. "
+                  f"Conv-busy time (union of the conv dispatches) {cbusy / 1e6 / a.steps:.1f} ms "
+                  f"per step = {cbusy / conv_calls / 1e3:.1f} µs per conv API call (bench.py's "
+                  f"avg_launch_us is the same union over its HIP-event intervals).", ""]
     lines += [
              "| kernel | calls/step | ms/step | avg µs | share |", "|---|---|---|---|---|"]
     for n, c, t in sorted(rows, key=lambda r: -r[2]):

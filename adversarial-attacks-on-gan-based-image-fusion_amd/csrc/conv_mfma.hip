@@ -32,6 +32,7 @@
 // spans. The epilogue stages the fp32 tile through LDS and then works on 8-channel vectors
 // (16-byte loads of every aux operand, 16-byte stores).
 #include "conv_common.h"
+#include "halo_epilogue.h"
 
 namespace mia {
 
@@ -45,7 +46,10 @@ __device__ __forceinline__ void wait_dma_steps(int steps) {
   else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER) : "memory");
 }
 
-template <typename T, typename TL, bool PRO, bool SMALLC>
+// EPI: −2 = LDS-staged shared epilogue (conv_epilogue); ≥ 0 = the register epilogue specialised
+// for feature mask EPI (halo_epilogue_f; MFMAs computed transposed, D[channel][pixel]), for
+// single-image tiles of whole 16-pixel rows with identity placement (see reg_epi_ok).
+template <typename T, typename TL, bool PRO, bool SMALLC, int EPI = -2>
 __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 128 ? 4 : 2) : 1) void conv_kernel(
     const ConvK k) {
   typedef typename Vec<T>::type VT;
@@ -219,7 +223,9 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = mfma_chunk<T>(af[i], bf[j], acc[i][j]);
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = EPI == -2 ? mfma_chunk<T>(af[i], bf[j], acc[i][j])   // D[pixel][channel]
+                                : mfma_chunk<T>(bf[j], af[i], acc[i][j]);  // D[channel][pixel]
     }
     if constexpr (STAGES == 2) {
       __syncthreads();  // retires the DMA of step kb+1 (vmcnt(0)) and frees stage st
@@ -235,7 +241,11 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
   if constexpr (STAGES != 2) __syncthreads();
 
   // ---- epilogue ---------------------------------------------------------------------------
-  {
+  if constexpr (EPI >= 0) {
+    const int n_img = m0 / HWo;  // the whole tile is in this image (reg_epi_ok)
+    halo_epilogue_f<T, TL, EPI>(k, acc, n_img, (m0 - n_img * HWo) >> 4, 0, n0, wm, wn, lane,
+                                HWo >> 4, 16);
+  } else {
     const int last = min(m0 + BM, G.m) - 1;
     const int n_first_img = m0 / HWo;
     const bool single = n_first_img == last / HWo;
@@ -247,7 +257,7 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
   }
 }
 
-template <typename T, typename TL, bool PRO, bool SMALLC>
+template <typename T, typename TL, bool PRO, bool SMALLC, int EPI = -2>
 static int launch_tile(ConvK& k, hipStream_t st) {
   k.nbn = (k.a.Cout + TL::BN - 1) / TL::BN;
   int blk = 0;
@@ -262,7 +272,7 @@ static int launch_tile(ConvK& k, hipStream_t st) {
   lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
   lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
   if (lds > 160 * 1024) return set_error("conv: LDS budget exceeded");
-  auto fn = conv_kernel<T, TL, PRO, SMALLC>;
+  auto fn = conv_kernel<T, TL, PRO, SMALLC, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -278,6 +288,28 @@ typedef Tile<2, 2, 4, 2, 2> Tile128x64;
 typedef Tile<2, 2, 4, 4, 2> Tile128x128;
 typedef Tile<4, 2, 4, 4, 3> Tile256x128;
 typedef Tile<2, 2, 2, 2, 2> Tile64x64;
+
+// Register epilogue on the 128x128 tile: 2-byte types, one group, identity output placement,
+// every tile inside one image (HWo % 128 == 0), the feature masks of the heavy short-K launches
+// (the StyleGAN2 up-conv adjoint with its fused backward front; the e4e style-head convs).
+// MIA_CONV_REGEPI=0 disables (A/B switch, read per launch).
+static int reg_epi_mask(const ConvK& k, int bytes) {
+  const char* e = getenv("MIA_CONV_REGEPI");
+  if ((e && atoi(e) == 0) || bytes != 2 || k.ng != 1 || k.a.shuffle_out) return -1;
+  const ConvGroup& G = k.g[0];
+  if (G.ay != 1 || G.ax != 1 || G.by != 0 || G.bx != 0 || G.ho != k.HT || G.wo != k.WT ||
+      (G.ho * G.wo) % 128 != 0)
+    return -1;
+  using namespace epi;
+  const int f = epi_mask(k);
+  switch (f) {
+    case OSC | SDOT: case OSC | SDOT | ACC: case OSC | SDOT | BAB: case OSC | SDOT | ACC | BAB:
+    case BIAS | PRELU:
+      return f;
+    default:
+      return -1;
+  }
+}
 
 template <typename T, bool PRO, bool SMALLC>
 static int launch_bn(ConvK& k, hipStream_t st) {
@@ -301,6 +333,18 @@ static int launch_bn(ConvK& k, hipStream_t st) {
   // (2-byte types only: in fp32, the reference-precision path, a small image keeps one tile per
   // image row block, so its sdot / csum sums stay single-atomic and run-to-run deterministic)
   if (sizeof(T) == 2 && tiles < small_below) return launch_tile<T, Tile64x64, PRO, SMALLC>(k, st);
+  if constexpr (!SMALLC && !PRO) {
+    using namespace epi;
+    switch (reg_epi_mask(k, sizeof(T))) {
+      case OSC | SDOT: return launch_tile<T, Tile128x128, PRO, SMALLC, OSC | SDOT>(k, st);
+      case OSC | SDOT | ACC: return launch_tile<T, Tile128x128, PRO, SMALLC, OSC | SDOT | ACC>(k, st);
+      case OSC | SDOT | BAB: return launch_tile<T, Tile128x128, PRO, SMALLC, OSC | SDOT | BAB>(k, st);
+      case OSC | SDOT | ACC | BAB:
+        return launch_tile<T, Tile128x128, PRO, SMALLC, OSC | SDOT | ACC | BAB>(k, st);
+      case BIAS | PRELU: return launch_tile<T, Tile128x128, PRO, SMALLC, BIAS | PRELU>(k, st);
+      default: break;
+    }
+  }
   const int64_t big_blocks = (m / 256) * ((k.a.Cout + 127) / 128);
   if (force == 2 && big_blocks >= 512) return launch_tile<T, Tile256x128, PRO, SMALLC>(k, st);
   return launch_tile<T, Tile128x128, PRO, SMALLC>(k, st);

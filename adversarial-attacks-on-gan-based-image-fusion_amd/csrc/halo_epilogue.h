@@ -201,10 +201,12 @@ struct Raw4 {  // 4 consecutive elements of T, loaded raw (8 or 16 bytes)
 // The same operations as halo_epilogue for one feature mask F, straight-line: every aux load of
 // the tile is issued first (one wait instead of one per fragment — a wait also drains the stores
 // issued before it), then the arithmetic and the 16-byte stores.
+// (Hg, Wg): the output grid the rows index; default (p.H, p.W). The generic tile passes a virtual
+// grid of 16-pixel rows (HWo / 16, 16), so that its linear pixel rows use the same indexing.
 template <typename T, typename TL, int F>
 __device__ __forceinline__ void halo_epilogue_f(const ConvK& k, const f32x4 (&acc)[TL::FM][TL::FN],
                                                 int n, int y0, int x0, int n0, int wm, int wn,
-                                                int lane) {
+                                                int lane, int Hg = -1, int Wg = -1) {
   constexpr int FM = TL::FM, FN = TL::FN;
   constexpr bool OSC = F & epi::OSC, NOISE = F & epi::NOISE, BIAS = F & epi::BIAS;
   constexpr bool TAP = F & epi::TAP, MASK = F & epi::MASK, ACC = F & epi::ACC;
@@ -215,7 +217,7 @@ __device__ __forceinline__ void halo_epilogue_f(const ConvK& k, const f32x4 (&ac
   constexpr bool WIDE = sizeof(T) == 2 && FN % 2 == 0;
   typedef typename Raw4<T>::type R4;
   const mia_conv_args& p = k.a;
-  const int H = p.H, W = p.W, Cout = p.Cout;
+  const int H = Hg < 0 ? p.H : Hg, W = Hg < 0 ? p.W : Wg, Cout = p.Cout;
   const int px = lane & 15, lrow = lane >> 4;
   const int cl = n0 + wn * FN * 16 + (lrow << 2);
   T* __restrict__ Y = (T*)p.y;

@@ -146,7 +146,7 @@ def _prof_call(name, flops, *args):
     if prof is not None:
         e1.record()
         prof.append((e0, e1, flops))
-        _tag(f"{name} {args[4:8] if name != 'mia_conv_s2_dgrad_halo' else ''}")
+        _tag(f"{name} {args[4:7] if name != 'mia_conv_s2_dgrad_halo' else ''}")
 
 
 def upconv_kpad(cin, phase, dtype):

@@ -16,7 +16,9 @@
 //     pieces) before the next halo is issued into the buffer just released; each wave drains its
 //     DMA (vmcnt(0)) AFTER its MFMAs and BEFORE its epilogue stores, so the wait never covers
 //     stores and the DMA had a whole patch to land;
-//   * the epilogue is halo_epilogue (registers, 16-byte stores; every conv_args feature).
+//   * the epilogue is halo_epilogue_f (registers, 16-byte stores); a single per-pixel operand
+//     (mask or old y) is DMA'd into LDS at the start of the patch (WresAux) and lands during the
+//     MFMAs instead of stalling the epilogue.
 // Wave w owns patch rows 4w … 4w+3 (one 16-pixel MFMA fragment per row) × all 64 channels.
 #include "conv_common.h"
 #include "halo_epilogue.h"
@@ -29,7 +31,26 @@ struct WresTile {
   static constexpr int HPIECES = (HROWS + 7) / 8;                                    // 41
   static constexpr int HBUF = HPIECES * 8 * ROWB;
   static constexpr int H_INS = (HPIECES + NW - 1) / NW;                              // 11
+  static constexpr int AUXW = FM * 16 * ROWB;  // one per-pixel epilogue operand of a wave: 8 KB
 };
+
+// Per-pixel epilogue operand prefetched into LDS (a wave's 64 pixels × 64 channels): MASK →
+// mask_a, ACC → old y. Register prefetch spills next to the 288 resident weight VGPRs; LDS-DMA
+// costs no registers. The tap pair (TAP | MASK, VGG dgrad) still loads in the epilogue: with two
+// operands the epilogue's extra live registers spill the weights (measured in the ISA: reloads
+// with vmcnt(0) inside the MFMA loop).
+template <int EPI>
+struct WresAux {
+  static constexpr bool TAP = EPI & epi::TAP, MASK = (EPI & epi::MASK) && !TAP;
+  static constexpr bool ACC = EPI & epi::ACC;
+  static constexpr int N = TAP ? 0 : (MASK ? 1 : 0) + (ACC ? 1 : 0);
+  static_assert(N <= 1, "one prefetched operand per wave");
+  static_assert(!(EPI & (epi::SDOT | epi::BAB | epi::NOISE)), "not a weights-resident epilogue");
+};
+
+// bank swizzle of the prefetched operand rows (16-B chunk c of pixel q stored at c ^ asw(q)): a
+// ds_read_b64 of 16 pixels × one channel quad pair hits 16 distinct (pixel parity, chunk) slots
+__device__ __forceinline__ int asw(int q) { return (q >> 1) & 7; }
 
 // EPI: the epilogue feature mask (halo_epilogue.h, specialised only; see wres_mask_ok); wave wm
 // owns rows wm·FM …, wn = 0, n0 = 0
@@ -42,6 +63,7 @@ __global__ __launch_bounds__(256, 1) void conv_wres_kernel(const ConvK k) {
   constexpr int VEC = 8;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef WresAux<EPI> AUX;
   const mia_conv_args& p = k.a;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -96,6 +118,25 @@ __global__ __launch_bounds__(256, 1) void conv_wres_kernel(const ConvK k) {
     }
   };
 
+  // wave wid DMAs the epilogue operands of its 4 output rows (pieces of 8 pixels = 1 KB)
+  char* const auxw = smem + 2 * HBUF + wid * (AUX::N * TL::AUXW);  // this wave's operand slots
+  auto issue_aux = [&](int n, int y0, int x0) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const T* srcs[1] = {AUX::MASK ? (const T*)p.mask_a : (const T*)p.y};
+#pragma unroll
+    for (int t = 0; t < AUX::N; ++t)
+#pragma unroll
+      for (int j = 0; j < FM * 2; ++j) {
+        const int q = j * 8 + (ln >> 3);  // wave-local pixel: row q / 16, column q % 16
+        const int y = y0 + wid * FM + (q >> 4), x = x0 + (q & 15);
+        const T* src = srcs[t] + ((size_t)(n * H + y) * W + x) * 64 + ((ln & 7) ^ asw(q)) * VEC;
+        __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(auxw + t * TL::AUXW + j * 1024),
+                                         16, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);  // one address live at a time (weights fill the VGPRs)
+      }
+  };
+
   int tile = blockIdx.x;
   if (tile < ntiles) issue_halo(tile, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -105,6 +146,9 @@ __global__ __launch_bounds__(256, 1) void conv_wres_kernel(const ConvK k) {
     // of this patch (buffer buf is complete)
     __syncthreads();
     const int next = tile + gridDim.x;
+    int n, y0, x0;
+    tile_pos(tile, n, y0, x0);
+    if constexpr (AUX::N > 0) issue_aux(n, y0, x0);  // land during this patch's MFMAs
     if (next < ntiles) issue_halo(next, buf ^ 1);
     const char* ha = smem + buf * HBUF;
     // opaque pixel-row lane index: the 36 swizzled A-fragment addresses (lane-dependent XOR, no
@@ -135,11 +179,31 @@ __global__ __launch_bounds__(256, 1) void conv_wres_kernel(const ConvK k) {
             acc[i][j] = mfma_chunk<T>(wreg[t][h][j], af[i], acc[i][j]);  // D[channel][pixel]
       }
     }
-    // the next patch's halo was issued a whole patch ago: drain it now, before any store
+    // the next patch's halo (and this patch's epilogue operands) were issued a whole patch ago:
+    // drain them now, before any store
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int n, y0, x0;
-    tile_pos(tile, n, y0, x0);
-    halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, 0, wid, 0, lane);
+    if constexpr (AUX::N > 0) {
+      {
+        typedef typename Raw4<T>::type R4;
+        EpiRows<T, FM, FN> R;
+        const int px = lane & 15, lrow = lane >> 4;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int q = i * 16 + px;
+          R.nz[i] = R.bnz[i] = 0.f;
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            // channels 16j + 4·lrow … +3: chunk 2j + lrow/2, byte 8·(lrow & 1) within it
+            const int off = q * ROWB + (((2 * j + (lrow >> 1)) ^ asw(q)) << 4) + ((lrow & 1) << 3);
+            if constexpr (AUX::MASK) R.rma[i][j] = *(const R4*)(auxw + off);
+            if constexpr (AUX::ACC) R.ryo[i][j] = *(const R4*)(auxw + off);
+          }
+        }
+        halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, 0, wid, 0, lane, -1, -1, &R);
+      }
+    } else {
+      halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, 0, wid, 0, lane);
+    }
     buf ^= 1;
   }
 }
@@ -197,11 +261,13 @@ int launch_conv_wres(ConvK& k, int dtype, hipStream_t st) {
   const int grid = std::min(ntiles, ncu);
   k.nbn = 1;
   k.nblk = ntiles;
-  const size_t lds = 2 * (size_t)TL::HBUF;
   using namespace epi;
+  const int f = epi_mask(k);
+  const int naux = (f & TAP) ? 0 : ((f & MASK) ? 1 : 0) + ((f & ACC) ? 1 : 0);
+  const size_t lds = 2 * (size_t)TL::HBUF + (size_t)TL::NW * naux * TL::AUXW;
   MIA_DISPATCH_DTYPE(dtype, T, {
     if constexpr (sizeof(T) == 2) {
-      switch (epi_mask(k)) {
+      switch (f) {
         case BIAS | RELU: return launch_wres_<T, BIAS | RELU>(k, grid, lds, st);
         case TAP | MASK: return launch_wres_<T, TAP | MASK>(k, grid, lds, st);
         case 0: return launch_wres_<T, 0>(k, grid, lds, st);

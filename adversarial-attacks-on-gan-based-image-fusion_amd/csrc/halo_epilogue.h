@@ -201,12 +201,28 @@ struct Raw4 {  // 4 consecutive elements of T, loaded raw (8 or 16 bytes)
 // The same operations as halo_epilogue for one feature mask F, straight-line: every aux load of
 // the tile is issued first (one wait instead of one per fragment — a wait also drains the stores
 // issued before it), then the arithmetic and the 16-byte stores.
+// Per-pixel aux operands of FMC fragment rows (noise, stored activation, tap pair, mask, old y).
+template <typename T, int FMC, int FN>
+struct EpiRows {
+  typedef typename Raw4<T>::type R4;
+  float nz[FMC], bnz[FMC];
+  R4 rx[FMC][FN], rta[FMC][FN], rtt[FMC][FN], rma[FMC][FN], ryo[FMC][FN];
+};
+
+template <typename TL>
+struct EpiChunk {  // rows per aux-load chunk (bounds the live registers for tall wave tiles)
+  static constexpr int FMC = TL::FM < 4 ? TL::FM : 4;
+};
+
 // (Hg, Wg): the output grid the rows index; default (p.H, p.W). The generic tile passes a virtual
 // grid of 16-pixel rows (HWo / 16, 16), so that its linear pixel rows use the same indexing.
+// pre: the per-pixel operands of a single-chunk wave tile already gathered by the caller (the
+// weights-resident kernel prefetches them into LDS during its MFMAs); nullptr: loaded here.
 template <typename T, typename TL, int F>
-__device__ __forceinline__ void halo_epilogue_f(const ConvK& k, const f32x4 (&acc)[TL::FM][TL::FN],
-                                                int n, int y0, int x0, int n0, int wm, int wn,
-                                                int lane, int Hg = -1, int Wg = -1) {
+__device__ __forceinline__ void halo_epilogue_f(
+    const ConvK& k, const f32x4 (&acc)[TL::FM][TL::FN], int n, int y0, int x0, int n0, int wm,
+    int wn, int lane, int Hg = -1, int Wg = -1,
+    const EpiRows<T, EpiChunk<TL>::FMC, TL::FN>* pre = nullptr) {
   constexpr int FM = TL::FM, FN = TL::FN;
   constexpr bool OSC = F & epi::OSC, NOISE = F & epi::NOISE, BIAS = F & epi::BIAS;
   constexpr bool TAP = F & epi::TAP, MASK = F & epi::MASK, ACC = F & epi::ACC;
@@ -256,11 +272,21 @@ __device__ __forceinline__ void halo_epilogue_f(const ConvK& k, const f32x4 (&ac
     for (int e = 0; e < 4; ++e) part[j][e] = partq[j][e] = pcs[j][e] = 0.f;
   // rows in chunks of FMC (the aux loads of a chunk are hoisted together; chunks bound the live
   // registers for tall wave tiles)
-  constexpr int FMC = FM < 4 ? FM : 4;
+  constexpr int FMC = EpiChunk<TL>::FMC;
 #pragma unroll
   for (int i0 = 0; i0 < FM; i0 += FMC) {
-  float nz[FMC], bnz[FMC];
-  R4 rx[FMC][FN], rta[FMC][FN], rtt[FMC][FN], rma[FMC][FN], ryo[FMC][FN];
+  EpiRows<T, FMC, FN> Rl;
+  const bool have = pre != nullptr && FMC == FM;
+  // the caller's operands by reference (a copy would double their registers)
+  EpiRows<T, FMC, FN>& R = have ? *const_cast<EpiRows<T, FMC, FN>*>(pre) : Rl;
+  float(&nz)[FMC] = R.nz;
+  float(&bnz)[FMC] = R.bnz;
+  R4(&rx)[FMC][FN] = R.rx;
+  R4(&rta)[FMC][FN] = R.rta;
+  R4(&rtt)[FMC][FN] = R.rtt;
+  R4(&rma)[FMC][FN] = R.rma;
+  R4(&ryo)[FMC][FN] = R.ryo;
+  if (!have) {
 #pragma unroll
   for (int i = 0; i < FMC; ++i) {
     const int y = y0 + wm * FM + i0 + i, x = x0 + px;
@@ -287,6 +313,7 @@ __device__ __forceinline__ void halo_epilogue_f(const ConvK& k, const f32x4 (&ac
     }
   }
 
+  }  // !have
 #pragma unroll
   for (int i = 0; i < FMC; ++i) {
     const int m = (n * H + y0 + wm * FM + i0 + i) * W + x0 + px;

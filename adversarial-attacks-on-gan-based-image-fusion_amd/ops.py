@@ -396,6 +396,18 @@ def mse_sum(a, b, loss, coef=1.0):
     return loss
 
 
+def ssim(ref, imgs, data_range, work, out):
+    """mia_ssim: ref (3,H,W), imgs (N,3,H,W) fp32 → out[n] = SSIM(gray(ref), gray(imgs[n]))."""
+    N, _, H, W = imgs.shape
+    _need(ref, (3, H, W), torch.float32, "ref")
+    _need(imgs, (N, 3, H, W), torch.float32, "imgs")
+    _numel_ok(work, N, torch.float64, "work")
+    _numel_ok(out, N, torch.float32, "out")
+    call("mia_ssim", ptr(ref), ptr(imgs), N, H, W, float(data_range), ptr(work), ptr(out),
+         stream())
+    return out
+
+
 def mse_grad_f32(a, b, g, coef, accumulate=False):
     _need(b, a.shape, torch.float32, "b")
     _need(g, a.shape, torch.float32, "g")

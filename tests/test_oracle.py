@@ -162,3 +162,22 @@ def test_oracle_adam_and_cw_modes_basic_properties():
     assert torch.isfinite(cw).all() and cw.abs().max() < 1.0
     # the selected image is one of the iterates within lr-sized steps of x0 (or x0 itself)
     assert (cw - x0).abs().max() <= 2 * 0.01 + 1e-6
+
+
+def test_ssim_oracle_filter_form_matches_window_loops():
+    """oracle/metrics_ref.structural_similarity (skimage's filter-and-crop form) equals the
+    explicit 7×7-window definition, is 1 on identical images, symmetric, and < 1 otherwise."""
+    from oracle import metrics_ref
+    rng = np.random.default_rng(7)
+    for H, W in ((7, 7), (12, 13), (20, 9)):
+        x = rng.uniform(-1, 1, (H, W))
+        y = np.clip(x + rng.normal(0, 0.2, (H, W)), -1, 1)
+        s = metrics_ref.structural_similarity(x, y)
+        assert abs(s - metrics_ref.ssim_direct(x, y)) < 1e-12
+        assert abs(s - metrics_ref.structural_similarity(y, x)) < 1e-12
+        assert s < 1.0
+        assert abs(metrics_ref.structural_similarity(x, x) - 1.0) < 1e-12
+    img = rng.uniform(-1, 1, (3, 16, 16))
+    g = metrics_ref.rgb2gray(img)
+    assert np.allclose(g, 0.2125 * img[0] + 0.7154 * img[1] + 0.0721 * img[2])
+    assert abs(metrics_ref.cal_ssmi(img, img) - 1.0) < 1e-12

@@ -1,0 +1,3 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_metrics.py > gpurun_out/t_metrics.log 2>&1 && echo metrics-ok

@@ -12,7 +12,7 @@ Submodules import lazily so the package can be imported (and the library inspect
 without a GPU; any compute call without the library or a GPU raises.
 """
 __all__ = ["attack", "fgsm", "build_net", "vgg16", "get_latents", "StyleFusionSimple",
-           "interpolation", "attack_distributed"]
+           "interpolation", "partial_adv_fusion_arithmetic", "attack_distributed"]
 
 
 def __getattr__(name):
@@ -23,7 +23,7 @@ def __getattr__(name):
                 "MappingNet"):
         from . import networks as _n
         return getattr(_n, name)
-    if name in ("StyleFusionSimple", "interpolation"):
+    if name in ("StyleFusionSimple", "interpolation", "partial_adv_fusion_arithmetic"):
         from . import style_fusion_simple as _f
         return getattr(_f, name)
     if name == "attack_distributed":

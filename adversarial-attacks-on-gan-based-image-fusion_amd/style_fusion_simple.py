@@ -154,3 +154,26 @@ def interpolation(drawer, all_latents, feature_idx=-1):
         I_all.append(img)
         feats.append(inner[feature_idx].float().clone())
     return I_fused, torch.cat(I_all, dim=0), torch.cat(feats, dim=0)
+
+
+def partial_adv_fusion_arithmetic(drawer, inputs, adv_inputs, all_latents, all_adv_latents):
+    """Partial-fusion sweep (interpolation.py:921-977): for j = 0 … M−1 the arithmetic fusion with
+    only latent j replaced by its adversarial one, then with all of them replaced. Returns the
+    M + 1 fused images (M+1, 3, S, S) in that order. The image files of ``args.save_img`` are I/O
+    and out of scope; ``inputs`` / ``adv_inputs`` only feed those files in the reference, so they
+    are checked for shape and otherwise unused."""
+    M = all_adv_latents.shape[0]
+    if tuple(all_latents.shape) != tuple(all_adv_latents.shape):
+        raise ValueError("all_latents and all_adv_latents must have the same shape")
+    if inputs is not None and adv_inputs is not None and inputs.shape[0] != adv_inputs.shape[0]:
+        raise ValueError("inputs and adv_inputs must hold the same images")
+    out = []
+    for j in range(M + 1):
+        if j < M:
+            lat = all_latents.clone()
+            lat[j] = all_adv_latents[j]
+        else:
+            lat = all_adv_latents.clone()
+        fused, _, _ = interpolation(drawer, lat, feature_idx=-1)
+        out.append(fused)
+    return torch.cat(out, dim=0)

@@ -290,6 +290,17 @@ def test_style_fusion_simple_api(cuda):
                                     .repeat(1, 14, 1), 256)
     assert rel_err(fused, ref_f) < 1e-4
     assert fe.shape[0] == 3
+    # partial-fusion sweep (interpolation.py:921-977): one adversarial latent at a time, then all
+    from gfa_amd import partial_adv_fusion_arithmetic
+    Wa = W + 0.05 * torch.randn(W.shape, generator=torch.Generator().manual_seed(3)).to(cuda)
+    sweep = partial_adv_fusion_arithmetic(drawer, None, None, W, Wa)
+    assert tuple(sweep.shape) == (4, 3, 256, 256)
+    for j in range(3):
+        lat = W.clone()
+        lat[j] = Wa[j]
+        assert torch.equal(sweep[j:j + 1], interpolation(drawer, lat)[0])
+    assert torch.equal(sweep[3:4], interpolation(drawer, Wa)[0])
+    assert not torch.equal(sweep[0], fused[0])
 
 
 def test_cfg1_fusion_pair_fgsm(cuda):

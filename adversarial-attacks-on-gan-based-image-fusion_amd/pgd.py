@@ -224,7 +224,9 @@ class AttackEngine:
         sq = ws.get("cw.sq", (N,), f32)
         prev = 1e10
         every = max(steps // 10, 1)
+        self.cw_steps_run = 0  # iterations executed (early stop), for bench.py's report
         for step in range(steps):
+            self.cw_steps_run = step + 1
             ops.cw_tanh(w, adv)
             ops.zero_(f)
             self._full_grad(adv, g, loss=f)

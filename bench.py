@@ -51,6 +51,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-steps", type=int, default=10)
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--norm", default="linf", choices=["linf", "l2_cw"],
+                    help="linf = PGD L∞ (the headline); l2_cw = C&W-L2 with the VGG perceptual "
+                         "objective (BASELINE config #5 at --size 1024 --dtype fp16), c = 1e-4, "
+                         "lr = 0.01, --pgd-steps iterations with the reference's early stop")
     ap.add_argument("--encoder", default="e4e", choices=["e4e", "linear"],
                     help="e4e = Encoder4Editing(50,'ir_se'), the reference's net.encoder "
                          "(code/utils/model_utils.py:24; default); linear = the SURVEY.md §7 "
@@ -138,8 +142,14 @@ def main():
     eps, alpha = 8 / 255, 2 / 255
     n_total = B * world
 
+    cw_runs = []
+
     def one_step():
-        adv = eng.run(x0, tgt, args.pgd_steps, eps, alpha)
+        if args.norm == "l2_cw":
+            adv = eng.run_cw(x0, tgt, args.pgd_steps, c=1e-4, lr=0.01)
+            cw_runs.append(eng.cw_steps_run)
+        else:
+            adv = eng.run(x0, tgt, args.pgd_steps, eps, alpha)
         if world > 1:
             gather_shards(adv, n_total)
         return adv
@@ -168,12 +178,17 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
     ms = elapsed / args.steps * 1e3
+    timed_cw = cw_runs[args.warmup:]
+    iters = sum(timed_cw) / len(timed_cw) if timed_cw else args.pgd_steps
     value = n_total * args.steps / elapsed
     flops_img_step = pgd.algorithmic_flops_per_image_step(eng.G, eng.V, eng.E)
     out = {
-        "metric": METRIC if (S, args.pgd_steps) == (256, 20) else
-                  f"attacked images/sec, PGD-{args.pgd_steps} L∞ ε=8/255 at {S}², "
-                  f"{world} MI355X (non-headline config)",
+        "metric": METRIC if (S, args.pgd_steps, args.norm) == (256, 20, "linf") else
+                  (f"attacked images/sec, PGD-{args.pgd_steps} L∞ ε=8/255 at {S}², "
+                   if args.norm == "linf" else
+                   f"attacked images/sec, C&W-L2 (c=1e-4, lr=0.01, ≤{args.pgd_steps} iterations, "
+                   f"early stop) with the VGG perceptual objective at {S}², ")
+                  + f"{world} MI355X (non-headline config)",
         "value": value, "unit": "attacked images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": DT_NAME[args.dtype],
@@ -181,13 +196,17 @@ def main():
                 f"({S}², cm=2), VGG16 trunk and "
                 + ("e4e Encoder4Editing(50,'ir_se')" if args.encoder == "e4e"
                    else "linear stand-in encoder") + " (no checkpoints offline)",
-        "config": {"workload": f"PGD-{args.pgd_steps} L∞ eps=8/255 alpha=2/255 at {S}², "
-                               f"{B} images/GPU (BASELINE config #4 per-GPU share), "
+        "config": {"workload": (f"PGD-{args.pgd_steps} L∞ eps=8/255 alpha=2/255" if args.norm ==
+                                "linf" else f"C&W-L2 ≤{args.pgd_steps} iterations") + f" at {S}², "
+                               f"{B} images/GPU"
+                               + (" (BASELINE config #4 per-GPU share)" if (S, B) == (256, 128)
+                                  else "") + ", "
                                f"RCCL all-gather of outputs when N>1",
-                   "encoder": args.encoder, "images_per_gpu": B, "global_batch": n_total, "size": S,
+                   "encoder": args.encoder, "norm": args.norm, "images_per_gpu": B, "global_batch": n_total, "size": S,
                    "pgd_steps": args.pgd_steps, "parallelism": f"dp{world}",
+                   **({"cw_iterations_run": timed_cw} if timed_cw else {}),
                    "algorithmic_gflop_per_image_step": flops_img_step / 1e9,
-                   "effective_tflops": flops_img_step * B * args.pgd_steps * world
+                   "effective_tflops": flops_img_step * B * iters * world
                    / (elapsed / args.steps) / 1e12,
                    "peak_hbm_gb_per_gpu": torch.cuda.max_memory_allocated(dev) / 1e9},
     }

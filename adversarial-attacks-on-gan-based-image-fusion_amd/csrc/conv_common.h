@@ -22,6 +22,10 @@ struct ConvK {
   int stride, HT, WT, ystride, cout_mod, log2cin, n_first_max, ng, nblk, nbn;
   int stagger_blocks;            // halo kernel: blocks of the first dispatch wave …
   unsigned stagger_cycles;       // … of which every other one starts this many clocks late
+  int prered;                    // register epilogues: pre-reduce the sums across the M waves in
+                                 // LDS before the atomics; on for the channel sum (SE pool) only:
+                                 // measured, the extra barrier costs more than it saves for the
+                                 // sdot / q sums of the StyledConv dgrads (MIA_EPI_PRERED=0: off)
   ConvGroup g[4];
 };
 
@@ -48,6 +52,12 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
 // conflict-free only for windows starting at row ≡ 0, 1 mod 4, which the halo kernel's
 // tap-shifted reads do not respect).
 __device__ __forceinline__ int fsw(int row) { return ((row >> 1) & 3) << 1; }
+
+// MIA_EPI_PRERED=0 turns the register epilogues' LDS pre-reduction off (A/B switch, per launch)
+inline int prered_enabled() {
+  const char* e = getenv("MIA_EPI_PRERED");
+  return e ? atoi(e) != 0 : 1;
+}
 
 __device__ __forceinline__ int div_kw(int t, int kw) {
   return kw == 3 ? (t * 11) >> 5 : (kw == 2 ? t >> 1 : t);  // exact for t < 9

@@ -281,7 +281,9 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
   }
   HT_STAMP(t_loop);
   if constexpr (EPI >= 0) {
-    halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, n0, wm, wn, lane);
+    // (the LDS is idle after the main loop's last barrier: the pre-reduction reuses it)
+    halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, n0, wm, wn, lane, -1, -1, nullptr,
+                                k.prered ? (float*)smem : nullptr, TL::WM, TL::BN);
   } else if constexpr (EPI == -1) {
 #if defined(MIA_HALO_STOREONLY)  // tuning experiment: raw accumulator stores only (wrong results)
     if constexpr (sizeof(T) == 2 && FN % 2 == 0) {
@@ -376,6 +378,7 @@ static int launch_halo_tile_(ConvK& k, hipStream_t st) {
   const char* es = getenv("MIA_HALO_STAGGER");  // clocks; tuning / A-B switch
   k.stagger_cycles = es ? (unsigned)atoi(es) : 0u;
   if (k.nblk < 4 * k.stagger_blocks) k.stagger_cycles = 0;  // short launches: not worth a tail
+  k.prered = prered_enabled() && EPI >= 0 && (EPI & epi::CSUM);
   hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), lds, st, k);
   return check_launch("conv_halo");
 }

@@ -244,7 +244,8 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
   if constexpr (EPI >= 0) {
     const int n_img = m0 / HWo;  // the whole tile is in this image (reg_epi_ok)
     halo_epilogue_f<T, TL, EPI>(k, acc, n_img, (m0 - n_img * HWo) >> 4, 0, n0, wm, wn, lane,
-                                HWo >> 4, 16);
+                                HWo >> 4, 16, nullptr, k.prered ? (float*)smem : nullptr, TL::WM,
+                                TL::BN);
   } else {
     const int last = min(m0 + BM, G.m) - 1;
     const int n_first_img = m0 / HWo;
@@ -280,6 +281,7 @@ static int launch_tile(ConvK& k, hipStream_t st) {
       return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     attr_set = true;
   }
+  k.prered = prered_enabled() && EPI >= 0 && (EPI & epi::CSUM);
   hipLaunchKernelGGL(fn, dim3(blk), dim3(TL::NT), lds, st, k);
   return check_launch("conv");
 }

@@ -120,6 +120,8 @@ __global__ __launch_bounds__(256, 1) void conv_wres_kernel(const ConvK k) {
 
   // wave wid DMAs the epilogue operands of its 4 output rows (pieces of 8 pixels = 1 KB)
   char* const auxw = smem + 2 * HBUF + wid * (AUX::N * TL::AUXW);  // this wave's operand slots
+  // sdot / q / csum pre-reduction of the 4 waves (each covers all 64 channels of its rows)
+  float* const red = k.prered ? (float*)(smem + 2 * HBUF + NW * AUX::N * TL::AUXW) : nullptr;
   auto issue_aux = [&](int n, int y0, int x0) {
     int ln = lane;
     asm volatile("" : "+v"(ln));
@@ -199,10 +201,11 @@ __global__ __launch_bounds__(256, 1) void conv_wres_kernel(const ConvK k) {
             if constexpr (AUX::ACC) R.ryo[i][j] = *(const R4*)(auxw + off);
           }
         }
-        halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, 0, wid, 0, lane, -1, -1, &R);
+        halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, 0, wid, 0, lane, -1, -1, &R, red, NW, 64);
       }
     } else {
-      halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, 0, wid, 0, lane);
+      halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, 0, wid, 0, lane, -1, -1, nullptr, red, NW,
+                                  64);
     }
     buf ^= 1;
   }
@@ -264,7 +267,8 @@ int launch_conv_wres(ConvK& k, int dtype, hipStream_t st) {
   using namespace epi;
   const int f = epi_mask(k);
   const int naux = (f & TAP) ? 0 : ((f & MASK) ? 1 : 0) + ((f & ACC) ? 1 : 0);
-  const size_t lds = 2 * (size_t)TL::HBUF + (size_t)TL::NW * naux * TL::AUXW;
+  const size_t lds = 2 * (size_t)TL::HBUF + (size_t)TL::NW * naux * TL::AUXW + 3 * TL::NW * 64 * 4;
+  k.prered = prered_enabled() && (f & CSUM);
   MIA_DISPATCH_DTYPE(dtype, T, {
     if constexpr (sizeof(T) == 2) {
       switch (f) {

@@ -222,7 +222,8 @@ template <typename T, typename TL, int F>
 __device__ __forceinline__ void halo_epilogue_f(
     const ConvK& k, const f32x4 (&acc)[TL::FM][TL::FN], int n, int y0, int x0, int n0, int wm,
     int wn, int lane, int Hg = -1, int Wg = -1,
-    const EpiRows<T, EpiChunk<TL>::FMC, TL::FN>* pre = nullptr) {
+    const EpiRows<T, EpiChunk<TL>::FMC, TL::FN>* pre = nullptr, float* red = nullptr, int nwm = 1,
+    int cw = 0) {
   constexpr int FM = TL::FM, FN = TL::FN;
   constexpr bool OSC = F & epi::OSC, NOISE = F & epi::NOISE, BIAS = F & epi::BIAS;
   constexpr bool TAP = F & epi::TAP, MASK = F & epi::MASK, ACC = F & epi::ACC;
@@ -395,10 +396,45 @@ __device__ __forceinline__ void halo_epilogue_f(
           if constexpr (BAB) b += __shfl_xor(b, o, 64);
           if constexpr (CSUM) cs += __shfl_xor(cs, o, 64);
         }
-        if (px == 0 && c < Cout) {
+        if (red != nullptr && nwm > 1) {  // (quantity, wave row, block channel) in LDS
+          if (px == 0) {
+            const int lc = c - n0 + e;
+            int qi = 0;
+            if constexpr (SDOT) red[(qi++ * nwm + wm) * cw + lc] = a;
+            if constexpr (BAB) red[(qi++ * nwm + wm) * cw + lc] = b;
+            if constexpr (CSUM) red[(qi++ * nwm + wm) * cw + lc] = cs;
+          }
+        } else if (px == 0 && c < Cout) {
           if constexpr (SDOT) atomicAdd(&p.sdot[(size_t)n * Cout + c + e], a);
           if constexpr (BAB) atomicAdd(&p.bab_q[(size_t)n * Cout + c + e], b);
           if constexpr (CSUM) atomicAdd(&p.csum[(size_t)n * Cout + c + e], cs);
+        }
+      }
+    }
+    if (red != nullptr && nwm > 1) {
+      // the waves of one channel range meet here; the first wave row sums them and issues one
+      // atomic per channel (nwm× fewer atomics)
+      __syncthreads();
+      if (wm == 0 && px == 0) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int c = cl + 16 * j;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (c >= Cout) continue;
+            const int lc = c - n0 + e;
+            int qi = 0;
+            float* dst[3] = {SDOT ? p.sdot : nullptr, BAB ? p.bab_q : nullptr,
+                             CSUM ? p.csum : nullptr};
+#pragma unroll
+            for (int qq = 0; qq < 3; ++qq) {
+              if (dst[qq] == nullptr) continue;
+              float t = 0.f;
+              for (int w = 0; w < nwm; ++w) t += red[(qi * nwm + w) * cw + lc];
+              atomicAdd(&dst[qq][(size_t)n * Cout + c + e], t);
+              ++qi;
+            }
+          }
         }
       }
     }

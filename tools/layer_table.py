@@ -27,9 +27,11 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--pgd-steps", type=int, default=20)
     ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16"])
     a = ap.parse_args()
     dev = torch.device("cuda:0")
-    T, S, B = torch.float16, 256, a.batch
+    T, S, B = bench.DT[a.dtype], a.size, a.batch
     enc = E4EEncoder(bench.encoder_weights("e4e", S), S, dtype=T, device=dev)
     eng = pgd.AttackEngine(enc, SynthesisNet(make_generator_weights(S, seed=0), S, dtype=T,
                                              device=dev), VGGNet(make_vgg_weights(1234), dtype=T,

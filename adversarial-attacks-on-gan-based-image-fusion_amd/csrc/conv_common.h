@@ -453,6 +453,8 @@ bool conv_wres_eligible(const ConvK& k, int dtype);
 int launch_conv_wres(ConvK& k, int dtype, hipStream_t st);
 // thin-channel layers: VGG conv1_1 forward and its input gradient (conv_thin.hip)
 bool conv_thin_eligible(const ConvK& k, int dtype);
+bool conv_thin32_eligible(const ConvK& k, int dtype);
+int launch_conv_thin32(ConvK& k, int dtype, hipStream_t st);
 int launch_conv_thin(ConvK& k, int dtype, hipStream_t st);
 
 }  // namespace mia

@@ -411,6 +411,7 @@ static int run_conv(ConvK& k, int dtype, hipStream_t st) {
   k.n_first_max = std::min(a.N, (256 + hw_min - 1) / hw_min + 1);
 
   if (conv_thin_eligible(k, dtype)) return launch_conv_thin(k, dtype, st);
+  if (conv_thin32_eligible(k, dtype)) return launch_conv_thin32(k, dtype, st);
   if (conv_wres_eligible(k, dtype)) return launch_conv_wres(k, dtype, st);
   if (conv_halo_eligible(k, dtype)) return launch_conv_halo(k, dtype, st);
   MIA_DISPATCH_DTYPE(dtype, T, return launch_conv<T>(k, st));

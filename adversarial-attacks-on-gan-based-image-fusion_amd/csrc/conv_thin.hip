@@ -15,6 +15,7 @@
 //   * the gradient kernel stages each input pixel once per wave work item in LDS (9 taps read it);
 //   * waves stride over the pixel groups / work items.
 #include "conv_common.h"
+#include "halo_epilogue.h"
 
 namespace mia {
 
@@ -208,6 +209,107 @@ __global__ __launch_bounds__(256) void conv_thin_out_kernel(const T* __restrict_
   }
 }
 
+// ---- 32 → 32-channel stride-1 3×3 layers (StyleGAN2 1024² StyledConvs, cm = 2) ----------------
+// K = 9 taps × 32 channels: ONE MFMA 16×16×32 K-chunk per tap. The wave holds all 9 × 2 weight
+// fragments in VGPRs (72 registers) and walks a contiguous run of 16-pixel groups (one image row
+// segment each): per tap one 16-byte A gather per lane straight from global memory (the
+// neighbours' re-reads hit L1 / L2), the optional modulation x·s[n][ci] on the fragment (PRO, the
+// StyledConv forward), 2 MFMAs → D[channel][pixel]; the epilogue is the specialised register
+// epilogue (halo_epilogue_f, FM = 1, FN = 2). The sdot / q / csum partials stay in registers over
+// the run and are flushed (shuffles + one atomic per channel) when the image changes.
+struct Thin32Tile {
+  static constexpr int FM = 1, FN = 2;
+};
+
+// the reductions of image n: the 16 pixel lanes by shuffles, then one atomic per channel
+template <int EPI>
+__device__ __forceinline__ void thin32_flush(const mia_conv_args& p, EpiSums<2>& sums, int n,
+                                             int frow, int fq) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float a = sums.part[j][e], b = sums.partq[j][e], cs = sums.pcs[j][e];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        if constexpr ((EPI & epi::SDOT) != 0) a += __shfl_xor(a, o, 64);
+        if constexpr ((EPI & epi::BAB) != 0) b += __shfl_xor(b, o, 64);
+        if constexpr ((EPI & epi::CSUM) != 0) cs += __shfl_xor(cs, o, 64);
+      }
+      const int c = 16 * j + 4 * fq + e;
+      if (frow == 0) {
+        if constexpr ((EPI & epi::SDOT) != 0) atomicAdd(&p.sdot[(size_t)n * 32 + c], a);
+        if constexpr ((EPI & epi::BAB) != 0) atomicAdd(&p.bab_q[(size_t)n * 32 + c], b);
+        if constexpr ((EPI & epi::CSUM) != 0) atomicAdd(&p.csum[(size_t)n * 32 + c], cs);
+      }
+      sums.part[j][e] = sums.partq[j][e] = sums.pcs[j][e] = 0.f;
+    }
+}
+
+template <typename T, bool PRO, int EPI>
+__global__ __launch_bounds__(256) void conv_thin32_kernel(const ConvK k) {
+  typedef typename Vec<T>::type VT;
+  typedef Thin32Tile TL;
+  constexpr bool RED = (EPI & (epi::SDOT | epi::BAB | epi::CSUM)) != 0;
+  const mia_conv_args& p = k.a;
+  const int lane = threadIdx.x & 63, frow = lane & 15, fq = lane >> 4;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
+  const int H = p.H, W = p.W;
+  const T* __restrict__ X = (const T*)p.x;
+  const T* __restrict__ Wt = (const T*)k.g[0].w;
+  const int kpad = k.g[0].kpad;
+  VT wr[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) wr[t][j] = *(const VT*)(Wt + (size_t)(16 * j + frow) * kpad + t * 32 + fq * 8);
+  const bool lrelu_in = p.act_in == MIA_ACT_LRELU_S2;
+  const int gpr = W / 16, gpi = H * gpr;
+  const int64_t ngroups = (int64_t)p.N * gpi;
+  // contiguous run of groups per wave (stays inside one image for the reductions)
+  const int64_t per = (ngroups + nwaves - 1) / nwaves;
+  const int64_t g0 = (int64_t)wave * per, g1 = g0 + per < ngroups ? g0 + per : ngroups;
+  EpiSums<TL::FN> sums;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sums.part[j][e] = sums.partq[j][e] = sums.pcs[j][e] = 0.f;
+  int cur_n = -1;
+  VT sv;
+  for (int64_t g = g0; g < g1; ++g) {
+    const int n = (int)(g / gpi);
+    const int rem = (int)(g - (int64_t)n * gpi);
+    const int y = rem / gpr, x0 = (rem - y * gpr) * 16;
+    if (n != cur_n) {
+      if constexpr (RED) {
+        if (cur_n >= 0) thin32_flush<EPI>(p, sums, cur_n, frow, fq);
+      }
+      cur_n = n;
+      if constexpr (PRO) {
+        const float mul = lrelu_in ? SQRT2 : 1.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sv[e] = from_f<T>(p.in_scale[(size_t)n * 32 + fq * 8 + e] * mul);
+      }
+    }
+    f32x4 acc[1][2] = {{f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}}};
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int sy = y + t / 3 - 1, sx = x0 + frow + t % 3 - 1;
+      const bool ok = sy >= 0 && sy < H && sx >= 0 && sx < W;
+      VT a = ld16_or_zero<T>(X + ((size_t)(n * H + (ok ? sy : 0)) * W + (ok ? sx : 0)) * 32 + fq * 8,
+                             ok);
+      if constexpr (PRO) modulate<T>(a, sv, lrelu_in);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[0][j] = mfma_chunk<T>(wr[t][j], a, acc[0][j]);
+    }
+    halo_epilogue_f<T, TL, EPI>(k, acc, n, y, x0, 0, 0, 0, lane, -1, -1, nullptr, nullptr, 1, 0,
+                                RED ? &sums : nullptr);
+  }
+  if constexpr (RED) {
+    if (cur_n >= 0) thin32_flush<EPI>(p, sums, cur_n, frow, fq);
+  }
+}
+
 static int grid_for(int64_t groups, int waves_per_cu = 32) {
   static int ncu = 0;
   if (!ncu) {
@@ -218,6 +320,66 @@ static int grid_for(int64_t groups, int waves_per_cu = 32) {
   }
   const int64_t waves = std::min<int64_t>(groups, (int64_t)ncu * waves_per_cu);
   return (int)std::max<int64_t>(1, (waves + 3) / 4);
+}
+
+// 32 → 32 layers: 2-byte type, one group, stride 1, 3×3 pad 1, identity placement, W % 16 == 0,
+// an epilogue feature mask with a specialisation (the StyledConv forward and input gradient).
+// MIA_CONV_THIN32=0 disables (A/B switch, read per launch).
+static bool thin32_mask_ok(int f, bool pro) {
+  using namespace epi;
+  if (pro) return f == (OSC | NOISE | BIAS | LRELU);
+  switch (f) {
+    case OSC | SDOT: case OSC | SDOT | ACC: case OSC | SDOT | BAB: case OSC | SDOT | ACC | BAB:
+    case 0: case ACC:
+      return true;
+    default:
+      return false;
+  }
+}
+
+bool conv_thin32_eligible(const ConvK& k, int dtype) {
+  const char* e = getenv("MIA_CONV_THIN32");
+  if (e && atoi(e) == 0) return false;
+  const mia_conv_args& a = k.a;
+  const ConvGroup& G = k.g[0];
+  if (dtype == MIA_F32 || k.ng != 1 || k.stride != 1 || G.kh != 3 || G.kw != 3 || G.pad_y != 1 ||
+      G.pad_x != 1 || G.ho != a.H || G.wo != a.W || G.ay != 1 || G.ax != 1 || G.by != 0 ||
+      G.bx != 0 || a.shuffle_out || a.W % 16 != 0 || k.HT != a.H || k.WT != a.W ||
+      k.ystride != a.Cout || a.Cin != 32 || a.Cout != 32 || G.kpad < 9 * 32 || !a.y)
+    return false;
+  const bool pro = a.in_scale != nullptr;
+  if (!pro && a.act_in != MIA_ACT_NONE) return false;
+  if (pro && k.cout_mod != a.Cout) return false;
+  return thin32_mask_ok(epi_mask(k), pro);
+}
+
+template <typename T, bool PRO, int F>
+static int launch_thin32_(const ConvK& k, int grid, hipStream_t st) {
+  hipLaunchKernelGGL((conv_thin32_kernel<T, PRO, F>), dim3(grid), dim3(256), 0, st, k);
+  return check_launch("conv_thin32");
+}
+
+int launch_conv_thin32(ConvK& k, int dtype, hipStream_t st) {
+  using namespace epi;
+  const int64_t groups = (int64_t)k.a.N * k.a.H * (k.a.W / 16);
+  const int grid = grid_for(groups, 16);
+  const bool pro = k.a.in_scale != nullptr;
+  MIA_DISPATCH_DTYPE(dtype, T, {
+    if constexpr (sizeof(T) == 2) {
+      if (pro) return launch_thin32_<T, true, OSC | NOISE | BIAS | LRELU>(k, grid, st);
+      switch (epi_mask(k)) {
+        case OSC | SDOT: return launch_thin32_<T, false, OSC | SDOT>(k, grid, st);
+        case OSC | SDOT | ACC: return launch_thin32_<T, false, OSC | SDOT | ACC>(k, grid, st);
+        case OSC | SDOT | BAB: return launch_thin32_<T, false, OSC | SDOT | BAB>(k, grid, st);
+        case OSC | SDOT | ACC | BAB:
+          return launch_thin32_<T, false, OSC | SDOT | ACC | BAB>(k, grid, st);
+        case 0: return launch_thin32_<T, false, 0>(k, grid, st);
+        case ACC: return launch_thin32_<T, false, ACC>(k, grid, st);
+        default: break;
+      }
+    }
+  });
+  return set_error("conv_thin32: no specialisation for this launch");
 }
 
 // Eligible launches (checked by run_conv): 2-byte type, one group, stride 1, 3×3 pad 1, identity

@@ -214,6 +214,13 @@ struct EpiChunk {  // rows per aux-load chunk (bounds the live registers for tal
   static constexpr int FMC = TL::FM < 4 ? TL::FM : 4;
 };
 
+// Per-lane partial sums of the reductions (sdot, q, csum), kept across calls by a caller that
+// flushes them itself (conv_thin.hip: one flush per image run instead of atomics per call).
+template <int FN>
+struct EpiSums {
+  float part[FN][4], partq[FN][4], pcs[FN][4];
+};
+
 // (Hg, Wg): the output grid the rows index; default (p.H, p.W). The generic tile passes a virtual
 // grid of 16-pixel rows (HWo / 16, 16), so that its linear pixel rows use the same indexing.
 // pre: the per-pixel operands of a single-chunk wave tile already gathered by the caller (the
@@ -223,7 +230,7 @@ __device__ __forceinline__ void halo_epilogue_f(
     const ConvK& k, const f32x4 (&acc)[TL::FM][TL::FN], int n, int y0, int x0, int n0, int wm,
     int wn, int lane, int Hg = -1, int Wg = -1,
     const EpiRows<T, EpiChunk<TL>::FMC, TL::FN>* pre = nullptr, float* red = nullptr, int nwm = 1,
-    int cw = 0) {
+    int cw = 0, EpiSums<TL::FN>* keep = nullptr) {
   constexpr int FM = TL::FM, FN = TL::FN;
   constexpr bool OSC = F & epi::OSC, NOISE = F & epi::NOISE, BIAS = F & epi::BIAS;
   constexpr bool TAP = F & epi::TAP, MASK = F & epi::MASK, ACC = F & epi::ACC;
@@ -384,6 +391,17 @@ __device__ __forceinline__ void halo_epilogue_f(
   }
   }  // row chunks
   if constexpr (SDOT || BAB || CSUM) {
+    if (keep != nullptr) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          keep->part[j][e] += part[j][e];
+          keep->partq[j][e] += partq[j][e];
+          keep->pcs[j][e] += pcs[j][e];
+        }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int c = cl + 16 * j;

@@ -816,3 +816,55 @@ def _thin_e4e_input_layer(cuda, dtype, N, H, W):
     torch.cuda.synchronize()
     assert rel_err(nchw(y), ref) < 2 * TOL[dtype]
     assert rel_err(nchw(gx), gx_ref) < 2 * TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,H,W", [(2, 32, 48), (3, 16, 16), (4, 256, 256)])
+@pytest.mark.parametrize("mode", ["modconv", "dgrad_sdot", "plain", "acc"])
+@pytest.mark.parametrize("thin", ["1", "0"])
+def test_conv_thin32_layers(cuda, monkeypatch, dtype, N, H, W, mode, thin):
+    """32 → 32-channel layers (StyleGAN2 1024² StyledConvs) on the weights-in-VGPR thin kernel
+    (conv_thin.hip conv_thin32_kernel; MIA_CONV_THIN32=0 = the implicit-GEMM tile): modulated
+    forward with demod / noise / bias / lrelu·√2, the input gradient with the style-gradient sdot
+    (partials kept per image run, flushed on image change: 4 × 256² exercises long runs), plain
+    and accumulating, against torch fp64."""
+    monkeypatch.setenv("MIA_CONV_THIN32", thin)
+    C = 32
+    g = torch.Generator().manual_seed(N * 31 + H + W + len(mode))
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
+    xq, wq = x.to(dtype).double(), w.to(dtype).double()
+    xd = nhwc(x, dtype).to(cuda)
+    wf = layouts.fwd_matrix(w, dtype).to(cuda)
+    y0 = torch.randn(N, C, H, W, generator=g)
+    y = nhwc(y0, dtype).to(cuda)
+    sd = sd_ref = None
+    if mode == "modconv":
+        s = torch.rand(N, C, generator=g) + 0.5
+        d = torch.rand(N, C, generator=g) + 0.5
+        nz = torch.randn(H * W, generator=g)
+        b = torch.randn(C, generator=g) * 0.1
+        pre = F.conv2d(xq * s.to(dtype).double().view(N, C, 1, 1), wq, padding=1) * d.double().view(
+            N, C, 1, 1) + 0.3 * nz.double().view(1, 1, H, W) + b.double().view(1, -1, 1, 1)
+        ref = F.leaky_relu(pre, 0.2) * math.sqrt(2)
+        ops.conv3x3(xd, wf, y, cout=C, in_scale=s.to(cuda), out_scale=d.to(cuda),
+                    noise=nz.to(cuda), noise_w=0.3, bias=b.to(cuda), act_out=ops.ACT_LRELU_S2)
+    elif mode == "dgrad_sdot":
+        s = torch.rand(N, C, generator=g) + 0.5
+        aux = torch.randn(N, C, H, W, generator=g)
+        conv = F.conv2d(xq, wq, padding=1)
+        ref = conv * s.double().view(N, C, 1, 1)
+        sd_ref = (conv * aux.to(dtype).double()).sum((2, 3))
+        sd = torch.zeros(N, C, device=cuda)
+        ops.conv3x3(xd, wf, y, cout=C, out_scale=s.to(cuda), aux_x=nhwc(aux, dtype).to(cuda),
+                    sdot=sd)
+    elif mode == "plain":
+        ref = F.conv2d(xq, wq, padding=1)
+        ops.conv3x3(xd, wf, y, cout=C)
+    else:
+        ref = F.conv2d(xq, wq, padding=1) + y0.to(dtype).double()
+        ops.conv3x3(xd, wf, y, cout=C, accumulate=True)
+    torch.cuda.synchronize()
+    assert rel_err(nchw(y), ref) < 2 * TOL[dtype]
+    if sd is not None:
+        assert rel_err(sd, sd_ref) < 2 * TOL[dtype]

@@ -33,6 +33,8 @@ SHAPES = [
     ("vgg 256² 64→64", 256, 64, 64, "vgg"),
     ("dgrad+tap 256² 64→64", 256, 64, 64, "tap"),
     ("dgrad 128² 128→64", 128, 128, 64, "plain"),
+    ("mod 1024² 32→32", 1024, 32, 32, "mod"),
+    ("dgrad+sdot 1024² 32→32", 1024, 32, 32, "sdot"),
     ("up 128²→256² 256→128", 128, 256, 128, "up"),
     ("up 64²→128² 512→256", 64, 512, 256, "up"),
     ("up 32²→64² 512→512", 32, 512, 512, "up"),

@@ -1,3 +1,4 @@
+# 32-channel thin kernel: parity, A/B, cfg3 bench line
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "thin32 or fused_backward_front or modconv" > gpurun_out/t_thin32.log 2>&1 && echo tests-ok &&

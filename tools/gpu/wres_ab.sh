@@ -1,3 +1,4 @@
+# weights-resident 64-channel kernel: parity and A/B against the generic tile
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "register_epilogue or halo_and_generic" > gpurun_out/t_wres.log 2>&1 && echo tests-ok &&

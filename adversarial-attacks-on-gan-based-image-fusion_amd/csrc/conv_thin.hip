@@ -276,10 +276,27 @@ __global__ __launch_bounds__(256) void conv_thin32_kernel(const ConvK k) {
     for (int e = 0; e < 4; ++e) sums.part[j][e] = sums.partq[j][e] = sums.pcs[j][e] = 0.f;
   int cur_n = -1;
   VT sv;
+  // the 9 A gathers of group g (issued one group ahead: they land during the previous group's
+  // MFMAs and epilogue)
+  auto gather = [&](int64_t g, VT (&a)[9]) __attribute__((always_inline)) {
+    const int n = (int)(g / gpi);
+    const int rem = (int)(g - (int64_t)n * gpi);
+    const int y = rem / gpr, x0 = (rem - y * gpr) * 16;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int sy = y + t / 3 - 1, sx = x0 + frow + t % 3 - 1;
+      const bool ok = sy >= 0 && sy < H && sx >= 0 && sx < W;
+      a[t] = ld16_or_zero<T>(X + ((size_t)(n * H + (ok ? sy : 0)) * W + (ok ? sx : 0)) * 32 + fq * 8,
+                             ok);
+    }
+  };
+  VT a_cur[9], a_nxt[9];
+  if (g0 < g1) gather(g0, a_cur);
   for (int64_t g = g0; g < g1; ++g) {
     const int n = (int)(g / gpi);
     const int rem = (int)(g - (int64_t)n * gpi);
     const int y = rem / gpr, x0 = (rem - y * gpr) * 16;
+    if (g + 1 < g1) gather(g + 1, a_nxt);
     if (n != cur_n) {
       if constexpr (RED) {
         if (cur_n >= 0) thin32_flush<EPI>(p, sums, cur_n, frow, fq);
@@ -294,16 +311,15 @@ __global__ __launch_bounds__(256) void conv_thin32_kernel(const ConvK k) {
     f32x4 acc[1][2] = {{f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}}};
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      const int sy = y + t / 3 - 1, sx = x0 + frow + t % 3 - 1;
-      const bool ok = sy >= 0 && sy < H && sx >= 0 && sx < W;
-      VT a = ld16_or_zero<T>(X + ((size_t)(n * H + (ok ? sy : 0)) * W + (ok ? sx : 0)) * 32 + fq * 8,
-                             ok);
+      VT a = a_cur[t];
       if constexpr (PRO) modulate<T>(a, sv, lrelu_in);
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[0][j] = mfma_chunk<T>(wr[t][j], a, acc[0][j]);
     }
     halo_epilogue_f<T, TL, EPI>(k, acc, n, y, x0, 0, 0, 0, lane, -1, -1, nullptr, nullptr, 1, 0,
                                 RED ? &sums : nullptr);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) a_cur[t] = a_nxt[t];
   }
   if constexpr (RED) {
     if (cur_n >= 0) thin32_flush<EPI>(p, sums, cur_n, frow, fq);

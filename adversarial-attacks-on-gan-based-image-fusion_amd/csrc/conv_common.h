@@ -340,7 +340,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
             for (int e = 0; e < 8; ++e) {
               const float gr = lrelu_s2_grad(xv[e]);
               const float gp = v[e] * gr;
-              const float c = gp * (xv[e] / gr - nz - bbias8[e]);
+              const float c = gp * (xv[e] * lrelu_s2_inv_grad(xv[e]) - nz - bbias8[e]);
               if (single) partq[e] += c;
               else atomicAdd(&p.bab_q[(size_t)n * Cout + col + e], c);
               v[e] = gp * dm8[e];

@@ -120,7 +120,7 @@ __device__ __forceinline__ void halo_epilogue(const ConvK& k, const f32x4 (&acc)
           for (int e = 0; e < 4; ++e) {
             const float gr = lrelu_s2_grad(xv[e]);
             const float gp = v[e] * gr;
-            partq[j][e] += gp * (xv[e] / gr - bnz - bbv[j][e]);
+            partq[j][e] += gp * (xv[e] * lrelu_s2_inv_grad(xv[e]) - bnz - bbv[j][e]);
             v[e] = gp * dmv[j][e];
           }
         }
@@ -356,7 +356,7 @@ __device__ __forceinline__ void halo_epilogue_f(
         if constexpr (BAB) {
           const float gr = lrelu_s2_grad(xv[e]);
           const float gp = v[e] * gr;
-          partq[j][e] += gp * (xv[e] / gr - bnz[i] - bbv[j][e]);
+          partq[j][e] += gp * (xv[e] * lrelu_s2_inv_grad(xv[e]) - bnz[i] - bbv[j][e]);
           v[e] = gp * dmv[j][e];
         }
         if constexpr (CSUM) pcs[j][e] += v[e];

@@ -32,6 +32,11 @@ constexpr float SQRT2 = 1.41421356237309504880f;
 // FusedLeakyReLU (rosinality op/fused_act): leaky_relu(v, 0.2) * sqrt(2); bias already in v.
 __device__ __forceinline__ float lrelu_s2(float v) { return (v > 0.f ? v : 0.2f * v) * SQRT2; }
 __device__ __forceinline__ float lrelu_s2_grad(float pre) { return pre > 0.f ? SQRT2 : 0.2f * SQRT2; }
+// 1 / lrelu_s2_grad: the pre-activation from a stored activation a = lrelu_s2(pre) is a · this
+// (a multiply instead of a fp32 division in the backward-front epilogues)
+__device__ __forceinline__ float lrelu_s2_inv_grad(float pre) {
+  return pre > 0.f ? 0.70710678118654752f : 3.5355339059327376f;
+}
 
 // Wave-level sum (64 lanes).
 __device__ __forceinline__ float wave_sum(float v) {

@@ -455,7 +455,7 @@ __global__ void torgb_bwd_kernel(const float* __restrict__ grgb, const T* __rest
           const float a = to_f(pr[e]);
           const float gr = lrelu_s2_grad(a);
           const float gp = gv * gr;
-          qa[e] += gp * (a / gr - nz - bs[e]);
+          qa[e] += gp * (a * lrelu_s2_inv_grad(a) - nz - bs[e]);
           gv = gp * dm[e];
         }
         ga[e] = from_f<T>(gv);

@@ -1,4 +1,4 @@
-// Up-sampling StyledConv forward as ONE halo-tiled MFMA kernel (2-byte types): the modulated
+// Up-sampling StyledConv forward as ONE halo-tiled MFMA kernel (fp32 / fp16 / bf16): the modulated
 // conv_transpose2d(stride 2) of rosinality ModulatedConv2d(upsample=True) [ext], reached through
 // net.decoder (code/attack/attack_main2.py:619-621). Blur, demod, noise, bias and the activation
 // follow in mia_upconv_blur_fwd.
@@ -14,12 +14,14 @@
 //   * a K-step is (offset, two phases sharing it): (0,0)·{p0,p1}, (0,0)·{p2,p3}, (0,−1)·{p0,p2},
 //     (−1,0)·{p0,p1}, (−1,−1)·{p0}; each step reads the offset's A fragments once for both
 //     phases, so the LDS reads per MFMA equal the stride-1 halo kernel's (0.5);
-//   * weights: the packed [Cin/64][5][2][Cout][64] tensor (layouts.upconv_halo_matrix), one 16-KB
-//     stage (2 slots × 64 channels × 128 B) per K-step through a 2-stage LDS-DMA ring;
+//   * weights: the packed [Cin/BK][5][2][Cout][BK] tensor (layouts.upconv_halo_matrix; BK = the
+//     channels of one 128-B row: 64 for 2-byte types, 32 for fp32), one 16-KB stage (2 slots × 64
+//     channels × 128 B) per K-step through a 2-stage LDS-DMA ring;
 //   * waves split DMA roles as in conv_halo.hip (2 weight waves, 2 halo waves, vmcnt retires in
 //     issue order); the next channel block's halo streams during steps 0–3;
 //   * accumulators: 4 phases × 4 patch rows × 2 channel fragments per wave (128 VGPRs); the
-//     epilogue exchanges fragment pairs (v_permlane16_swap) for 16-byte stores into T.
+//     2-byte epilogue exchanges fragment pairs (v_permlane16_swap) for 16-byte stores into T, the
+//     fp32 one stores each lane's 4 consecutive channels as one 16-byte vector.
 // The phase positions on the last row / column of T's phase grids (y = R or x = R; they exist for
 // the even phases only) go to the generic kernel as four one-row / one-column groups.
 //
@@ -57,7 +59,7 @@ __device__ __forceinline__ constexpr int up_phase(int st, int slot) {
 
 struct UpK {
   const void* x;
-  const void* w;  // packed [Cin/64][5][2][Cout][64]
+  const void* w;  // packed [Cin/BK][5][2][Cout][BK]
   void* t;        // (N, 2R+1, 2R+1, Cout); DG: (N, 2R, 2R, Cout)
   const float* style;
   const void* mask_a;       // DG: (N, 2R, 2R, Cout) or NULL
@@ -69,7 +71,7 @@ template <typename T, bool PRO, bool DG>
 __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
   typedef HaloUp TL;
   typedef typename Vec<T>::type VT;
-  constexpr int VEC = 8, BK = 64;
+  constexpr int VEC = Vec<T>::N, BK = ROWB / (int)sizeof(T);  // elements per chunk / per row
   constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, BN = TL::BN, PH = TL::PH, PW = TL::PW;
   constexpr int HSIDE = TL::HSIDE, HROWS = TL::HROWS, HBUF = TL::HBUF, BSTAGE = TL::BSTAGE;
   constexpr int B_INS = TL::B_INS, H_INS = TL::H_INS, HPS = TL::HPS, BWAVES = TL::BWAVES;
@@ -221,6 +223,42 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
   // ---- epilogue: phase (py, px) of input position (y, x) → T(2y+py, 2x+px) ----------------------
   T* __restrict__ Y = (T*)k.t;
   const int TS = DG ? 2 * R : 2 * R + 1, lrow = lane >> 4;
+  if constexpr (sizeof(T) == 4) {
+    // D[channel][pixel]: lane (frow, fq) holds channels 4·fq … 4·fq+3 of fragment j for pixel
+    // x0 + frow — one 16-byte vector per (phase, row, fragment)
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int py = ph >> 1, px = ph & 1;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int ty = 2 * (y0 + wm * FM + i) + (DG ? 1 - py : py);
+        const int tx = 2 * (x0 + frow) + (DG ? 1 - px : px);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int c = n0 + wn * FN * 16 + 16 * j + 4 * fq;
+          const size_t off = ((size_t)(n * TS + ty) * TS + tx) * Cout + c;
+          f32x4 v = acc[ph][i][j];
+          if constexpr (DG) {
+            if (k.mask_a) {
+              const f32x4 m = *(const f32x4*)((const float*)k.mask_a + off);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float sl = k.mask_slope ? k.mask_slope[c + e] : 0.f;
+                v[e] = m[e] > 0.f ? v[e] : sl * v[e];
+              }
+            }
+            if (k.accumulate) {
+              const f32x4 o = *(const f32x4*)((const float*)Y + off);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] += o[e];
+            }
+          }
+          *(f32x4*)((float*)Y + off) = v;
+        }
+      }
+    }
+    return;
+  } else {
   typedef T t2 __attribute__((ext_vector_type(2)));
   float msl[8];
   if constexpr (DG) {
@@ -275,6 +313,7 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
       *(uint4*)(Y + off) = make_uint4(a[0], a[1], b[0], b[1]);
     }
   }
+  }  // 2-byte epilogue
 }
 
 template <typename T, bool PRO, bool DG = false>
@@ -300,7 +339,7 @@ static int launch_upconv_halo(UpK& k, hipStream_t st) {
 bool upconv_halo_eligible(int dtype, int R, int Cin, int Cout) {
   const char* e = getenv("MIA_UPCONV_HALO");  // tuning / A-B switch: 0 = generic phase GEMMs
   if (e && atoi(e) == 0) return false;
-  return dtype != MIA_F32 && R % 16 == 0 && Cin % 64 == 0 && Cout % HaloUp::BN == 0 &&
+  return R % 16 == 0 && Cin % 64 == 0 && Cout % HaloUp::BN == 0 &&
          (int64_t)(2 * R + 1) * (2 * R + 1) < (1LL << 31);
 }
 
@@ -311,18 +350,16 @@ int launch_upconv_halo(const void* x, const void* w_up, void* t, int N, int R, i
   k.N = N; k.R = R; k.Cin = Cin; k.Cout = Cout; k.act_in = act_in;
   const bool pro = style != nullptr || act_in != MIA_ACT_NONE;
   MIA_DISPATCH_DTYPE(dtype, T, {
-    if constexpr (sizeof(T) == 2) {
-      return pro ? launch_upconv_halo<T, true, false>(k, st)
-                 : launch_upconv_halo<T, false, false>(k, st);
-    }
+    return pro ? launch_upconv_halo<T, true, false>(k, st)
+               : launch_upconv_halo<T, false, false>(k, st);
   });
-  return set_error("upconv_halo: 2-byte types only");
+  return set_error("upconv_halo: unknown dtype");
 }
 
 bool s2_dgrad_halo_eligible(int dtype, int R, int Cg, int Cx) {
   const char* e = getenv("MIA_S2DG_HALO");  // tuning / A-B switch: 0 = generic phase GEMMs
   if (e && atoi(e) == 0) return false;
-  return dtype != MIA_F32 && R % 16 == 0 && Cg % 64 == 0 && Cx % HaloUp::BN == 0 &&
+  return R % 16 == 0 && Cg % 64 == 0 && Cx % HaloUp::BN == 0 &&
          (int64_t)4 * R * R < (1LL << 31);
 }
 
@@ -332,10 +369,8 @@ int launch_s2_dgrad_halo(const void* g, const void* w, void* gx, int N, int R, i
   UpK k = {};
   k.x = g; k.w = w; k.t = gx; k.mask_a = mask_a; k.mask_slope = mask_slope;
   k.N = N; k.R = R; k.Cin = Cg; k.Cout = Cx; k.accumulate = accumulate;
-  MIA_DISPATCH_DTYPE(dtype, T, {
-    if constexpr (sizeof(T) == 2) return launch_upconv_halo<T, false, true>(k, st);
-  });
-  return set_error("s2_dgrad_halo: 2-byte types only");
+  MIA_DISPATCH_DTYPE(dtype, T, return launch_upconv_halo<T, false, true>(k, st));
+  return set_error("s2_dgrad_halo: unknown dtype");
 }
 
 }  // namespace mia
@@ -347,7 +382,7 @@ extern "C" int mia_conv_s2_dgrad_halo(const void* g, const void* w_halo, void* g
                                       int accumulate, int dtype, void* stream) {
   MIA_CHECK_ARG(g && w_halo && gx && N > 0, "bad args");
   MIA_CHECK_ARG(s2_dgrad_halo_eligible(dtype, R, Cg, Cx),
-                "needs fp16/bf16, R % 16 == 0, Cg % 64 == 0, Cx % 64 == 0 "
+                "needs R % 16 == 0, Cg % 64 == 0, Cx % 64 == 0 "
                 "(use mia_conv2d phase groups otherwise)");
   MIA_CHECK_ARG((int64_t)N * R * R * Cg < (1LL << 31), "input too large for 32-bit offsets");
   return launch_s2_dgrad_halo(g, w_halo, gx, N, R, Cg, Cx, mask_a, mask_slope, accumulate, dtype,

@@ -121,8 +121,7 @@ class E4EEncoder:
                 U["w2d"] = mt(layouts.dgrad_matrix(w2, T))
             else:
                 U["w2d"] = [(mt(m), py, px) for m, py, px in layouts.s2_dgrad_phases(w2, T)]
-                U["w2dh"] = mt(layouts.s2_dgrad_halo_matrix(w2, T)) if T != torch.float32 \
-                    else None
+                U["w2dh"] = mt(layouts.s2_dgrad_halo_matrix(w2, T))
             U["se_w1"] = dd(p[pre + ".res_layer.5.fc1.weight"].reshape(U["cr"], depth))
             U["se_w2"] = dd(p[pre + ".res_layer.5.fc2.weight"].reshape(depth, U["cr"]))
             if cin != depth:

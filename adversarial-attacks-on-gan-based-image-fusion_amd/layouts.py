@@ -73,21 +73,28 @@ UPCONV_HALO_STEPS = (((0, 0), (0, 1)), ((0, 0), (2, 3)), ((0, 1), (0, 2)), ((1, 
                      ((1, 1), (0, None)))
 
 
+def halo_bk(dtype):
+    """Channels per 128-B operand row (one K-step of a channel block): 32 fp32, 64 otherwise."""
+    return 32 if dtype == torch.float32 else 64
+
+
 def upconv_halo_matrix(w, dtype):
-    """Packed weights of mia_upconv_fwd_halo: (Cin/64, 5, 2, Cout, 64), slot weight
-    W[:, ci, py + 2·jy, px + 2·jx] (T[2m+p] = Σ_j x[m−j]·W[p+2j], as upconv_subpixel_matrices)."""
+    """Packed weights of mia_upconv_fwd_halo: (Cin/BK, 5, 2, Cout, BK) with BK = halo_bk(dtype),
+    slot weight W[:, ci, py + 2·jy, px + 2·jx] (T[2m+p] = Σ_j x[m−j]·W[p+2j], as
+    upconv_subpixel_matrices)."""
     cout, cin = w.shape[:2]
     if cin % 64:
         raise ValueError("Cin must be a multiple of 64")
+    bk = halo_bk(dtype)
     w = w.double()
-    out = torch.zeros(cin // 64, 5, 2, cout, 64, dtype=torch.float64)
+    out = torch.zeros(cin // bk, 5, 2, cout, bk, dtype=torch.float64)
     for st, ((jy, jx), phases) in enumerate(UPCONV_HALO_STEPS):
         for slot, ph in enumerate(phases):
             if ph is None:
                 continue
             py, px = ph >> 1, ph & 1
             wk = w[:, :, py + 2 * jy, px + 2 * jx]  # (cout, cin)
-            out[:, st, slot] = wk.reshape(cout, cin // 64, 64).permute(1, 0, 2)
+            out[:, st, slot] = wk.reshape(cout, cin // bk, bk).permute(1, 0, 2)
     return out.to(dtype)
 
 
@@ -163,5 +170,5 @@ def s2_dgrad_halo_matrix(w, dtype):
     """Packed weights of mia_conv_s2_dgrad_halo for the forward stride-2 conv w (Cout, Cin, 3, 3):
     the halo up-conv layout of the channel-transposed, spatially flipped kernel (the input
     gradient is the transposed conv mirrored: offsets +j, output phase 1 − p, kernel index
-    2 − (p + 2j)). (Cout/64, 5, 2, Cin, 64)."""
+    2 − (p + 2j)). (Cout/BK, 5, 2, Cin, BK)."""
     return upconv_halo_matrix(w.double().transpose(0, 1).flip(2, 3), dtype)

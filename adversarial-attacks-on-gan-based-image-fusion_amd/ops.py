@@ -5,7 +5,7 @@ import ctypes
 
 import torch
 
-from . import _lib
+from . import _lib, layouts
 from ._lib import ACT_LRELU_S2, ACT_NONE, ACT_PRELU, ACT_RELU, ConvArgs, call  # noqa: F401
 
 DTYPES = {torch.float32: _lib.MIA_F32, torch.float16: _lib.MIA_F16, torch.bfloat16: _lib.MIA_BF16}
@@ -174,7 +174,8 @@ def upconv_fwd(x, w_phases, t_out, cout, act_in=ACT_NONE, style=None, flops=None
         ptr(w)
     fl = flops if flops is not None else 2 * N * R * R * 9 * Cin * cout
     if w_up is not None:
-        _need(w_up, (Cin // 64, 5, 2, cout, 64), T, "w_up")
+        bk = layouts.halo_bk(T)
+        _need(w_up, (Cin // bk, 5, 2, cout, bk), T, "w_up")
         _prof_call("mia_upconv_fwd_halo", fl, ptr(x), wp, ptr(w_up), ptr(t_out), N, R, Cin, cout,
                    act_in, ptr(style), dt(T), stream())
         return t_out
@@ -812,7 +813,8 @@ def s2_dgrad_halo(g, w_halo, gx, mask_a=None, mask_slope=None, accumulate=False,
     T = g.dtype
     if R != R2:
         raise ValueError("square inputs only")
-    _need(w_halo, (Cg // 64, 5, 2, Cx, 64), T, "w_halo")
+    bk = layouts.halo_bk(T)
+    _need(w_halo, (Cg // bk, 5, 2, Cx, bk), T, "w_halo")
     _need(gx, (N, 2 * R, 2 * R, Cx), T, "gx")
     if mask_a is not None:
         _need(mask_a, gx.shape, T, "mask_a")
@@ -829,7 +831,7 @@ def s2_dgrad_halo_ok(dtype, R, Cg, Cx):
     import os
     if os.environ.get("MIA_S2DG_HALO") == "0":
         return False
-    return dtype != torch.float32 and R % 16 == 0 and Cg % 64 == 0 and Cx % 64 == 0
+    return R % 16 == 0 and Cg % 64 == 0 and Cx % 64 == 0
 
 
 def sum_slices(x, y):

@@ -344,9 +344,14 @@ def fgsm(net, imgs, eps, **kw):
 
 
 def algorithmic_flops_per_image_step(synth, vgg, encoder=None):
-    """G fwd ×3 (fwd, dgrad, style-grad) + VGG ×4 (two calls, fwd + dgrad)
-    + the e4e encoder ×2 (fwd + input gradient) when it is the real one (the linear stand-in's
-    FLOPs are excluded, §8d)."""
+    """GEMM work one PGD iteration needs per image: G ×2 (forward + input gradient) + VGG ×4
+    (two calls, forward + input gradient each) + the e4e encoder ×2 (forward + input gradient)
+    when it is the real one (the linear stand-in's FLOPs are excluded).
+
+    SURVEY.md §8d counted G ×3 with a separate style-gradient GEMM. The kernels never form the
+    per-sample weight gradient: ∂L/∂s[n][ci] = Σ_p x[n,p,ci]·(Wᵀg)[n,p,ci] is a dot product
+    over the dgrad output the input gradient computes anyway (2·H·W·Cin FLOP per layer, the
+    `sdot` epilogue), so crediting it as a third GEMM would overstate the work by ~13 %."""
     enc = 2 * getattr(encoder, "flops_fwd_per_image", 0) if encoder is not None else 0
-    return 3 * synth.flops_fwd_per_image + 4 * vgg.flops_fwd_per_image + enc
+    return 2 * synth.flops_fwd_per_image + 4 * vgg.flops_fwd_per_image + enc
 

@@ -6,11 +6,17 @@ batch 1024 over 8 GPUs = 128 per GPU; weak scaling) through the reference's netw
 encoder (IR-SE50 Encoder4Editing), the StyleGAN2 synthesis and the VGG16 trunk, random-init.
 Inputs are resident in HBM before the timed region. Rank 0 prints ONE JSON line.
 
-    python bench.py [--gpus N --steps K --warmup W --batch B --dtype fp16|bf16|fp32
-                     --encoder e4e|linear]
+    python bench.py [--gpus N --steps K --warmup W --batch B --dtype fp32|fp16|bf16
+                     --encoder e4e|linear --lowp fp16|bf16|none]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+`value` is measured at fp32, the reference's arithmetic (the reference runs its networks in
+torch's default float32 on cuda:0, code/attack/interpolation.py:1095). A reduced-precision run of
+the same workload (fp16 by default) is reported beside it as the labelled sub-record
+`low_precision` (N=1 only); it is never `value`.
 """
 import argparse
+import gc
 import glob
 import json
 import os
@@ -35,7 +41,7 @@ from gfa_amd.weights import (make_e4e_weights, make_encoder_weights,  # noqa: E4
 METRIC = "attacked images/sec, PGD-20 L∞ ε=8/255 at 256², 1/2/4/8 MI355X"  # BASELINE.json
 DT = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
 DT_NAME = {"fp32": "f32", "fp16": "f16", "bf16": "bf16"}
-# MI355X_MICROARCH.md chip table: dense MFMA peaks (TFLOP/s)
+# MI355X_MICROARCH.md chip table: dense MFMA peaks (TFLOP/s); fp32 = v_mfma_f32_16x16x4_f32
 PEAK_TFLOPS = {"fp32": 157.3, "fp16": 2500.0, "bf16": 2500.0}
 
 
@@ -47,9 +53,14 @@ def parse():
     ap.add_argument("--batch", type=int, default=128, help="images per GPU")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--pgd-steps", type=int, default=20)
-    ap.add_argument("--dtype", default="fp16", choices=list(DT))
+    ap.add_argument("--dtype", default="fp32", choices=list(DT),
+                    help="compute dtype of `value` (default fp32 = the reference's precision)")
+    ap.add_argument("--lowp", default="fp16", choices=["fp16", "bf16", "none"],
+                    help="dtype of the labelled reduced-precision sub-record (N=1 only)")
+    ap.add_argument("--lowp-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-steps", type=int, default=10)
+    ap.add_argument("--cpu-pgd-steps", type=int, default=None,
+                    help="PGD iterations of the wall-clocked CPU attack (default: --pgd-steps)")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--norm", default="linf", choices=["linf", "l2_cw"],
                     help="linf = PGD L∞ (the headline); l2_cw = C&W-L2 with the VGG perceptual "
@@ -66,9 +77,11 @@ def encoder_weights(kind, size):
     return make_e4e_weights(size, seed=1) if kind == "e4e" else make_encoder_weights(size, seed=1)
 
 
-def cpu_baseline(size, pgd_steps, sample_steps, encoder):
-    """The oracle (CPU restatement, fp32, all host cores) on a bounded sample: one 256² image,
-    `sample_steps` PGD iterations, extrapolated to a PGD-`pgd_steps` attack."""
+def cpu_baseline(size, pgd_steps, encoder):
+    """The oracle (CPU restatement, fp32, all host cores) on a bounded sample of the same
+    workload: ONE complete PGD-`pgd_steps` attack of one 256² image (target precompute + every
+    iteration), wall-clocked end to end — BASELINE.md's procedure at B=1. B=min(N,8)=8 would
+    take 8× as long (≈ 3–4 min on the box's 16 cores) and is left out of the default run."""
     from oracle import attack_ref, vgg_ref
     # the box's CPU share (OMP_NUM_THREADS is set to it there); affinity shows the whole machine
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
@@ -80,26 +93,22 @@ def cpu_baseline(size, pgd_steps, sample_steps, encoder):
     g = torch.Generator().manual_seed(123)
     x0 = torch.rand(1, 3, size, size, generator=g) * 2 - 1
     t = torch.rand(1, 3, size, size, generator=g) * 2 - 1
-    refs = attack_ref.Refs(gp, vp, ep, x0, t, size)
-    attack_ref.loss_grad(gp, vp, ep, x0, refs, size)  # warm-up
+    attack_ref.pgd(gp, vp, ep, x0, t, size, 8 / 255, 2 / 255, 1)  # warm-up (allocator, threads)
     t0 = time.perf_counter()
-    adv = x0.clone()
-    for _ in range(sample_steps):
-        _, gr = attack_ref.loss_grad(gp, vp, ep, adv, refs, size)
-        adv = attack_ref.project_step(adv, x0, gr, 2 * 8 / 255, 2 * 2 / 255)
-    dt = (time.perf_counter() - t0) / sample_steps
-    return {"value": 1.0 / (dt * pgd_steps), "unit": "attacked images/s", "cores": cores,
-            "kind": "port",
-            "sample": f"oracle fp32 CPU, 1 image @{size}², {sample_steps} PGD step(s) timed "
-                      f"({dt:.2f} s/step) extrapolated to PGD-{pgd_steps}; "
+    adv = attack_ref.pgd(gp, vp, ep, x0, t, size, 8 / 255, 2 / 255, pgd_steps)
+    dt = time.perf_counter() - t0
+    assert adv.shape == x0.shape
+    return {"value": 1.0 / dt, "unit": "attacked images/s", "cores": cores, "kind": "port",
+            "sample": f"oracle fp32 CPU: one complete PGD-{pgd_steps} attack of 1 image @{size}² "
+                      f"({encoder} encoder), wall clock {dt:.1f} s incl. the target precompute; "
                       f"torch.set_num_threads({cores})"}
 
 
-def pmc_traffic(dtype, batch, size, pgd_steps, encoder="linear"):
-    """HBM bytes per conv_kernel launch from the newest committed PMC profile of this exact
-    workload (profiles/rNN_bench_<dtype>_b<batch>.json, written by profiles/summarize_rocprof.py
-    from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this bench; FETCH_SIZE ×2 per the
-    gfx950 correction). PMC counters cannot be read from inside the timed process, hence a file."""
+def pmc_profile(dtype, batch, size, pgd_steps, encoder="linear"):
+    """The newest committed PMC profile of this exact workload
+    (profiles/rNN_bench_<dtype>_b<batch>[_e4e].json, written by profiles/summarize_rocprof.py from
+    separate FETCH_SIZE / WRITE_SIZE / MFMA-busy rocprofv3 passes of this bench; FETCH_SIZE ×2 per
+    the gfx950 correction). PMC counters cannot be read from inside the timed process."""
     if size != 256 or pgd_steps != 20:
         return None, None
     suffix = "_e4e" if encoder == "e4e" else ""
@@ -108,25 +117,28 @@ def pmc_traffic(dtype, batch, size, pgd_steps, encoder="linear"):
     for f in reversed(files):
         with open(f) as fh:
             d = json.load(fh)
-        v = d.get("conv_kernel", {}).get("hbm_bytes_per_launch")
-        if v:
-            return v, os.path.relpath(f, ROOT)
+        if d.get("conv_kernel", {}).get("hbm_bytes_per_launch"):
+            return d["conv_kernel"], os.path.relpath(f, ROOT)
     return None, None
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("launch N>1 with torch.distributed.run (one process per GPU)")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-    T = DT[args.dtype]
+def union_ms(iv):
+    """Total length of the union of [start, end] intervals (ms)."""
+    iv = sorted(iv)
+    tot, (cs, ce) = 0.0, iv[0]
+    for s0, e in iv[1:]:
+        if s0 > ce:
+            tot += ce - cs
+            cs, ce = s0, e
+        else:
+            ce = max(ce, e)
+    return tot + ce - cs
+
+
+def run_leg(args, dtype, steps, warmup, dev, world, rank, roofline):
+    """Build the networks at `dtype`, run `warmup` untimed and `steps` timed complete attacks
+    (barrier + synchronize on both sides, max over ranks). Returns the measurements."""
+    T = DT[dtype]
     S, B = args.size, args.batch
     gp = make_generator_weights(S, seed=0)
     ep = encoder_weights(args.encoder, S)
@@ -141,7 +153,6 @@ def main():
     tgt = (torch.rand(B, 3, S, S, generator=g) * 2 - 1).to(dev)
     eps, alpha = 8 / 255, 2 / 255
     n_total = B * world
-
     cw_runs = []
 
     def one_step():
@@ -154,11 +165,12 @@ def main():
             gather_shards(adv, n_total)
         return adv
 
-    for _ in range(args.warmup):
+    torch.cuda.reset_peak_memory_stats(dev)
+    for _ in range(warmup):
         one_step()
     torch.cuda.synchronize()
     prof = []
-    if not args.no_roofline:
+    if roofline:
         ops.PROFILE = prof
     if world > 1:
         dist.barrier()
@@ -166,8 +178,8 @@ def main():
     t_ref = torch.cuda.Event(enable_timing=True)  # origin of the conv launches' event intervals
     t_ref.record()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_step()
+    for _ in range(steps):
+        adv = one_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -177,11 +189,73 @@ def main():
         tt = torch.tensor([elapsed], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.item()
+    # sanity of the output the timed region produced: finite, inside the ε-ball and [-1, 1]
+    ok = bool(torch.isfinite(adv).all()) and float(adv.abs().max()) <= 1.0
+    if args.norm == "linf":
+        ok = ok and float((adv - x0).abs().max()) <= 2 * eps + 1e-6
+    timed_cw = cw_runs[warmup:]
+    r = {"elapsed": elapsed, "n_total": n_total, "timed_cw": timed_cw,
+         "iters": sum(timed_cw) / len(timed_cw) if timed_cw else args.pgd_steps,
+         "flops_img_step": pgd.algorithmic_flops_per_image_step(eng.G, eng.V, eng.E),
+         "peak_hbm_gb": torch.cuda.max_memory_allocated(dev) / 1e9, "output_ok": ok}
+    if prof:
+        # the e4e style heads run on side streams, so launches may overlap: a launch's own
+        # duration includes the time it shares the chip. The conv-busy time is the union of the
+        # launches' [start, end] event intervals (device clock, origin t_ref); achieved =
+        # algorithmic FLOPs ÷ conv-busy time, avg_launch_us = conv-busy time per launch.
+        iv = [(t_ref.elapsed_time(a), t_ref.elapsed_time(b)) for a, b, _ in prof]
+        r["conv_busy_ms"] = union_ms(iv)
+        r["conv_sum_ms"] = sum(e - s0 for s0, e in iv)
+        r["conv_flops"] = sum(f for _, _, f in prof)
+        r["conv_launches"] = len(prof)
+    del eng, enc, x0, tgt
+    return r
+
+
+def roofline_record(args, dtype, r):
+    tot_ms, n = r["conv_busy_ms"], r["conv_launches"]
+    ach = r["conv_flops"] / (tot_ms * 1e-3) / 1e12
+    peak = PEAK_TFLOPS[dtype]
+    pmc, src = pmc_profile(dtype, args.batch, args.size, args.pgd_steps, args.encoder)
+    rec = {"kernel": "3x3 conv: every conv API call of the step (mia::conv_halo_kernel, "
+                     "mia::upconv_halo_kernel + its edge launch, mia::conv_kernel, "
+                     "mia::conv_wres_kernel, mia::conv_thin_*: StyledConv fwd, up-conv, dgrads, "
+                     "VGG fwd/dgrad" + (", e4e convs and their input gradients)"
+                                        if args.encoder == "e4e" else ")"),
+           "bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
+           "traffic": pmc.get("hbm_bytes_per_launch") if pmc else None,
+           "traffic_unit": "bytes/launch", "traffic_source": src,
+           "launches": n, "avg_launch_us": tot_ms / n * 1e3,
+           "avg_launch_us_overlapped": r["conv_sum_ms"] / n * 1e3,
+           "algorithmic_gflop_per_launch": r["conv_flops"] / n / 1e9,
+           "share_of_step_time": tot_ms / (r["elapsed"] * 1e3)}
+    if pmc and pmc.get("mfma_busy_frac") is not None:
+        rec["mfma_busy_frac_pmc"] = pmc["mfma_busy_frac"]
+    return rec
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("launch N>1 with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist_world = 1
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+        dist_world = dist.get_world_size()
+    S, B = args.size, args.batch
+    r = run_leg(args, args.dtype, args.steps, args.warmup, dev, world, rank,
+                not args.no_roofline)
+    elapsed, n_total = r["elapsed"], r["n_total"]
     ms = elapsed / args.steps * 1e3
-    timed_cw = cw_runs[args.warmup:]
-    iters = sum(timed_cw) / len(timed_cw) if timed_cw else args.pgd_steps
     value = n_total * args.steps / elapsed
-    flops_img_step = pgd.algorithmic_flops_per_image_step(eng.G, eng.V, eng.E)
+    flops_img_step = r["flops_img_step"]
+    timed_cw = r["timed_cw"]
     out = {
         "metric": METRIC if (S, args.pgd_steps, args.norm) == (256, 20, "linf") else
                   (f"attacked images/sec, PGD-{args.pgd_steps} L∞ ε=8/255 at {S}², "
@@ -202,49 +276,35 @@ def main():
                                + (" (BASELINE config #4 per-GPU share)" if (S, B) == (256, 128)
                                   else "") + ", "
                                f"RCCL all-gather of outputs when N>1",
-                   "encoder": args.encoder, "norm": args.norm, "images_per_gpu": B, "global_batch": n_total, "size": S,
+                   "encoder": args.encoder, "norm": args.norm, "images_per_gpu": B,
+                   "global_batch": n_total, "size": S,
                    "pgd_steps": args.pgd_steps, "parallelism": f"dp{world}",
+                   "dist_world_size": dist_world,
                    **({"cw_iterations_run": timed_cw} if timed_cw else {}),
                    "algorithmic_gflop_per_image_step": flops_img_step / 1e9,
-                   "effective_tflops": flops_img_step * B * iters * world
+                   "effective_tflops": flops_img_step * B * r["iters"] * world
                    / (elapsed / args.steps) / 1e12,
-                   "peak_hbm_gb_per_gpu": torch.cuda.max_memory_allocated(dev) / 1e9},
+                   "peak_hbm_gb_per_gpu": r["peak_hbm_gb"],
+                   "output_in_eps_ball_and_finite": r["output_ok"]},
     }
-    if prof:
-        # the e4e style heads run on side streams, so launches overlap: a launch's own duration
-        # includes the time it shares the chip. The conv-busy time is the union of the launches'
-        # [start, end] event intervals (all on the device clock, origin t_ref); achieved =
-        # algorithmic FLOPs ÷ conv-busy time, avg_launch_us = conv-busy time per launch.
-        iv = sorted((t_ref.elapsed_time(a), t_ref.elapsed_time(b)) for a, b, _ in prof)
-        sum_ms = sum(e - s0 for s0, e in iv)
-        tot_ms, (cs, ce) = 0.0, iv[0]
-        for s0, e in iv[1:]:
-            if s0 > ce:
-                tot_ms += ce - cs
-                cs, ce = s0, e
-            else:
-                ce = max(ce, e)
-        tot_ms += ce - cs
-        tot_fl = sum(f for _, _, f in prof)
-        n = len(prof)
-        ach = tot_fl / (tot_ms * 1e-3) / 1e12
-        peak = PEAK_TFLOPS[args.dtype]
-        traffic, src = pmc_traffic(args.dtype, B, S, args.pgd_steps, args.encoder)
-        out["roofline"] = {
-            "kernel": "3x3 conv: every conv API call of the step (mia::conv_halo_kernel, "
-                      "mia::upconv_halo_kernel + its edge launch, mia::conv_kernel, "
-                      "mia::conv_wres_kernel, mia::conv_thin_*: StyledConv fwd, up-conv, dgrads, VGG fwd/dgrad"
-                      + (", e4e convs and their input gradients)" if args.encoder == "e4e"
-                         else ")"),
-            "bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,
-            "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": src,
-            "launches": n, "avg_launch_us": tot_ms / n * 1e3,
-            "avg_launch_us_overlapped": sum_ms / n * 1e3,
-            "algorithmic_gflop_per_launch": tot_fl / n / 1e9,
-            "share_of_step_time": tot_ms / (elapsed * 1e3)}
+    if "conv_busy_ms" in r:
+        out["roofline"] = roofline_record(args, args.dtype, r)
+    if world == 1 and args.lowp != "none" and args.lowp != args.dtype:
+        gc.collect()
+        torch.cuda.empty_cache()
+        lw = max(1, min(args.warmup, 1))
+        rl = run_leg(args, args.lowp, args.lowp_steps, lw, dev, world, rank,
+                     not args.no_roofline)
+        sub = {"note": "reduced-precision run of the same workload; NOT the headline value",
+               "dtype": DT_NAME[args.lowp], "value": rl["n_total"] * args.lowp_steps
+               / rl["elapsed"], "unit": "attacked images/s", "steps": args.lowp_steps,
+               "warmup": lw, "ms_per_step": rl["elapsed"] / args.lowp_steps * 1e3,
+               "output_in_eps_ball_and_finite": rl["output_ok"]}
+        if "conv_busy_ms" in rl:
+            sub["roofline"] = roofline_record(args, args.lowp, rl)
+        out["low_precision"] = sub
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(S, args.pgd_steps, args.cpu_sample_steps,
-                                           args.encoder)
+        out["cpu_baseline"] = cpu_baseline(S, args.cpu_pgd_steps or args.pgd_steps, args.encoder)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

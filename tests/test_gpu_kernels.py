@@ -641,7 +641,7 @@ def test_conv_thin_vgg_input_layer(cuda, monkeypatch, dtype, N, H, W, thin, e4e)
     assert rel_err(nchw(gx), gx_ref) < 2 * TOL[dtype]
 
 
-@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("N,cin,cout,R", [(2, 64, 64, 16), (1, 128, 192, 32), (2, 256, 128, 16),
                                           (1, 64, 64, 8)])
 @pytest.mark.parametrize("lrelu_in", [False, True])

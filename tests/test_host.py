@@ -266,6 +266,19 @@ def test_s2_dgrad_halo_packing_is_the_adjoint(R):
     assert torch.allclose(out.permute(0, 3, 1, 2), gx, atol=1e-9)
 
 
+def test_upconv_halo_packing_fp32_rows():
+    """fp32 operand rows hold 32 channels (128 B): the packed halo up-conv weights are
+    (Cin/32, 5, 2, Cout, 32) and carry the same entries as the 64-channel packing."""
+    from gfa_amd import layouts
+    w = torch.randn(64, 128, 3, 3, generator=torch.Generator().manual_seed(2), dtype=torch.float64)
+    p32 = layouts.upconv_halo_matrix(w, torch.float32)
+    p64 = layouts.upconv_halo_matrix(w, torch.float64)
+    assert tuple(p32.shape) == (4, 5, 2, 64, 32) and tuple(p64.shape) == (2, 5, 2, 64, 64)
+    a = p32.double().permute(2, 1, 3, 0, 4).reshape(2, 5, 64, 128)
+    b = p64.permute(2, 1, 3, 0, 4).reshape(2, 5, 64, 128)
+    assert torch.allclose(a, b.float().double())
+
+
 def test_psp_checkpoint_split(tmp_path):
     """A pSp/e4e checkpoint (state_dict with encoder.* / decoder.* keys, latent_avg, opts) saved
     by torch.save loads with weights_only=True and splits into the generator and e4e dicts."""

@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--pgd-steps", type=int, default=20)
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--size", type=int, default=256)
-    ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16"])
+    ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16", "fp32"])
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     T, S, B = bench.DT[a.dtype], a.size, a.batch

@@ -100,9 +100,9 @@ SIGNATURES = {
     "mia_tap_grad": (c_int, [P, P, P, c_int64, c_float, c_int, c_int, P]),
     "mia_image_grad": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_float, c_int, P]),
     "mia_pgd_update": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, c_float,
-                               c_float, c_float, c_float, c_int, P]),
+                               c_float, c_float, c_float, P, c_int, P]),
     "mia_grad_assemble": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float,
-                                  c_float, c_int, P]),
+                                  c_float, P, c_int, P]),
     "mia_cw_init": (c_int, [P, P, c_int64, P]),
     "mia_cw_tanh": (c_int, [P, P, c_int64, P]),
     "mia_cw_grad": (c_int, [P, P, P, P, c_int64, c_float, c_float, P]),

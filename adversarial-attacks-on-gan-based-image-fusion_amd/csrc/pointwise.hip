@@ -757,15 +757,24 @@ __device__ __forceinline__ float assemble_grad(int64_t i, float xv, float x0v, c
   return g;
 }
 
+// A non-finite gradient element (an fp16 loss-scale overflow upstream, or a NaN in the
+// weights) marks its image in nonfinite[n]; the host reads the flags once per attack
+// (pgd.AttackEngine) instead of letting sign(NaN) = 0 freeze the pixel silently. Racing writers
+// store the same value.
+__device__ __forceinline__ void flag_nonfinite(int* nonfinite, int64_t i, int S, float g) {
+  if (nonfinite && !__builtin_isfinite(g)) nonfinite[i / ((int64_t)3 * S * S)] = 1;
+}
+
 template <typename T>
 __global__ void pgd_update_kernel(float* __restrict__ x, const float* __restrict__ x0,
                                   const T* __restrict__ gv, const float* __restrict__ genc, int N,
                                   int S, int pf, int cpad, int enc_res, float coef_img, float a,
-                                  float e, float lo, float hi) {
+                                  float e, float lo, float hi, int* __restrict__ nonfinite) {
   const int64_t total = (int64_t)N * 3 * S * S;
   for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
     const float xv = x[i], x0v = x0[i];
     const float g = assemble_grad(i, xv, x0v, gv, genc, S, pf, cpad, enc_res, coef_img);
+    flag_nonfinite(nonfinite, i, S, g);
     x[i] = project1(xv, x0v, g, a, e, lo, hi);
   }
 }
@@ -774,10 +783,14 @@ template <typename T>
 __global__ void grad_assemble_kernel(const float* __restrict__ x, const float* __restrict__ x0,
                                      const T* __restrict__ gv, const float* __restrict__ genc,
                                      float* __restrict__ g, int N, int S, int pf, int cpad,
-                                     int enc_res, float coef_img, float scale) {
+                                     int enc_res, float coef_img, float scale,
+                                     int* __restrict__ nonfinite) {
   const int64_t total = (int64_t)N * 3 * S * S;
-  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB)
-    g[i] = scale * assemble_grad(i, x[i], x0[i], gv, genc, S, pf, cpad, enc_res, coef_img);
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
+    const float v = scale * assemble_grad(i, x[i], x0[i], gv, genc, S, pf, cpad, enc_res, coef_img);
+    flag_nonfinite(nonfinite, i, S, v);
+    g[i] = v;
+  }
 }
 
 // ---- C&W L2 in tanh space (torchattacks CW, interpolation.py:98-193), images in [-1, 1]:
@@ -1142,23 +1155,27 @@ extern "C" int mia_image_grad(const float* rec, const float* t, const void* g_vg
 
 extern "C" int mia_pgd_update(float* x, const float* x0, const void* g_vgg, const float* g_enc,
                               int N, int S, int pf, int cpad, int enc_res, float coef_img, float a,
-                              float e, float lo, float hi, int dtype, void* stream) {
+                              float e, float lo, float hi, int* nonfinite, int dtype,
+                              void* stream) {
   MIA_CHECK_ARG(x && x0 && pf >= 1 && S % pf == 0 && enc_res >= 1 && S % enc_res == 0, "bad args");
   const int64_t total = (int64_t)N * 3 * S * S;
   MIA_DISPATCH_DTYPE(dtype, T,
       MIA_LAUNCH(pgd_update_kernel<T>, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0, x, x0,
-                 (const T*)g_vgg, g_enc, N, S, pf, cpad, enc_res, coef_img, a, e, lo, hi));
+                 (const T*)g_vgg, g_enc, N, S, pf, cpad, enc_res, coef_img, a, e, lo, hi,
+                 nonfinite));
   return MIA_OK;
 }
 
 extern "C" int mia_grad_assemble(const float* x, const float* x0, const void* g_vgg,
                                  const float* g_enc, float* g, int N, int S, int pf, int cpad,
-                                 int enc_res, float coef_img, float scale, int dtype, void* stream) {
+                                 int enc_res, float coef_img, float scale, int* nonfinite,
+                                 int dtype, void* stream) {
   MIA_CHECK_ARG(x && x0 && g && pf >= 1 && S % pf == 0 && (!g_enc || S % enc_res == 0), "bad args");
   const int64_t total = (int64_t)N * 3 * S * S;
   MIA_DISPATCH_DTYPE(dtype, T,
       MIA_LAUNCH(grad_assemble_kernel<T>, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0, x,
-                 x0, (const T*)g_vgg, g_enc, g, N, S, pf, cpad, enc_res, coef_img, scale));
+                 x0, (const T*)g_vgg, g_enc, g, N, S, pf, cpad, enc_res, coef_img, scale,
+                 nonfinite));
   return MIA_OK;
 }
 

@@ -39,17 +39,29 @@ def gather_shards(local, n_total, group=None):
     return torch.cat(pieces, 0)
 
 
-def attack_distributed(net, imgs, eps, steps, *, target, group=None, **kw):
+def attack_distributed(net, imgs, eps, steps, *, target, group=None, random_start=False, seed=0,
+                       **kw):
     """Every rank passes the full batch (or at least its shape-compatible copy); each attacks its
-    contiguous shard on its own GPU and all ranks return the full adversarial batch."""
-    from .pgd import attack
+    contiguous shard on its own GPU and all ranks return the full adversarial batch.
+
+    * A rank whose shard is empty (world > n) runs no attack and contributes only the zero padding
+      of the all-gather (every rank must still enter the collective).
+    * The random-start noise is drawn ONCE for the full batch from ``seed`` (the same host draw as
+      a single-GPU ``attack(..., random_start=True, seed=seed)``) and sliced per shard, so the
+      output does not depend on the world size."""
+    from . import pgd
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     n = imgs.shape[0]
     lo, hi = shard_bounds(n, world, rank)
+    gather_dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else net.decoder.device
+    if hi == lo:
+        local = torch.zeros((0,) + tuple(imgs.shape[1:]), dtype=torch.float32, device=gather_dev)
+        return gather_shards(local, n, group).to(imgs.device)
     tgt = target if target.shape[0] == 1 else target[lo:hi]
-    dev = net.decoder.device
-    local = attack(net, imgs[lo:hi], eps, steps, target=tgt, **kw).to(dev)
-    if dist.get_backend(group) == "gloo":
-        local = local.cpu()
-    return gather_shards(local, n, group).to(imgs.device)
+    noise = None
+    if random_start:
+        noise = pgd.make_start_noise(tuple(imgs.shape), seed)[lo:hi]
+    local = pgd.attack(net, imgs[lo:hi], eps, steps, target=tgt, random_start=random_start,
+                       seed=seed, start_noise=noise, **kw)
+    return gather_shards(local.to(gather_dev, torch.float32), n, group).to(imgs.device)

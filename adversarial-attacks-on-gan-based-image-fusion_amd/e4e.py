@@ -166,7 +166,6 @@ class E4EEncoder:
         b0l = self.heads[0]["lb"]
         self.lin_bias = [b0l] + [(h["lb"] + b0l).contiguous() for h in self.heads[1:]]
         self.flops_fwd_per_image = self._count_flops()
-        self._plans = {}
         self._side = None
 
     def _side_streams(self):
@@ -290,8 +289,11 @@ class E4EEncoder:
         return lat
 
     def _plan(self, ws, N, kind, lat):
-        key = (kind, N, lat.data_ptr())
-        plan = self._plans.get(key)
+        # cached in the workspace (a plan keeps its operand tensors alive): a fresh AttackEngine
+        # per attack() call must not pin the previous calls' buffers through the encoder
+        plans = ws.cache.setdefault("e4e.plans", {})
+        key = (id(self), kind, N, lat.data_ptr())
+        plan = plans.get(key)
         if plan is not None:
             return plan
         f32 = torch.float32
@@ -311,7 +313,7 @@ class E4EEncoder:
             for i in range(1, S):
                 plan.add(gf[i], D, 1, N, D, [(lat[:, i, :], S * D, 1, self.heads[i]["lw"], D, 1,
                                               D)])
-        self._plans[key] = plan
+        plans[key] = plan
         return plan
 
     @staticmethod

@@ -439,8 +439,10 @@ def image_grad(rec, t, g_vgg, g_img, pf, coef):
     return g_img
 
 
-def pgd_update(x, x0, g_vgg, g_enc, pf, enc_res, coef_img, a, e, lo=-1.0, hi=1.0):
+def pgd_update(x, x0, g_vgg, g_enc, pf, enc_res, coef_img, a, e, lo=-1.0, hi=1.0,
+               nonfinite=None):
     N, _, S, _ = x.shape
+    _numel_ok(nonfinite, N, torch.int32, "nonfinite")
     _need(x0, x.shape, torch.float32, "x0")
     cpad = 8
     if g_vgg is not None:
@@ -450,13 +452,14 @@ def pgd_update(x, x0, g_vgg, g_enc, pf, enc_res, coef_img, a, e, lo=-1.0, hi=1.0
         _numel_ok(g_enc, N * 3 * enc_res * enc_res, torch.float32, "g_enc")
     gdt = dt(g_vgg) if g_vgg is not None else _lib.MIA_F32
     call("mia_pgd_update", ptr(x), ptr(x0), ptr(g_vgg), ptr(g_enc), N, S, pf, cpad, enc_res,
-         float(coef_img), float(a), float(e), float(lo), float(hi), gdt, stream())
+         float(coef_img), float(a), float(e), float(lo), float(hi), ptr(nonfinite), gdt, stream())
     return x
 
 
-def grad_assemble(x, x0, g_vgg, g_enc, g, pf, enc_res, coef_img, scale=1.0):
+def grad_assemble(x, x0, g_vgg, g_enc, g, pf, enc_res, coef_img, scale=1.0, nonfinite=None):
     """∇_x L (fp32 NCHW) from the VGG input-path and encoder gradients (mia_grad_assemble)."""
     N, C, S, S2 = x.shape
+    _numel_ok(nonfinite, N, torch.int32, "nonfinite")
     if C != 3 or S != S2:
         raise ValueError("x must be (N,3,S,S)")
     _need(x0, x.shape, torch.float32, "x0")
@@ -469,7 +472,7 @@ def grad_assemble(x, x0, g_vgg, g_enc, g, pf, enc_res, coef_img, scale=1.0):
         _need(g_enc, (N, 3, enc_res, enc_res), torch.float32, "g_enc")
     T = g_vgg.dtype if g_vgg is not None else torch.float32
     call("mia_grad_assemble", ptr(x), ptr(x0), ptr(g_vgg), ptr(g_enc), ptr(g), N, S, pf, cpad,
-         enc_res, float(coef_img), float(scale), dt(T), stream())
+         enc_res, float(coef_img), float(scale), ptr(nonfinite), dt(T), stream())
     return g
 
 

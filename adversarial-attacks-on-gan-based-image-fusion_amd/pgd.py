@@ -26,7 +26,15 @@ from .weights import ENC_POOL_RES, STYLE_DIM
 from .workspace import Workspace
 
 LOSS_WEIGHTS = dict(lat_t=10.0, lat_o=-1.0, img_rec_t=1.0, vgg_rec_t=0.1, img_o=10.0, vgg_img=1.0)
-DEFAULT_LOSS_SCALE = {torch.float32: 1.0, torch.float16: 2.0 ** 16, torch.bfloat16: 2.0 ** 16}
+# Gradient (loss) scale per compute dtype. fp16: its range tops out at 65504, and the e4e
+# encoder's backward from the latent terms (weight 10·2/(n_latent·512) per element) reaches
+# 1e3–1e4 × λ… at λ = 2^16 whole images overflowed to inf/NaN (3 of 8 at 256², measured); at
+# λ ≤ 2^12 none did and the gradient's sign agreed with fp32 on 99.98 % of the significant
+# pixels, at λ = 2^8 too — 2^8 keeps 16× headroom. bf16 has fp32's exponent range: no scaling.
+# An overflow that still happens is caught (per-image non-finite flags, read once per attack):
+# the engine divides λ by RESCALE and re-runs the attack, at most MAX_RESCALES times.
+DEFAULT_LOSS_SCALE = {torch.float32: 1.0, torch.float16: 2.0 ** 8, torch.bfloat16: 1.0}
+RESCALE, MAX_RESCALES = 16.0, 4
 
 
 def _f32(v):
@@ -45,13 +53,18 @@ class AttackEngine:
         self.R = min(self.size, 256)  # the objective pools to 256² (attack_main2.py:590-591)
         self.pf = self.size // self.R
         self.ws = Workspace(synth.device)
-        self.loss_scale = float(loss_scale if loss_scale is not None
-                                else DEFAULT_LOSS_SCALE[self.dtype])
         self.w = dict(weights)
         R = self.R
         self.tap_numel = [64 * R * R, 64 * R * R, 128 * (R // 4) ** 2,
                           512 * ops.pool_out(R // 4, True) ** 2]
-        lam = self.loss_scale
+        self.rescales = 0  # loss-scale reductions of the last attack (overflow re-runs)
+        self.set_loss_scale(loss_scale if loss_scale is not None
+                            else DEFAULT_LOSS_SCALE[self.dtype])
+
+    def set_loss_scale(self, lam):
+        """λ: every gradient coefficient carries it (fp16 range); the projections and the Adam /
+        C&W updates divide it back out (sign(λ·g) = sign(g))."""
+        self.loss_scale = lam = float(lam)
         S2 = 3 * self.size * self.size
         nl = self.G.n_latent * STYLE_DIM
         self.c_lat_t = lam * self.w["lat_t"] * 2.0 / nl
@@ -74,6 +87,7 @@ class AttackEngine:
         self.N = N
         self.x0 = x0
         self.t = t
+        self.nonfinite = ops.zero_(ws.get("nonfinite", (N,), torch.int32))
         self.lat_t = ws.get("ref.lat_t", (N, self.G.n_latent, STYLE_DIM), torch.float32)
         self.lat_t.copy_(self._encode(t, "ref.in")[0])
         self.lat_o = ws.get("ref.lat_o", (N, self.G.n_latent, STYLE_DIM), torch.float32)
@@ -148,8 +162,29 @@ class AttackEngine:
     def step(self, x, a, e):
         g_xv, g_enc = self.gradient(x)
         ops.pgd_update(x, self.x0, g_xv, g_enc, self.pf, ENC_POOL_RES, self.c_img_o, _f32(a),
-                       _f32(e))
+                       _f32(e), nonfinite=self.nonfinite)
         return x
+
+    def overflowed(self):
+        """Images whose gradient had a non-finite element since prepare() (one host sync)."""
+        return self.nonfinite.nonzero().flatten().tolist()
+
+    def _with_rescale(self, run_once):
+        """Run an attack; if any image's gradient overflowed, lower λ and run it again (fp16).
+        A non-finite gradient at λ that cannot be lowered (fp32 / bf16, or after MAX_RESCALES)
+        raises: sign(NaN) = 0 would otherwise leave those pixels silently unattacked."""
+        self.rescales = 0
+        while True:
+            out = run_once()
+            bad = self.overflowed()
+            if not bad:
+                return out
+            if self.dtype != torch.float16 or self.rescales >= MAX_RESCALES:
+                raise FloatingPointError(
+                    f"non-finite gradient for images {bad[:8]} (dtype {self.dtype}, loss scale "
+                    f"{self.loss_scale:g}): check the weights / inputs, or run fp32")
+            self.set_loss_scale(self.loss_scale / RESCALE)
+            self.rescales += 1
 
     def full_gradient(self, x):
         """∇_x L (unscaled, fp32 NCHW) at x."""
@@ -180,13 +215,17 @@ class AttackEngine:
     def _full_grad(self, x, g, loss=None):
         """g ← ∇_x L (loss-scaled, fp32 NCHW) by the gradient-assembly kernel."""
         g_xv, g_enc = self.gradient(x, loss)
-        ops.grad_assemble(x, self.x0, g_xv, g_enc, g, self.pf, ENC_POOL_RES, self.c_img_o)
+        ops.grad_assemble(x, self.x0, g_xv, g_enc, g, self.pf, ENC_POOL_RES, self.c_img_o,
+                          nonfinite=self.nonfinite)
         return g
 
     def run_adam(self, x0, t, steps, lr=0.01, betas=(0.9, 0.999), eps=1e-8):
         """``optimize_vgg`` literal mode (interpolation.py:743-843): Adam(lr) on the pixels,
         descending L, no ε-ball or clamp. The gradient carries the loss scale λ, so Adam's eps is
         scaled by λ too (m̂/(√v̂ + λ·eps) on λ·g ≡ m̂/(√v̂ + eps) on g)."""
+        return self._with_rescale(lambda: self._run_adam(x0, t, steps, lr, betas, eps))
+
+    def _run_adam(self, x0, t, steps, lr, betas, eps):
         self.prepare(x0, t)
         ws = self.ws
         x = ws.get("adv", x0.shape, torch.float32)
@@ -204,6 +243,9 @@ class AttackEngine:
         [-1,1] space: adv = tanh(w); cost = Σ‖(adv − x0)/2‖² + c·Σ L_n(adv); Adam(lr) on w;
         best-L2 tracking with success = L_n(adv) < L_n(x0); early stop every steps//10 when the
         cost rises (one host sync there). See oracle.attack_ref.cw_attack."""
+        return self._with_rescale(lambda: self._run_cw(x0, t, steps, c, lr, betas, eps))
+
+    def _run_cw(self, x0, t, steps, c, lr, betas, eps):
         self.prepare(x0, t)
         ws = self.ws
         N = x0.shape[0]
@@ -244,6 +286,10 @@ class AttackEngine:
 
     def run(self, x0, t, steps, eps, alpha, random_start=False, start_noise=None):
         """PGD-steps from x0 toward the objective; returns the adversarial images (new tensor)."""
+        return self._with_rescale(
+            lambda: self._run_pgd(x0, t, steps, eps, alpha, random_start, start_noise))
+
+    def _run_pgd(self, x0, t, steps, eps, alpha, random_start, start_noise):
         e, a = 2.0 * eps, 2.0 * alpha
         self.prepare(x0, t)
         x = self.ws.get("adv", x0.shape, torch.float32)
@@ -269,9 +315,16 @@ def _check_images(imgs, size, name):
 NORMS = ("linf", "adam", "l2_cw")
 
 
-def attack(net, imgs, eps, steps, *, target=None, vgg=None, alpha=2 / 255, random_start=False,
-           seed=0, norm="linf", loss="gan_vgg", loss_scale=None, lr=0.01, cw_c=1e-4,
-           return_info=False):
+def make_start_noise(shape, seed):
+    """The random-start draw: host-seeded U(-1,1) of the FULL batch shape (scaled by e in the
+    kernel); ``attack_distributed`` slices it per shard so every world size sees the same noise."""
+    g = torch.Generator().manual_seed(int(seed))
+    return torch.rand(shape, generator=g) * 2 - 1
+
+
+def attack(net, imgs, eps, steps, *, target=None, vgg=None, alpha=0.01, random_start=False,
+           seed=0, start_noise=None, norm="linf", loss="gan_vgg", loss_scale=None, lr=0.01,
+           cw_c=1e-4, return_info=False):
     """Craft adversarial images against the GAN fusion pipeline.
 
     net     pSp-like bundle: net.encoder, net.decoder (.size), net.latent_avg, net.opts
@@ -280,6 +333,10 @@ def attack(net, imgs, eps, steps, *, target=None, vgg=None, alpha=2 / 255, rando
             on CPU or GPU; not modified.
     eps     L∞ radius in [0,1] pixel units (8/255 in the reference's PGD call, interpolation.py:1343).
     steps   iterations (PGD: 1 with alpha=eps and random_start=False is FGSM).
+    alpha   PGD step in [0,1] pixel units; default 0.01 = the reference's PGD call
+            (interpolation.py:1343; torchattacks' own default is 2/255).
+    start_noise  optional host U(-1,1) tensor of imgs' shape for random_start (default: drawn
+            from ``seed`` by ``make_start_noise(imgs.shape, seed)``).
     target  white-box target image(s) (N or 1, 3, S, S) — the ``img_target`` of optimize_vgg.
     norm    'linf'  — torchattacks PGD rule (interpolation.py:62-96) on the objective;
             'adam'  — optimize_vgg literal (interpolation.py:743-843): Adam(lr) on the pixels,
@@ -320,8 +377,11 @@ def attack(net, imgs, eps, steps, *, target=None, vgg=None, alpha=2 / 255, rando
     eng = AttackEngine(net.encoder.impl, net.decoder.impl, vgg.impl, loss_scale=loss_scale)
     noise = None
     if random_start:
-        g = torch.Generator().manual_seed(int(seed))
-        noise = (torch.rand(x0.shape, generator=g) * 2 - 1).to(dev)
+        if start_noise is None:
+            start_noise = make_start_noise(tuple(x0.shape), seed)
+        if tuple(start_noise.shape) != tuple(x0.shape):
+            raise ValueError("start_noise must have the shape of imgs")
+        noise = start_noise.to(dev, torch.float32).contiguous()
     if norm == "linf":
         adv = eng.run(x0, t, int(steps), float(eps), float(alpha), random_start, noise)
     elif norm == "adam":
@@ -331,7 +391,7 @@ def attack(net, imgs, eps, steps, *, target=None, vgg=None, alpha=2 / 255, rando
     adv = adv.to(imgs.device)
     if return_info:
         info = dict(loss=eng.loss(adv.to(dev)), steps=int(steps), eps=eps, alpha=alpha, norm=norm,
-                    dtype=str(eng.dtype), loss_scale=eng.loss_scale)
+                    dtype=str(eng.dtype), loss_scale=eng.loss_scale, rescales=eng.rescales)
         return adv, info
     return adv
 

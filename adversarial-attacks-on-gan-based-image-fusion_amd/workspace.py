@@ -7,6 +7,9 @@ class Workspace:
     def __init__(self, device):
         self.device = torch.device(device)
         self._bufs = {}
+        # objects derived from this workspace's buffers (e.g. the e4e GemmPlans, which hold
+        # pointers into them): they live and die with the workspace, never with the network
+        self.cache = {}
 
     def get(self, name, shape, dtype):
         shape = tuple(int(s) for s in shape)
@@ -21,3 +24,4 @@ class Workspace:
 
     def clear(self):
         self._bufs.clear()
+        self.cache.clear()

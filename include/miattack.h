@@ -259,10 +259,12 @@ int mia_image_grad(const float* rec, const float* t, const void* g_vgg, float* g
 /* Sign-project step (K11, interpolation.py:92-94, cost = −L):
  *   g = unpool_pf(g_vgg)/pf² + coef_img·(x − x0) + unpool(g_enc)/(pool_enc²)   [fp32]
  *   adv = x + a·sign(−g); δ = clamp(adv − x0, −e, e); x = clamp(x0 + δ, lo, hi)   (in place)
- * g_vgg may be NULL; g_enc may be NULL (else (N,3,enc_res,enc_res) fp32). */
+ * g_vgg may be NULL; g_enc may be NULL (else (N,3,enc_res,enc_res) fp32).
+ * nonfinite: NULL or int[N]; set to 1 for every image with a non-finite gradient element (an
+ * fp16 loss-scale overflow: the host lowers the scale and re-runs). */
 int mia_pgd_update(float* x, const float* x0, const void* g_vgg, const float* g_enc, int N,
                    int S, int pf, int cpad, int enc_res, float coef_img, float a, float e,
-                   float lo, float hi, int dtype, void* stream);
+                   float lo, float hi, int* nonfinite, int dtype, void* stream);
 /* PGD random start (torchattacks PGD.forward, interpolation.py:73-76): x = clamp(x0 + e·u, lo, hi),
  * u = host-seeded U(-1,1) draws. */
 /* ∇_x L as an fp32 image: scale·(coef_img·(x − x0) + avg_pool adjoints of the VGG input-path
@@ -271,7 +273,7 @@ int mia_pgd_update(float* x, const float* x0, const void* g_vgg, const float* g_
  * (optimize_vgg, interpolation.py:767,822) and C&W modes. */
 int mia_grad_assemble(const float* x, const float* x0, const void* g_vgg, const float* g_enc,
                       float* g, int N, int S, int pf, int cpad, int enc_res, float coef_img,
-                      float scale, int dtype, void* stream);
+                      float scale, int* nonfinite, int dtype, void* stream);
 /* C&W L2 in tanh space (torchattacks CW, interpolation.py:98-193), images in [-1,1]:
  * w = atanh(x) (x clamped to ±(1 − 2^-20)); adv = tanh(w);
  * g_w = (½(adv − x) + c·scale·g_f)·(1 − adv²) for cost = Σ‖(adv − x)/2‖² + c·Σ f(adv);

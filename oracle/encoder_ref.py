@@ -22,6 +22,35 @@ import torch
 import torch.nn.functional as F
 
 BN_EPS = 1e-5
+# Teacher-forced activation masks (tests only): {key: bool tensor (NCHW)}. Under forced_masks the
+# positive set of a PReLU / LeakyReLU is taken from the given mask instead of the sign of its own
+# fp64 pre-activation, so the oracle's backward follows the same piecewise-linear branch as the
+# device run (a pre-activation within rounding of 0 may take either branch). Keys: "in" (input
+# layer PReLU), "body.{i}" (unit i's PReLU), "styles.{i}.{j}" (head i's j-th LeakyReLU(0.01)).
+_FORCED = None
+
+
+class forced_masks:
+    def __init__(self, masks):
+        self.masks = masks
+
+    def __enter__(self):
+        global _FORCED
+        _FORCED = self.masks
+        return self
+
+    def __exit__(self, *exc):
+        global _FORCED
+        _FORCED = None
+
+
+def _leaky(x, slope, key):
+    """PReLU (per-channel tensor slope) / LeakyReLU (float slope), optionally mask-forced."""
+    m = _FORCED.get(key) if _FORCED is not None else None
+    if m is None:
+        return F.prelu(x, slope) if torch.is_tensor(slope) else F.leaky_relu(x, slope)
+    s = slope.view(1, -1, 1, 1) if torch.is_tensor(slope) else slope
+    return torch.where(m.to(x.device), x, s * x)
 E4E_STAGES = [(64, 64, 3), (64, 128, 4), (128, 256, 14), (256, 512, 3)]  # helpers.get_blocks(50)
 COARSE, MIDDLE = 3, 7
 
@@ -61,7 +90,7 @@ def bottleneck_ir_se(p, pre, x, cin, depth, stride):
         sc = _bn(p, pre + ".shortcut_layer.1", sc)
     r = _bn(p, pre + ".res_layer.0", x)
     r = F.conv2d(r, _w(p, pre + ".res_layer.1.weight", x), stride=1, padding=1)
-    r = F.prelu(r, _w(p, pre + ".res_layer.2.weight", x))
+    r = _leaky(r, _w(p, pre + ".res_layer.2.weight", x), pre)
     r = F.conv2d(r, _w(p, pre + ".res_layer.3.weight", x), stride=stride, padding=1)
     r = _bn(p, pre + ".res_layer.4", r)
     # SEModule(depth, 16)
@@ -77,7 +106,7 @@ def gradual_style_block(p, pre, x, spatial):
     for j in range(int(math.log2(spatial))):
         x = F.conv2d(x, _w(p, f"{pre}.convs.{2 * j}.weight", x), _w(p, f"{pre}.convs.{2 * j}.bias", x),
                      stride=2, padding=1)
-        x = F.leaky_relu(x, 0.01)
+        x = _leaky(x, 0.01, f"{pre}.{j}")
     x = x.reshape(-1, 512)
     w = _w(p, pre + ".linear.weight", x)
     return F.linear(x, w * (1.0 / math.sqrt(w.shape[1])), _w(p, pre + ".linear.bias", x))
@@ -91,7 +120,7 @@ def e4e_features(p, x):
     """Input layer + IR-SE50 body; returns (c1, c2, c3) (Encoder4Editing.forward, i = 6, 20, 23)."""
     x = F.conv2d(x, _w(p, "input_layer.0.weight", x), padding=1)
     x = _bn(p, "input_layer.1", x)
-    x = F.prelu(x, _w(p, "input_layer.2.weight", x))
+    x = _leaky(x, _w(p, "input_layer.2.weight", x), "in")
     c = {}
     for i, (cin, depth, stride) in enumerate(_units()):
         x = bottleneck_ir_se(p, f"body.{i}", x, cin, depth, stride)

@@ -1,0 +1,72 @@
+"""Shared builders for the GPU parity tests (not a test module)."""
+import torch
+
+from gfa_amd import pgd
+from gfa_amd.vgg import VGGNet
+from gfa_amd.weights import (make_e4e_weights, make_encoder_weights, make_generator_weights,
+                             make_vgg_weights)
+
+
+def nchw(t):
+    return t.permute(0, 3, 1, 2).double().cpu()
+
+
+def seeded(seed, shape):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(shape, generator=g) * 2 - 1
+
+
+def engine(size, dtype, cuda, encoder="e4e", gen_seed=0, enc_seed=1, vgg_seed=1234):
+    """AttackEngine over the reference's three networks (seeded random init) and the oracle's
+    parameter dicts for the same weights."""
+    from gfa_amd.e4e import E4EEncoder
+    from gfa_amd.encoder import SyntheticEncoder
+    from gfa_amd.stylegan2 import SynthesisNet
+    from oracle import vgg_ref
+    gp = make_generator_weights(size, seed=gen_seed)
+    ep = (make_e4e_weights(size, seed=enc_seed) if encoder == "e4e"
+          else make_encoder_weights(size, seed=enc_seed))
+    vs = make_vgg_weights(vgg_seed)
+    enc = (E4EEncoder(ep, size, dtype=dtype, device=cuda) if encoder == "e4e"
+           else SyntheticEncoder(ep, size, device=cuda))
+    eng = pgd.AttackEngine(enc, SynthesisNet(gp, size, dtype=dtype, device=cuda),
+                           VGGNet(vs, dtype=dtype, device=cuda))
+    return eng, (gp, vgg_ref.load_positional(vs), ep)
+
+
+def to64(params):
+    gp, vp, ep = params
+    return ({k: v.double() for k, v in gp.items()},
+            {k: (w.double(), b.double()) for k, (w, b) in vp.items()},
+            {k: (v.double() if torch.is_tensor(v) else v) for k, v in ep.items()})
+
+
+def e4e_masks(enc):
+    """The device run's PReLU / LeakyReLU branch per activation (sign of the stored activation =
+    sign of the pre-activation, slopes > 0), keyed as oracle.encoder_ref.forced_masks expects.
+    Reflects the encoder's most recent forward."""
+    m = {"in": nchw(enc._a0) > 0}
+    for i, U in enumerate(enc.units):
+        m[f"body.{i}"] = nchw(U["_a1"]) > 0
+    for i, hd in enumerate(enc.heads):
+        for j, a in enumerate(hd["_acts"]):
+            m[f"styles.{i}.{j}"] = nchw(a) > 0
+    return m
+
+
+def grad_stats(got, ref, big_frac=1e-2):
+    """(‖Δ‖/‖ref‖, max|Δ|/max|ref|, sign agreement where |ref| > big_frac·max|ref|)."""
+    got, ref = got.double().cpu(), ref.double().cpu()
+    nrm = ((got - ref).norm() / ref.norm()).item()
+    mx = ((got - ref).abs().max() / ref.abs().max()).item()
+    big = ref.abs() > big_frac * ref.abs().max()
+    agree = (torch.sign(got[big]) == torch.sign(ref[big])).float().mean().item()
+    return nrm, mx, agree
+
+
+def free():
+    """Release the caching allocator's blocks between the large tests (callers drop their
+    engines first)."""
+    import gc
+    gc.collect()
+    torch.cuda.empty_cache()

@@ -5,6 +5,7 @@ import socket
 
 import torch
 import torch.distributed as dist
+import pytest
 import torch.multiprocessing as mp
 
 
@@ -44,3 +45,60 @@ def test_gather_shards_world2_uneven():
             p.join(timeout=120)
             assert p.exitcode == 0
         assert all(ok for _, ok in res), res
+
+
+def _fake_attack(net, imgs, eps, steps, *, target, random_start=False, seed=0, start_noise=None,
+                 **kw):
+    """CPU elementwise stand-in for pgd.attack: depends on the image, its own target row and the
+    random-start noise, so shard order, target slicing and noise slicing are all visible."""
+    assert imgs.shape[0] >= 1, "attack() must not run on an empty shard"
+    out = imgs * 0.5 + target.expand_as(imgs) * 0.25
+    if random_start:
+        assert start_noise is not None and start_noise.shape == imgs.shape
+        out = out + 1e-3 * start_noise
+    return out + steps * eps
+
+
+def _attack_worker(rank, world, port, n, tgt1, rs, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import types
+
+    import gfa_import  # noqa: F401
+    from gfa_amd import dist as gdist
+    from gfa_amd import pgd
+    pgd.attack = _fake_attack  # the distributed wrapper looks it up at call time
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(3)
+        imgs = torch.rand(n, 3, 4, 4, generator=g) * 2 - 1
+        target = torch.rand(1 if tgt1 else n, 3, 4, 4, generator=g) * 2 - 1
+        net = types.SimpleNamespace(decoder=types.SimpleNamespace(device=torch.device("cpu")))
+        got = gdist.attack_distributed(net, imgs, 8 / 255, 3, target=target, random_start=rs,
+                                       seed=11)
+        noise = pgd.make_start_noise(tuple(imgs.shape), 11) if rs else None
+        want = _fake_attack(net, imgs, 8 / 255, 3, target=target, random_start=rs,
+                            start_noise=noise)
+        out_q.put((rank, torch.equal(got, want)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,tgt1,rs", [(2, 5, False, True), (3, 7, True, False),
+                                             (3, 8, False, True), (3, 2, False, True)])
+def test_attack_distributed_matches_single_process(world, n, tgt1, rs):
+    """attack_distributed over gloo (world 2 and 3, uneven n, world > n with an empty shard,
+    per-image or broadcast target, random start) returns on every rank exactly the single-process
+    result: shard order, target slicing, the world-size-independent noise draw and the trimmed
+    all-gather."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_attack_worker, args=(r, world, port, n, tgt1, rs, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in res), res

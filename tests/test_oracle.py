@@ -181,3 +181,56 @@ def test_ssim_oracle_filter_form_matches_window_loops():
     g = metrics_ref.rgb2gray(img)
     assert np.allclose(g, 0.2125 * img[0] + 0.7154 * img[1] + 0.0721 * img[2])
     assert abs(metrics_ref.cal_ssmi(img, img) - 1.0) < 1e-12
+
+
+# ---- the objective pinned to the reference's own optimize_vgg -------------------------------------
+# tests/golden/objective_golden.npz: oracle/gen_golden_objective.py ran the reference's
+# optimize_vgg (interpolation.py:743-843, unchanged, fp64) with the oracle networks in the slots of
+# the un-vendored modules and recorded its losses, gradients and final image.
+
+@pytest.fixture(scope="module")
+def objg():
+    return np.load(os.path.join(GOLDEN, "objective_golden.npz"))
+
+
+def _rel(a, b):
+    a, b = torch.as_tensor(np.asarray(a)).double(), torch.as_tensor(np.asarray(b)).double()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-300)).item()
+
+
+def test_oracle_adam_mode_matches_reference_optimize_vgg(objg):
+    """attack_ref.adam_attack + attack_ref.objective (fp64) reproduce the reference's own
+    optimize_vgg run (linear stand-in encoder, 3 Adam iterations at 256²): every iteration's
+    inversion_loss (the reference's '%.5f' text), gradient (slices + random projections of the
+    whole tensor) and the final image."""
+    from oracle import gen_golden_objective as gen
+    torch.set_num_threads(os.cpu_count() or 1)
+    n, lr, size = int(objg["n_iters"]), float(objg["lr"]), int(objg["size"])
+    gp, vp, ep = gen.networks("linear")
+    x0, t = gen.seeded_pair(size)
+    img, losses, grads = attack_ref.adam_attack(gp, vp, ep, x0.double(), t.double(), size, n,
+                                                lr=lr, dtype=torch.float64, return_trace=True)
+    probes = gen.projections(size)
+    ref_l = objg["linear/losses"]
+    assert np.all(np.abs(np.array(losses) - ref_l) <= 5.1e-6), (losses, ref_l)
+    for k, g in enumerate(grads):
+        assert _rel(g[gen.SLICE].numpy(), objg[f"linear/grad{k}/slice"]) < 1e-9, k
+        proj = [float((p * g).sum()) for p in probes]
+        assert _rel(proj, objg[f"linear/grad{k}/proj"]) < 1e-9, k
+    assert _rel(img[gen.SLICE].numpy(), objg["linear/img/slice"]) < 1e-12
+    assert _rel([float((p * img).sum()) for p in probes], objg["linear/img/proj"]) < 1e-12
+
+
+def test_oracle_e4e_objective_matches_reference_optimize_vgg(objg):
+    """With the e4e restatement in the encoder slot: the objective and its full gradient at x0
+    (iteration 0 of the reference's optimize_vgg) from attack_ref.loss_grad (fp64)."""
+    from oracle import gen_golden_objective as gen
+    torch.set_num_threads(os.cpu_count() or 1)
+    size = int(objg["size"])
+    gp, vp, ep = gen.networks("e4e")
+    x0, t = gen.seeded_pair(size)
+    refs = attack_ref.Refs(gp, vp, ep, x0.double(), t.double(), size)
+    L, g = attack_ref.loss_grad(gp, vp, ep, x0.double(), refs, size)
+    assert abs(float(L) - float(objg["e4e/losses"][0])) <= 5.1e-6
+    assert _rel(g.numpy(), objg["e4e/grad0/full"]) < 1e-6  # stored as float32
+    assert _rel(g[gen.SLICE].numpy(), objg["e4e/grad0/slice"]) < 1e-9

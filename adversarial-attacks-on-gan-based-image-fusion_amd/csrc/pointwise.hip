@@ -1247,10 +1247,32 @@ extern "C" int mia_repeat(const void* src, void* dst, int64_t bytes, int count, 
              (const uint8_t*)src, (uint8_t*)dst, bytes, count);
 }
 
+// Byte fill on the caller's stream as a kernel of our own (no hipMemsetAsync: the runtime's fill
+// path crashed inside rocprofv3 --pmc collection, and a plain kernel is capturable like the rest):
+// 16-byte stores when the buffer and length allow, else 4-byte, else bytes.
+template <typename V>
+__global__ void fill_kernel(V* __restrict__ dst, V v, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)mia::TPB + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * mia::TPB)
+    dst[i] = v;
+}
+
 extern "C" int mia_memset(void* dst, int value, int64_t bytes, void* stream) {
   MIA_CHECK_ARG(dst && bytes >= 0, "bad args");
   if (bytes == 0) return MIA_OK;
-  if (hipMemsetAsync(dst, value, (size_t)bytes, (hipStream_t)stream) != hipSuccess)
-    return mia::set_error("hipMemsetAsync failed");
+  const unsigned b = (unsigned)value & 0xffu, w = b * 0x01010101u;
+  const uintptr_t a = (uintptr_t)dst;
+  if (a % 16 == 0 && bytes % 16 == 0) {
+    const int64_t n = bytes / 16;
+    MIA_LAUNCH(fill_kernel<uint4>, dim3(blocks_for(n, mia::TPB, 65536)), dim3(mia::TPB), 0,
+               (uint4*)dst, make_uint4(w, w, w, w), n);
+  } else if (a % 4 == 0 && bytes % 4 == 0) {
+    const int64_t n = bytes / 4;
+    MIA_LAUNCH(fill_kernel<unsigned>, dim3(blocks_for(n, mia::TPB, 65536)), dim3(mia::TPB), 0,
+               (unsigned*)dst, w, n);
+  } else {
+    MIA_LAUNCH(fill_kernel<unsigned char>, dim3(blocks_for(bytes, mia::TPB, 65536)),
+               dim3(mia::TPB), 0, (unsigned char*)dst, (unsigned char)b, bytes);
+  }
   return MIA_OK;
 }

@@ -26,7 +26,8 @@ BN_EPS = 1e-5
 # positive set of a PReLU / LeakyReLU is taken from the given mask instead of the sign of its own
 # fp64 pre-activation, so the oracle's backward follows the same piecewise-linear branch as the
 # device run (a pre-activation within rounding of 0 may take either branch). Keys: "in" (input
-# layer PReLU), "body.{i}" (unit i's PReLU), "styles.{i}.{j}" (head i's j-th LeakyReLU(0.01)).
+# layer PReLU), "body.{i}" (unit i's PReLU), "body.{i}.se" (its SE block's ReLU, (N, C/16, 1, 1)),
+# "styles.{i}.{j}" (head i's j-th LeakyReLU(0.01)).
 _FORCED = None
 
 
@@ -95,7 +96,7 @@ def bottleneck_ir_se(p, pre, x, cin, depth, stride):
     r = _bn(p, pre + ".res_layer.4", r)
     # SEModule(depth, 16)
     s = F.adaptive_avg_pool2d(r, 1)
-    s = F.relu(F.conv2d(s, _w(p, pre + ".res_layer.5.fc1.weight", x)))
+    s = _leaky(F.conv2d(s, _w(p, pre + ".res_layer.5.fc1.weight", x)), 0.0, pre + ".se")
     s = torch.sigmoid(F.conv2d(s, _w(p, pre + ".res_layer.5.fc2.weight", x)))
     return r * s + sc
 

@@ -102,6 +102,8 @@ def main():
     ap.add_argument("stats")
     ap.add_argument("--fetch")
     ap.add_argument("--write")
+    ap.add_argument("--mfma", help="counter_collection.csv of the SQ_VALU_MFMA_BUSY_CYCLES / "
+                    "GRBM_GUI_ACTIVE / SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE pass")
     ap.add_argument("--steps", type=int, default=3, help="bench steps in the trace (warmup+timed)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--title", default="")
@@ -161,6 +163,33 @@ def main():
             w = wr.get(k, [1, 0.0])
             lines.append(f"| `{short(k)}` | {2 * fe[k][1] / fe[k][0] / 1e6:.2f} | "
                          f"{w[1] / max(w[0], 1) / 1e6:.2f} |")
+    if a.mfma:
+        c = {k: read_pmc(a.mfma, k) for k in ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE",
+                                              "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE")}
+        busy, gui = c["SQ_VALU_MFMA_BUSY_CYCLES"], c["GRBM_GUI_ACTIVE"]
+
+        def agg(d, pat=CONV):
+            return sum(v[1] for k, v in d.items() if pat.search(k)) / 1024.0  # undo KiB scaling
+
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs → ÷8 = the dispatch's cycles; the MFMA busy
+        # cycles are summed over every SIMD (256 CUs × 4) → busy fraction of the matrix pipes
+        frac = agg(busy) / (agg(gui) / 8.0 * 1024.0)
+        ldsc = agg(c["SQ_LDS_BANK_CONFLICT"]) / max(agg(c["SQ_LDS_IDX_ACTIVE"]), 1.0)
+        out["conv_kernel"]["mfma_busy_frac"] = frac
+        out["conv_kernel"]["lds_bank_conflict_frac"] = ldsc
+        lines += ["", "PMC pass SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE / SQ_LDS_BANK_CONFLICT / "
+                  "SQ_LDS_IDX_ACTIVE (MFMA busy = busy cycles ÷ (GRBM_GUI_ACTIVE/8 × 1024 SIMDs); "
+                  "LDS conflict = conflict cycles ÷ LDS-active cycles):",
+                  f"conv kernels: MFMA busy {frac:.3f}, LDS bank-conflict cycles {ldsc:.4f} of "
+                  f"LDS-active", "", "| kernel | launches | MFMA busy | LDS conflict |",
+                  "|---|---|---|---|"]
+        for k in sorted(busy, key=lambda k: -busy[k][1])[:40]:
+            g = gui.get(k, [1, 0.0])[1] / 1024.0
+            ia = c["SQ_LDS_IDX_ACTIVE"].get(k, [1, 0.0])[1]
+            bc = c["SQ_LDS_BANK_CONFLICT"].get(k, [1, 0.0])[1]
+            lines.append(f"| `{short(k)}` | {busy[k][0]} | "
+                         f"{busy[k][1] / 1024.0 / max(g / 8.0 * 1024.0, 1.0):.3f} | "
+                         f"{bc / ia if ia else 0.0:.4f} |")
     open(a.out + ".md", "w").write("\n".join(lines) + "\n")
     json.dump(out, open(a.out + ".json", "w"), indent=1)
     print(json.dumps(out))

@@ -48,6 +48,7 @@ def e4e_masks(enc):
     m = {"in": nchw(enc._a0) > 0}
     for i, U in enumerate(enc.units):
         m[f"body.{i}"] = nchw(U["_a1"]) > 0
+        m[f"body.{i}.se"] = (U["_u"] > 0).cpu()[:, :, None, None]  # relu(fc1(avg)), (N, C/16)
     for i, hd in enumerate(enc.heads):
         for j, a in enumerate(hd["_acts"]):
             m[f"styles.{i}.{j}"] = nchw(a) > 0

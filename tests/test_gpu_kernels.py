@@ -6,7 +6,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from gfa_amd import layouts, ops
+from gfa_amd import _lib, layouts, ops
 from oracle import attack_ref, stylegan2_ref
 
 pytestmark = pytest.mark.gpu
@@ -868,3 +868,17 @@ def test_conv_thin32_layers(cuda, monkeypatch, dtype, N, H, W, mode, thin):
     assert rel_err(nchw(y), ref) < 2 * TOL[dtype]
     if sd is not None:
         assert rel_err(sd, sd_ref) < 2 * TOL[dtype]
+
+
+@pytest.mark.parametrize("off,nbytes", [(0, 4096), (0, 4100), (4, 64), (1, 33), (16, 1 << 20),
+                                        (3, 7), (0, 16)])
+@pytest.mark.parametrize("value", [0, 0xA5])
+def test_memset_fill_kernel(cuda, off, nbytes, value):
+    """mia_memset (the library's own fill kernel, 16-/4-/1-byte paths by alignment) writes exactly
+    [off, off + nbytes) and nothing around it."""
+    buf = torch.full((nbytes + 64,), 0x3C, dtype=torch.uint8, device=cuda)
+    _lib.call("mia_memset", buf.data_ptr() + off, value, nbytes, ops.stream())
+    got = buf.cpu()
+    want = torch.full((nbytes + 64,), 0x3C, dtype=torch.uint8)
+    want[off:off + nbytes] = value
+    assert torch.equal(got, want)

@@ -8,7 +8,14 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmiattack.so")
+# MIA_F32_ARITH=native loads the A/B build whose fp32 convs run v_mfma_f32_16x16x4_f32
+# (csrc/Makefile `native`); the default build runs them as exact three-way bf16 splits
+# (conv_common.h, mfma_chunk<float>). Everything else is the same source.
+F32_ARITH = os.environ.get("MIA_F32_ARITH", "bf16x6")
+if F32_ARITH not in ("bf16x6", "native"):
+    raise ValueError(f"MIA_F32_ARITH must be bf16x6 or native, not {F32_ARITH!r}")
+LIB_PATH = os.path.join(HERE, "libmiattack.so" if F32_ARITH == "bf16x6"
+                        else "libmiattack_f32native.so")
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 P = c_void_p

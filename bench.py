@@ -41,8 +41,23 @@ from gfa_amd.weights import (make_e4e_weights, make_encoder_weights,  # noqa: E4
 METRIC = "attacked images/sec, PGD-20 L∞ ε=8/255 at 256², 1/2/4/8 MI355X"  # BASELINE.json
 DT = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
 DT_NAME = {"fp32": "f32", "fp16": "f16", "bf16": "bf16"}
-# MI355X_MICROARCH.md chip table: dense MFMA peaks (TFLOP/s); fp32 = v_mfma_f32_16x16x4_f32
-PEAK_TFLOPS = {"fp32": 157.3, "fp16": 2500.0, "bf16": 2500.0}
+# MI355X_MICROARCH.md chip table: dense MFMA peaks (TFLOP/s). fp32 runs on the bf16 matrix pipe
+# as exact three-way bf16 splits with six bf16 products per fp32 product (conv_common.h,
+# mfma_chunk<float>): its peak is 2500 / 6 = 416.7 fp32 TFLOP/s. MIA_F32_ARITH=native (the A/B
+# build on v_mfma_f32_16x16x4_f32): 157.3.
+PEAK_TFLOPS = {"fp32": 2500.0 / 6, "fp32native": 157.3, "fp16": 2500.0, "bf16": 2500.0}
+F32_ARITH_NOTE = {
+    "bf16x6": "fp32 storage and accumulation; each fp32 operand split exactly into three bf16 "
+              "terms (hi+mid+lo), six bf16 products per fp32 product on v_mfma_f32_16x16x32_bf16 "
+              "(dropped terms < 2^-23|ab|; error vs fp64 = the native fp32 MFMA's, "
+              "tests/test_gpu_kernels.py::test_fp32_arithmetic_is_fp32_accurate)",
+    "native": "fp32 on v_mfma_f32_16x16x4_f32"}
+
+
+def arith_key(dtype):
+    """Profile / peak key of a compute dtype: fp32 is split by its arithmetic."""
+    from gfa_amd import _lib
+    return "fp32native" if dtype == "fp32" and _lib.F32_ARITH == "native" else dtype
 
 
 def parse():
@@ -215,8 +230,9 @@ def run_leg(args, dtype, steps, warmup, dev, world, rank, roofline):
 def roofline_record(args, dtype, r):
     tot_ms, n = r["conv_busy_ms"], r["conv_launches"]
     ach = r["conv_flops"] / (tot_ms * 1e-3) / 1e12
-    peak = PEAK_TFLOPS[dtype]
-    pmc, src = pmc_profile(dtype, args.batch, args.size, args.pgd_steps, args.encoder)
+    key = arith_key(dtype)
+    peak = PEAK_TFLOPS[key]
+    pmc, src = pmc_profile(key, args.batch, args.size, args.pgd_steps, args.encoder)
     rec = {"kernel": "3x3 conv: every conv API call of the step (mia::conv_halo_kernel, "
                      "mia::upconv_halo_kernel + its edge launch, mia::conv_kernel, "
                      "mia::conv_wres_kernel, mia::conv_thin_*: StyledConv fwd, up-conv, dgrads, "
@@ -231,6 +247,11 @@ def roofline_record(args, dtype, r):
            "share_of_step_time": tot_ms / (r["elapsed"] * 1e3)}
     if pmc and pmc.get("mfma_busy_frac") is not None:
         rec["mfma_busy_frac_pmc"] = pmc["mfma_busy_frac"]
+    if dtype == "fp32":
+        from gfa_amd import _lib
+        rec["arithmetic"] = F32_ARITH_NOTE[_lib.F32_ARITH]
+        rec["peak_note"] = ("2500 TFLOP/s dense bf16 / 6 products" if key == "fp32"
+                            else "v_mfma_f32_16x16x4_f32")
     return rec
 
 
@@ -285,7 +306,8 @@ def main():
                    "effective_tflops": flops_img_step * B * r["iters"] * world
                    / (elapsed / args.steps) / 1e12,
                    "peak_hbm_gb_per_gpu": r["peak_hbm_gb"],
-                   "output_in_eps_ball_and_finite": r["output_ok"]},
+                   "output_in_eps_ball_and_finite": r["output_ok"],
+                   **({"fp32_arithmetic": arith_key("fp32")} if args.dtype == "fp32" else {})},
     }
     if "conv_busy_ms" in r:
         out["roofline"] = roofline_record(args, args.dtype, r)

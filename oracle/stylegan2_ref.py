@@ -82,11 +82,33 @@ def modulated_conv2d(p, prefix, x, w, demodulate=True, upsample=False, s=None):
     return out
 
 
+# Teacher-forced LeakyReLU branches (tests only): {styled-conv prefix: bool tensor (NCHW)}, the
+# device run's positive set per layer (see vgg_ref.forced_masks).
+_FORCED = None
+
+
+class forced_masks:
+    def __init__(self, masks):
+        self.masks = masks
+
+    def __enter__(self):
+        global _FORCED
+        _FORCED = self.masks
+        return self
+
+    def __exit__(self, *exc):
+        global _FORCED
+        _FORCED = None
+
+
 def styled_conv(p, prefix, x, w, noise, upsample=False, s=None):
     out = modulated_conv2d(p, prefix + ".conv", x, w, demodulate=True, upsample=upsample, s=s)
     out = out + p[prefix + ".noise.weight"].to(x.dtype) * noise.to(x.dtype)
     b = p[prefix + ".activate.bias"].to(x.dtype)
-    return F.leaky_relu(out + b.view(1, -1, 1, 1), 0.2) * math.sqrt(2.0)
+    pre = out + b.view(1, -1, 1, 1)
+    if _FORCED is not None and prefix in _FORCED:
+        return torch.where(_FORCED[prefix], pre, 0.2 * pre) * math.sqrt(2.0)
+    return F.leaky_relu(pre, 0.2) * math.sqrt(2.0)
 
 
 def to_rgb(p, prefix, x, w, skip=None, s=None):

@@ -22,25 +22,58 @@ def load_positional(state_dict):
     return params
 
 
+# Teacher-forced branches (tests only): a list of {key: bool tensor (NCHW)} consumed one per
+# vgg_forward call. Keys: the conv names (ReLU positive set) and "pool1" / "pool2" / "pool3" (the
+# one-hot argmax of every 2×2 window at the pool's input resolution). Under forcing the oracle
+# follows the device run's branch wherever a pre-activation or a window's maximum is within
+# rounding of a tie; the function is the same piecewise-linear one.
+_FORCED = None
+
+
+class forced_masks:
+    def __init__(self, per_call):
+        self.per_call = list(per_call)
+
+    def __enter__(self):
+        global _FORCED
+        _FORCED = self.per_call
+        return self
+
+    def __exit__(self, *exc):
+        global _FORCED
+        _FORCED = None
+
+
 def vgg_forward(params, image):
     """vgg.py:44-64. Returns (conv1_1, conv1_2, conv3_2[=pool2 output], conv4_2)."""
+    forced = _FORCED.pop(0) if _FORCED else None
+
     def conv(name, x):
         w, b = params[name]
-        return F.relu(F.conv2d(x, w.to(x.dtype), b.to(x.dtype), padding=1))
+        y = F.conv2d(x, w.to(x.dtype), b.to(x.dtype), padding=1)
+        if forced is not None:
+            return torch.where(forced[name], y, torch.zeros_like(y))
+        return F.relu(y)
+
+    def pool(name, x, ceil_mode=False):
+        if forced is not None:  # the forced window maxima: a sum over each window of x·one-hot
+            xm = torch.where(forced[name], x, torch.zeros_like(x))
+            return F.avg_pool2d(xm, 2, 2, ceil_mode=ceil_mode, divisor_override=1)
+        return F.max_pool2d(x, 2, 2, ceil_mode=ceil_mode)
 
     out = conv("conv1_1", image)
     c11 = out
     out = conv("conv1_2", out)
     c12 = out
-    out = F.max_pool2d(out, 2, 2)
+    out = pool("pool1", out)
     out = conv("conv2_1", out)
     out = conv("conv2_2", out)
-    out = F.max_pool2d(out, 2, 2)
+    out = pool("pool2", out)
     c32 = out
     out = conv("conv3_1", out)
     out = conv("conv3_2", out)
     out = conv("conv3_3", out)
-    out = F.max_pool2d(out, 2, 2, ceil_mode=True)
+    out = pool("pool3", out, ceil_mode=True)
     out = conv("conv4_1", out)
     out = conv("conv4_2", out)
     return c11, c12, c32, out

@@ -32,3 +32,14 @@ def cuda():
     from gfa_amd import _lib
     _lib.load()  # fail loudly if the library is missing: no fallback path exists
     return torch.device("cuda:0")
+
+
+def pytest_make_parametrize_id(config, val, argname):
+    # readable ids for torch dtypes (-k float32 / float16 / bfloat16 select a precision)
+    try:
+        import torch
+        if isinstance(val, torch.dtype):
+            return str(val).replace("torch.", "")
+    except Exception:
+        pass
+    return None

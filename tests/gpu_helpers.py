@@ -55,6 +55,90 @@ def e4e_masks(enc):
     return m
 
 
+def g_masks(G, ws, n=None):
+    """The device generator's LeakyReLU branch per StyledConv (sign of the stored activation
+    g.pre{i}), keyed by the oracle's styled-conv prefixes (conv1, convs.0, convs.1, …)."""
+    m = {}
+    i = 0
+    while f"g.pre{i}" in ws._bufs:
+        a = nchw(ws._bufs[f"g.pre{i}"]) > 0
+        m["conv1" if i == 0 else f"convs.{i - 1}"] = a if n is None else a[:n]
+        i += 1
+    return m
+
+
+def pool_onehot(x):
+    """One-hot of the first maximum of every 2×2 window (row-major order, ceil-mode padding with
+    −inf), the tie rule of maxpool2_bwd_kernel (pointwise.hip)."""
+    N, C, H, W = x.shape
+    xp = torch.nn.functional.pad(x, (0, W % 2, 0, H % 2), value=float("-inf"))
+    Hp, Wp = xp.shape[2], xp.shape[3]
+    win = xp.reshape(N, C, Hp // 2, 2, Wp // 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(
+        N, C, Hp // 2, Wp // 2, 4)
+    oh = torch.nn.functional.one_hot(win.argmax(-1), 4).bool()
+    oh = oh.reshape(N, C, Hp // 2, Wp // 2, 2, 2).permute(0, 1, 2, 4, 3, 5).reshape(N, C, Hp, Wp)
+    return oh[:, :, :H, :W]
+
+
+def vgg_masks(a, n=None):
+    """The device VGG forward's branches (ReLU positive sets from the stored post-ReLU outputs,
+    pool window argmaxes from the pool inputs), keyed as oracle.vgg_ref.forced_masks expects."""
+    sl = (lambda t: t) if n is None else (lambda t: t[:n])
+    m = {}
+    for k, name in (("c11", "conv1_1"), ("c12", "conv1_2"), ("c21", "conv2_1"), ("c22", "conv2_2"),
+                    ("c31", "conv3_1"), ("c32", "conv3_2"), ("c33", "conv3_3"), ("c41", "conv4_1"),
+                    ("c42", "conv4_2")):
+        m[name] = sl(nchw(a[k]) > 0)
+    for k, name in (("c12", "pool1"), ("c22", "pool2"), ("c33", "pool3")):
+        m[name] = sl(pool_onehot(nchw(a[k])))
+    return m
+
+
+class capture_vgg:
+    """Records vgg_masks() of every device VGG forward while active (the gradient pass runs the
+    reconstruction path first, then the input path, as the oracle objective does)."""
+
+    def __init__(self, V, n=None):
+        self.V, self.n, self.masks = V, n, []
+
+    def __enter__(self):
+        self._fwd = self.V.forward
+
+        def fwd(x, ws, tag):
+            a = self._fwd(x, ws, tag)
+            self.masks.append(vgg_masks(a, self.n))
+            return a
+        self.V.forward = fwd
+        return self
+
+    def __exit__(self, *exc):
+        self.V.forward = self._fwd
+
+
+class forced_all:
+    """Oracle context following every branch of the device's most recent gradient pass: e4e
+    PReLU / LeakyReLU / SE ReLU, generator LeakyReLU, VGG ReLU and pool argmax (both VGG passes,
+    captured with capture_vgg). ``n``: the first n images only."""
+
+    def __init__(self, eng, vgg_cap, n=None):
+        from oracle import encoder_ref, stylegan2_ref, vgg_ref
+        em = e4e_masks(eng.E)
+        if n is not None:
+            em = {k: v[:n] for k, v in em.items()}
+        self.ctx = [encoder_ref.forced_masks(em),
+                    stylegan2_ref.forced_masks(g_masks(eng.G, eng.ws, n)),
+                    vgg_ref.forced_masks(vgg_cap.masks[-2:])]
+
+    def __enter__(self):
+        for c in self.ctx:
+            c.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        for c in reversed(self.ctx):
+            c.__exit__(*exc)
+
+
 def grad_stats(got, ref, big_frac=1e-2):
     """(‖Δ‖/‖ref‖, max|Δ|/max|ref|, sign agreement where |ref| > big_frac·max|ref|)."""
     got, ref = got.double().cpu(), ref.double().cpu()

@@ -882,3 +882,39 @@ def test_memset_fill_kernel(cuda, off, nbytes, value):
     want = torch.full((nbytes + 64,), 0x3C, dtype=torch.uint8)
     want[off:off + nbytes] = value
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("path", ["halo", "generic", "upconv"])
+def test_fp32_arithmetic_is_fp32_accurate(cuda, monkeypatch, path):
+    """The fp32 convs run as exact three-way bf16 splits with six products (conv_common.h,
+    mfma_chunk<float>; the dropped mid·lo, lo·mid, lo·lo terms are < 2^-23·|ab|). At the largest
+    K of the attack (9·512 = 4608) the error against fp64 is set by the fp32 accumulation, as for
+    the native v_mfma_f32_16x16x4_f32 build (MIA_F32_ARITH=native, measured on these seeded
+    operands: max-abs 1.12e-5 / 1.22e-5 / 5.2e-6, norm-relative 1.18e-6 / 1.19e-6 / 6.6e-7 for
+    halo / generic / upconv; the split build: 1.18e-5 / 9.1e-6 / 5.6e-6 and 1.05e-6 / 1.05e-6 /
+    5.8e-7). Bound: 2× the native figures."""
+    monkeypatch.setenv("MIA_CONV_HALO", "0" if path == "generic" else "1")
+    g = torch.Generator().manual_seed(77)
+    N, H, Cin, Cout = 2, 16, 512, 256
+    x = torch.randn(N, Cin, H, H, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)
+    if path == "upconv":  # the sub-pixel up-sampling conv (transposed, stride 2) on the halo kernel
+        ref = F.conv_transpose2d(x.double(), w.double().transpose(0, 1), stride=2)
+        t = torch.empty(N, 2 * H + 1, 2 * H + 1, Cout, device=cuda)
+        ops.upconv_fwd(nhwc(x, torch.float32).to(cuda),
+                       [m.to(cuda) for m in layouts.upconv_subpixel_matrices(w, torch.float32)],
+                       t, cout=Cout, w_up=layouts.upconv_halo_matrix(w, torch.float32).to(cuda))
+        got = t.permute(0, 3, 1, 2).double().cpu()
+    else:
+        ref = F.conv2d(x.double(), w.double(), padding=1)
+        y = torch.empty(N, H, H, Cout, device=cuda)
+        ops.conv3x3(nhwc(x, torch.float32).to(cuda), layouts.fwd_matrix(w, torch.float32).to(cuda),
+                    y, cout=Cout)
+        got = nchw(y).cpu()
+    torch.cuda.synchronize()
+    err = (got - ref).abs()
+    native = {"halo": (1.12e-5, 1.18e-6), "generic": (1.22e-5, 1.19e-6), "upconv": (5.2e-6, 6.6e-7)}
+    mx, nrm = err.max().item(), (err.norm() / ref.norm()).item()
+    print(f"{path}: max-abs err {mx:.3e}, norm-relative {nrm:.3e} (native fp32 MFMA "
+          f"{native[path][0]:.2e}, {native[path][1]:.2e})")
+    assert mx <= 2 * native[path][0] and nrm <= 2 * native[path][1]

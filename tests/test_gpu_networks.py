@@ -203,8 +203,22 @@ def test_cw_mode_matches_oracle(cuda, c):
     eng, x0, t, (gp, vp, ep) = _engine(size, torch.float32, N, cuda, seed=6)
     adv = eng.run_cw(x0.to(cuda), t.to(cuda), steps, c=c, lr=lr).cpu()
     ref = attack_ref.cw_attack(gp, vp, ep, x0, t, size, steps, c=c, lr=lr)
-    d = (adv - ref).abs()
-    assert (d > 1e-3).float().mean().item() <= 1e-2
+    # step 0 compares f(tanh(atanh(x0))) with f(x0): equal up to rounding, so an image whose
+    # step-0 margin is within fp32 noise may take either branch; it must then match the oracle
+    # run that takes the other branch for that image
+    with torch.no_grad():
+        refs = attack_ref.Refs(gp, vp, ep, x0, t, size)
+        lim = 1.0 - 2.0 ** -20
+        f0 = attack_ref.objective(gp, vp, ep, x0, refs, size, per_image=True)
+        f1 = attack_ref.objective(gp, vp, ep, torch.tanh(torch.atanh(x0.clamp(-lim, lim))), refs,
+                                  size, per_image=True)
+    tie = (f1 - f0).abs() <= 1e-5 * f0.abs()
+    alt = attack_ref.cw_attack(gp, vp, ep, x0, t, size, steps, c=c, lr=lr, flip_step0=tie) \
+        if tie.any() else ref
+    for n in range(N):
+        bad = ((adv[n] - ref[n]).abs() > 1e-3).float().mean().item()
+        bad_alt = ((adv[n] - alt[n]).abs() > 1e-3).float().mean().item()
+        assert min(bad, bad_alt if tie[n] else 1.0) <= 1e-2, (n, bad, bad_alt, tie.tolist())
     assert adv.abs().max().item() <= 1.0
 
 

@@ -234,3 +234,36 @@ def test_oracle_e4e_objective_matches_reference_optimize_vgg(objg):
     assert abs(float(L) - float(objg["e4e/losses"][0])) <= 5.1e-6
     assert _rel(g.numpy(), objg["e4e/grad0/full"]) < 1e-6  # stored as float32
     assert _rel(g[gen.SLICE].numpy(), objg["e4e/grad0/slice"]) < 1e-9
+
+
+def test_forced_branches_reproduce_the_free_forward():
+    """Forcing the oracle's VGG ReLU / pool-argmax and generator LeakyReLU branches to the ones its
+    own forward takes leaves the output unchanged (the forced forms are the same functions)."""
+    from gpu_helpers import pool_onehot
+    from oracle import stylegan2_ref, vgg_ref
+    from gfa_amd.weights import make_generator_weights, make_vgg_weights
+    g = torch.Generator().manual_seed(5)
+    vp = {k: (w.double(), b.double()) for k, (w, b) in
+          vgg_ref.load_positional(make_vgg_weights(3)).items()}
+    x = torch.rand(2, 3, 18, 18, generator=g, dtype=torch.float64) * 2 - 1
+    free = vgg_ref.vgg_forward(vp, x)
+    # the branches of the free forward, recomputed layer by layer
+    masks, out = {}, x
+    for name in vgg_ref.LAYERS:
+        w, b = vp[name]
+        pre = torch.nn.functional.conv2d(out, w, b, padding=1)
+        masks[name] = pre > 0
+        out = torch.relu(pre)
+        pool = {"conv1_2": "pool1", "conv2_2": "pool2", "conv3_3": "pool3"}.get(name)
+        if pool:
+            masks[pool] = pool_onehot(out)
+            out = torch.nn.functional.max_pool2d(out, 2, 2, ceil_mode=pool == "pool3")
+    with vgg_ref.forced_masks([masks]):
+        forced = vgg_ref.vgg_forward(vp, x)
+    for a, b in zip(free, forced):
+        assert torch.equal(a, b)
+    gp = {k: v.double() for k, v in make_generator_weights(32, seed=0).items()}
+    lat = torch.randn(1, 8, 512, generator=g, dtype=torch.float64)
+    img = stylegan2_ref.synthesis(gp, lat, 32)
+    with stylegan2_ref.forced_masks({}):  # no entry: the free branch
+        assert torch.equal(img, stylegan2_ref.synthesis(gp, lat, 32))

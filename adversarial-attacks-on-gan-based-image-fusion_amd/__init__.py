@@ -12,7 +12,8 @@ Submodules import lazily so the package can be imported (and the library inspect
 without a GPU; any compute call without the library or a GPU raises.
 """
 __all__ = ["attack", "fgsm", "build_net", "vgg16", "get_latents", "StyleFusionSimple",
-           "interpolation", "partial_adv_fusion_arithmetic", "attack_distributed"]
+           "interpolation", "partial_adv_fusion_arithmetic", "attack_distributed",
+           "patch_attack", "patch_white_box"]
 
 
 def __getattr__(name):
@@ -26,6 +27,9 @@ def __getattr__(name):
     if name in ("StyleFusionSimple", "interpolation", "partial_adv_fusion_arithmetic"):
         from . import style_fusion_simple as _f
         return getattr(_f, name)
+    if name in ("patch_attack", "patch_white_box"):
+        from . import patch as _p
+        return _p.attack if name == "patch_attack" else _p.patch_white_box
     if name == "attack_distributed":
         from .dist import attack_distributed
         return attack_distributed

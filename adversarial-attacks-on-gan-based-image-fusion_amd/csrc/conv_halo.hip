@@ -37,13 +37,8 @@ struct HaloTile {
   static constexpr int FM = FM_, WM = PH_ / FM_, WN = 2, FN = BN_ / 32;
   static constexpr int PH = PH_, PW = 16, NW = WM * WN, NT = 64 * NW, BM = PH * PW, BN = BN_;
   static constexpr int WAVES_PER_SIMD = (NW == 4 && FM == 4) ? 2 : 1;  // launch-bounds hint
-#if defined(MIA_HALO_EXP) && MIA_HALO_EXP >= 2
-  static constexpr int STAGES = MIA_HALO_EXP;
-  static constexpr int NHBUF = 1;  // tuning experiment: one halo buffer (wrong results)
-#else
   static constexpr int STAGES = STAGES_;
   static constexpr int NHBUF = NHBUF_;
-#endif
   static constexpr int HW = PW + 2, HROWS = (PH + 2) * HW;  // 324 / 180 halo pixels
   static constexpr int HPIECES = (HROWS + 7) / 8;          // DMA pieces of 8 rows (1 KB)
   static constexpr int HBUF = HPIECES * 8 * ROWB;          // per halo buffer
@@ -162,9 +157,6 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
     }
   };
   auto issue_h = [&](int cb, int j, int buf) {  // H-wave: its halo piece j of channel block cb
-#if defined(MIA_HALO_EXP) && MIA_HALO_EXP == 1
-    return;  // tuning experiment: no halo traffic
-#endif
     const T* a = src[j] ? src[j] + cb * BK : zero;
     __builtin_amdgcn_global_load_lds((gptr_t)a,
                                      (lptr_t)(hbuf + buf * HBUF + (hw + HWAVES * j) * 1024), 16,
@@ -285,42 +277,7 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
     halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, n0, wm, wn, lane, -1, -1, nullptr,
                                 k.prered ? (float*)smem : nullptr, TL::WM, TL::BN);
   } else if constexpr (EPI == -1) {
-#if defined(MIA_HALO_STOREONLY)  // tuning experiment: raw accumulator stores only (wrong results)
-    if constexpr (sizeof(T) == 2 && FN % 2 == 0) {
-      T* Yp = (T*)p.y;
-      const int lrow = lane >> 4;
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int m = (n * H + y0 + wm * FM + i) * W + x0 + (lane & 15);
-#pragma unroll
-        for (int q = 0; q < FN / 2; ++q) {
-          typedef T t2 __attribute__((ext_vector_type(2)));
-          unsigned a2[2], b2[2];
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const t2 ta = {(T)acc[i][2 * q][2 * h], (T)acc[i][2 * q][2 * h + 1]};
-            const t2 tb = {(T)acc[i][2 * q + 1][2 * h], (T)acc[i][2 * q + 1][2 * h + 1]};
-            a2[h] = __builtin_bit_cast(unsigned, ta);
-            b2[h] = __builtin_bit_cast(unsigned, tb);
-            const auto r = __builtin_amdgcn_permlane16_swap(a2[h], b2[h], false, false);
-            a2[h] = r[0];
-            b2[h] = r[1];
-          }
-          const int c = n0 + wn * FN * 16 + 16 * (2 * q + (lrow & 1)) + 8 * (lrow >> 1);
-          *(uint4*)(Yp + (size_t)m * p.Cout + c) = make_uint4(a2[0], a2[1], b2[0], b2[1]);
-        }
-      }
-    }
-#elif defined(MIA_HALO_NOEPI)  // tuning experiment: no epilogue (wrong results)
-    float z = 0.f;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) z += acc[i][j][0] + acc[i][j][3];
-    if (z == 1234.5f) ((float*)p.y)[tid] = z;
-#else
     halo_epilogue<T, TL>(k, acc, n, y0, x0, n0, wm, wn, lane);
-#endif
   } else {
     __syncthreads();
     const int img_row = n * H + y0;

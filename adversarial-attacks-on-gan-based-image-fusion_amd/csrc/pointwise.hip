@@ -849,6 +849,31 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
   }
 }
 
+// Adversarial patch (code/attack/patch/adversarial_patch.py:131-134, attack_main2.py:413-420):
+//   patch −= g (the full-image gradient, step 1);  adv = (1 − m)·img + m·patch;
+//   adv = clamp(adv, lo, hi) with lo / hi = min / max of the clean images.
+// Each torch op is one fp32 rounding (no contraction), so the result is bit-identical to torch's
+// fp32 ops for the same gradient. `g` may be null (composite only, patch_white_box). `shared` =
+// numel of mask / patch when they are one image broadcast over the batch (0: same shape as img).
+__global__ void patch_update_kernel(float* __restrict__ patch, const float* __restrict__ g,
+                                    const float* __restrict__ img, const float* __restrict__ mask,
+                                    float* __restrict__ adv, int64_t len, int64_t shared, float lo,
+                                    float hi) {
+#pragma clang fp contract(off)
+  for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < len; i += (int64_t)gridDim.x * TPB) {
+    const int64_t j = shared ? i % shared : i;
+    float pv = patch[j];
+    if (g) {
+      pv = pv - g[i];
+      patch[j] = pv;
+    }
+    const float m = mask[j];
+    const float a = (1.f - m) * img[i];
+    const float b = m * pv;
+    adv[i] = fminf(fmaxf(a + b, lo), hi);
+  }
+}
+
 // PixelNorm of the mapping network input (rosinality PixelNorm): y = x / sqrt(mean(x²) + eps)
 // over each row of `cols` values; one block per row.
 __global__ void pixel_norm_kernel(const float* __restrict__ x, float* __restrict__ y, int cols,
@@ -1225,6 +1250,16 @@ extern "C" int mia_adam_step(float* p, const float* g, float* m, float* v, int64
   const float bc2sqrt = sqrtf(1.f - powf(beta2, (float)t));
   MIA_LAUNCH(adam_kernel, dim3(blocks_for(len, TPB, 65536)), dim3(TPB), 0, p, g, m, v, len, lr,
              beta1, beta2, eps, bc1, bc2sqrt);
+}
+
+extern "C" int mia_patch_update(float* patch, const float* g, const float* img, const float* mask,
+                                float* adv, int64_t len, int64_t shared, float lo, float hi,
+                                void* stream) {
+  MIA_CHECK_ARG(patch && img && mask && adv && len > 0 && shared >= 0 && lo <= hi, "bad args");
+  MIA_CHECK_ARG(!g || !shared, "a gradient step needs a per-image patch (shared = 0)");
+  MIA_CHECK_ARG(!shared || len % shared == 0, "len must be a multiple of shared");
+  MIA_LAUNCH(patch_update_kernel, dim3(blocks_for(len, TPB, 65536)), dim3(TPB), 0, patch, g, img,
+             mask, adv, len, shared, lo, hi);
 }
 
 extern "C" int mia_pixel_norm(const float* x, float* y, int rows, int cols, float eps,

@@ -530,6 +530,22 @@ def adam_step(p, g, m, v, lr, beta1, beta2, eps, t):
     return p
 
 
+def patch_update(patch, g, img, mask, adv, lo, hi):
+    """adversarial_patch.py:131-134: patch −= g (g None: composite only); adv ← clamp((1−m)·img +
+    m·patch, lo, hi). patch / mask: img's shape, or one image's shape (composite only)."""
+    _need(adv, img.shape, torch.float32, "adv")
+    _need(img, img.shape, torch.float32, "img")
+    full = patch.numel() == img.numel()
+    if not full and (g is not None or img.numel() % patch.numel()):
+        raise ValueError("patch / mask: img's shape, or one image's shape for the composite")
+    _need(mask, patch.shape, torch.float32, "mask")
+    if g is not None:
+        _need(g, img.shape, torch.float32, "g")
+    call("mia_patch_update", ptr(patch), ptr(g) if g is not None else None, ptr(img), ptr(mask),
+         ptr(adv), img.numel(), 0 if full else patch.numel(), float(lo), float(hi), stream())
+    return adv
+
+
 def gemm(M, N, K, alpha, A, sam, sak, B, sbk, sbn, beta, C, scm, scn, bias=None):
     """C[m,n] = alpha Σ_k A[m*sam+k*sak] B[k*sbk+n*sbn] + beta C[m*scm+n*scn] + bias[n] (fp32).
     Offsets into A/B/C are given by passing views (data_ptr of a strided view is honoured)."""

@@ -26,6 +26,8 @@ from .weights import ENC_POOL_RES, STYLE_DIM
 from .workspace import Workspace
 
 LOSS_WEIGHTS = dict(lat_t=10.0, lat_o=-1.0, img_rec_t=1.0, vgg_rec_t=0.1, img_o=10.0, vgg_img=1.0)
+# the patch attack's loss (code/attack/patch/adversarial_patch.py:125): only −MSE(E(x0'), E(x'))
+PATCH_WEIGHTS = dict(lat_t=0.0, lat_o=-1.0, img_rec_t=0.0, vgg_rec_t=0.0, img_o=0.0, vgg_img=0.0)
 # Gradient (loss) scale per compute dtype. fp16: its range tops out at 65504, and the e4e
 # encoder's backward from the latent terms (weight 10·2/(n_latent·512) per element) reaches
 # 1e3–1e4 × λ… at λ = 2^16 whole images overflowed to inf/NaN (3 of 8 at 256², measured); at
@@ -54,6 +56,10 @@ class AttackEngine:
         self.pf = self.size // self.R
         self.ws = Workspace(synth.device)
         self.w = dict(weights)
+        # latent terms only (the patch attack): the generator and VGG terms carry weight 0, so
+        # their gradient is 0·g and the step runs the encoder forward / backward alone
+        self.lat_only = all(self.w[k] == 0 for k in ("img_rec_t", "vgg_rec_t", "img_o",
+                                                     "vgg_img"))
         R = self.R
         self.tap_numel = [64 * R * R, 64 * R * R, 128 * (R // 4) ** 2,
                           512 * ops.pool_out(R // 4, True) ** 2]
@@ -132,6 +138,8 @@ class AttackEngine:
         returns them; both are scaled by loss_scale. ``loss`` (fp32 [N], zeroed by the caller)
         receives the per-image objective at x from the same forward pass (no host sync)."""
         ws, G, V, E = self.ws, self.G, self.V, self.E
+        if self.lat_only:
+            return self._gradient_lat(x, loss)
         lat, xin = self._encode(x, "in.x")
         rec = G.forward(lat, ws)
         self.rec = rec
@@ -158,6 +166,52 @@ class AttackEngine:
             E.backward_nhwc(g_lat, ws, g_xv, accumulate=True)
             return g_xv, None
         return g_xv, E.backward(g_lat, ws)
+
+    def _gradient_lat(self, x, loss=None):
+        """gradient() when only the latent terms carry weight: E forward, the two latent MSE
+        gradients, E backward (no generator, no VGG). Same return convention."""
+        ws, E = self.ws, self.E
+        lat, xin = self._encode(x, "in.x")
+        if loss is not None:
+            self._loss_terms("lat", loss, lat)
+        g_lat = ws.get("g.lat", lat.shape, torch.float32)
+        ops.mse_grad_f32(lat, self.lat_t, g_lat, self.c_lat_t)
+        ops.mse_grad_f32(lat, self.lat_o, g_lat, self.c_lat_o, accumulate=True)
+        N = x.shape[0]
+        g_xv = ops.zero_(ws.get("g.xv0", (N, self.R, self.R, CPAD), self.dtype))
+        if xin is not None:
+            E.backward_nhwc(g_lat, ws, g_xv, accumulate=True)
+            return g_xv, None
+        return g_xv, E.backward(g_lat, ws)
+
+    def run_patch(self, img, t, patch, mask, max_count):
+        """The adversarial-patch loop (code/attack/patch/adversarial_patch.py:103-160) on the
+        engine's loss weights (PATCH_WEIGHTS for the reference's loss): adv = (1−m)·img + m·patch;
+        max_count times: g = ∇_adv L, patch −= g (the full-image gradient, step 1), adv =
+        clamp((1−m)·img + m·patch, min(img), max(img)). `patch` (img's shape, fp32) is updated in
+        place, as the reference's. Returns (adv, rec) with rec = G(E(adv')) of the last
+        iteration's input (the reference's adv_img_rec)."""
+        ws = self.ws
+        f32 = torch.float32
+        self.prepare(img, t)
+        lo, hi = float(img.min()), float(img.max())  # torch.min / torch.max of the batch (:134)
+        adv = ws.get("adv", img.shape, f32)
+        ops.patch_update(patch, None, img, mask, adv, -float("inf"), float("inf"))  # :111 no clamp
+        last = ws.get("patch.last", img.shape, f32)
+        g = ws.get("g.full", img.shape, f32)
+        for it in range(int(max_count)):
+            if it == max_count - 1:
+                last.copy_(adv)
+            g_xv, g_enc = self.gradient(adv)
+            # the reference's MSEs are batch means (nn.MSELoss over the whole batch, :116): the
+            # raw-gradient step scales with 1/N, unlike the sign steps of PGD
+            ops.grad_assemble(adv, self.x0, g_xv, g_enc, g, self.pf, ENC_POOL_RES, self.c_img_o,
+                              1.0 / (self.loss_scale * img.shape[0]), nonfinite=self.nonfinite)
+            ops.patch_update(patch, g, img, mask, adv, lo, hi)
+        if self.overflowed():
+            raise FloatingPointError("non-finite patch gradient (run fp32)")
+        lat, _ = self._encode(last if max_count > 0 else adv, "in.x")
+        return adv.clone(), self.G.forward(lat, ws).clone()
 
     def step(self, x, a, e):
         g_xv, g_enc = self.gradient(x)

@@ -290,6 +290,13 @@ int mia_random_start(float* x, const float* x0, const float* u, int64_t len, flo
 /* K11 alone, given a full fp32 gradient (bit-exact contract vs torch fp32). */
 int mia_sign_project(float* x, const float* x0, const float* g, int64_t len, float a, float e,
                      float lo, float hi, void* stream);
+/* Adversarial patch step (code/attack/patch/adversarial_patch.py:131-134): patch −= g;
+ * adv = clamp((1 − mask)·img + mask·patch, lo, hi), lo / hi = min / max of the clean images
+ * (:134). g = NULL: the composite only (patch_white_box, attack_main2.py:413-420). mask / patch
+ * have img's shape (shared = 0) or one image's shape broadcast over the batch (shared = its
+ * numel; composite only). Bit-exact vs torch fp32 ops. */
+int mia_patch_update(float* patch, const float* g, const float* img, const float* mask,
+                     float* adv, int64_t len, int64_t shared, float lo, float hi, void* stream);
 /* Adam on pixels (K12, optim.Adam at interpolation.py:767,822): fp32 state, step t ≥ 1. */
 int mia_adam_step(float* p, const float* g, float* m, float* v, int64_t len, float lr,
                   float beta1, float beta2, float eps, int t, void* stream);

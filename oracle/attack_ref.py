@@ -15,6 +15,8 @@
   minimises L, so cost = −L (the targeted form, ``:83-86``). ε, α are in [0,1] pixel units and the
   tensors live in [-1,1]: e = 2ε, a = 2α, lo/hi = −1/+1.
 """
+import contextlib
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -170,3 +172,38 @@ def cw_attack(gp, vp, ep, x0, t, size, steps, c=1e-4, lr=0.01, dtype=torch.float
                 return best
             prev = cost.item()
     return best
+
+
+PATCH_WEIGHTS = dict(lat_t=0.0, lat_o=-1.0, img_rec_t=0.0, vgg_rec_t=0.0, img_o=0.0, vgg_img=0.0)
+
+
+def patch_attack(gp, vp, ep, img, patch, mask, t, size, max_count, dtype=torch.float32,
+                 grad_ctx=None):
+    """code/attack/patch/adversarial_patch.py:103-160 (``attack``), batch semantics kept:
+    refs under no_grad (:108-112); adv = (1−m)·img + m·patch (:114, no clamp); per iteration the
+    loss 0·l_lat_t − 1·l_lat_o + 0·l_img + 0·l_lpips with batch-mean MSEs (:117-125) — the
+    objective below with PATCH_WEIGHTS is the per-image form; the batch-mean MSE of the reference
+    is the per-image mean averaged over the batch, so its gradient is this one ÷ N —
+    backward, patch −= grad (:127-131), adv = clamp((1−m)·img + m·patch, min(img), max(img))
+    (:133-134). Returns (adv, patch, rec) with rec = G(E(adv')) of the last iteration's input.
+    ``grad_ctx`` (tests): a context-manager factory entered around each gradient evaluation only
+    (e.g. encoder_ref.forced_masks of a device run), not around the target precompute."""
+    img, patch, mask, t = (z.to(dtype) for z in (img, patch, mask, t))
+    refs = Refs(gp, vp, ep, img, t, size)
+    patch = patch.clone()
+    adv = (1 - mask) * img + mask * patch
+    lo, hi = torch.min(img), torch.max(img)
+    n = img.shape[0]
+    rec = None
+    for _ in range(max_count):
+        x = adv.detach().requires_grad_(True)
+        with (grad_ctx() if grad_ctx is not None else contextlib.nullcontext()):
+            L = objective(gp, vp, ep, x, refs, size, weights=PATCH_WEIGHTS, per_image=True)
+            (g,) = torch.autograd.grad(L.sum() / n, x)
+        with torch.no_grad():
+            pf = max(1, size // 256)
+            xp = F.avg_pool2d(adv, pf) if pf > 1 else adv
+            rec = stylegan2_ref.synthesis(gp, encoder_ref.apply(ep, xp, size), size)
+            patch = patch - g
+            adv = torch.clamp((1 - mask) * img + mask * patch, lo, hi)
+    return adv.detach(), patch.detach(), rec

@@ -1,0 +1,93 @@
+"""Adversarial patch attack (code/attack/patch/adversarial_patch.py:103-160,
+attack_main2.py:413-420) on the GPU against oracle.attack_ref.patch_attack / torch fp32 ops."""
+import numpy as np
+import pytest
+import torch
+
+import gfa_amd
+from gfa_amd import networks, ops
+from gpu_helpers import e4e_masks, seeded, to64
+from oracle import attack_ref, encoder_ref, vgg_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _square(N, S, side, y0, x0):
+    """The tensors square_transform returns (un-vendored): a batch-shaped 0/1 mask and a patch of
+    U(-1,1) inside it."""
+    m = torch.zeros(N, 3, S, S)
+    m[:, :, y0:y0 + side, x0:x0 + side] = 1.0
+    p = seeded(41, (N, 3, S, S)) * m
+    return p, m
+
+
+@pytest.mark.parametrize("frac_mask", [False, True])
+def test_patch_update_bit_exact(cuda, frac_mask):
+    """mia_patch_update vs adversarial_patch.py:131-134 in torch fp32 (separately rounded ops)."""
+    N, S = 3, 40
+    img = seeded(1, (N, 3, S, S))
+    g = seeded(2, (N, 3, S, S)) * 1e-2
+    patch, mask = _square(N, S, 12, 5, 9)
+    if frac_mask:
+        mask = (seeded(3, mask.shape) + 1) / 2
+    lo, hi = float(img.min()), float(img.max())
+    want_p = patch - g
+    want = torch.clamp((1 - mask) * img + mask * want_p, lo, hi)
+    pd, adv = patch.to(cuda), torch.empty(N, 3, S, S, device=cuda)
+    ops.patch_update(pd, g.to(cuda), img.to(cuda), mask.to(cuda), adv, lo, hi)
+    torch.cuda.synchronize()
+    assert torch.equal(pd.cpu(), want_p) and torch.equal(adv.cpu(), want)
+    # patch_white_box: one shared patch / mask, per-image min / max (attack_main2.py:413-420)
+    p1, m1 = patch[:1], mask[:1]
+    want = torch.cat([torch.clamp((1 - m1) * img[i] + m1 * p1, img[i].min(), img[i].max())
+                      for i in range(N)])
+    got = gfa_amd.patch_white_box(img.to(cuda), m1.to(cuda), p1.to(cuda)).cpu()
+    assert torch.equal(got, want)
+
+
+def _params(net):
+    p = net.params
+    return p["generator"], vgg_ref.load_positional(p["vgg"]), p["encoder"]
+
+
+def test_patch_attack_vs_oracle_linear_encoder(cuda):
+    """3 iterations at 32² with the linear stand-in encoder (no activation branches): the
+    patch's total change and the final images vs the fp64 oracle."""
+    S, N, it = 32, 2, 3
+    net = networks.build_net(S, seed=3, device=cuda)
+    img = seeded(5, (N, 3, S, S)) * 0.9
+    patch, mask = _square(N, S, 10, 4, 7)
+    adv, m, p, rec = gfa_amd.patch_attack(img.to(cuda), patch.to(cuda), mask.to(cuda), net, it)
+    gp, vp, ep = to64(_params(net))
+    a_ref, p_ref, r_ref = attack_ref.patch_attack(gp, vp, ep, img.double(), patch.double(),
+                                                  mask.double(), img.double(), S, it,
+                                                  dtype=torch.float64)
+    dp, dp_ref = p.cpu().double() - patch.double(), p_ref - patch.double()
+    rel = ((dp - dp_ref).norm() / dp_ref.norm()).item()
+    print(f"patch change vs oracle: rel {rel:.2e}, |Δpatch| {dp_ref.abs().max():.3e}")
+    assert dp_ref.abs().max() > 0 and rel < 1e-4
+    assert (adv.cpu().double() - a_ref).abs().max() < 1e-5
+    assert (rec.cpu().double() - r_ref).abs().max() < 1e-4
+    assert torch.equal(m.cpu(), mask)
+    lo, hi = img.min(), img.max()
+    assert adv.min() >= lo and adv.max() <= hi
+
+
+def test_patch_attack_e4e_first_step_branch_forced(cuda):
+    """One iteration at 256² with the e4e encoder (the reference's network): the patch update vs
+    the fp64 oracle on the device run's encoder branches (encoder_ref.forced_masks)."""
+    S, N = 256, 1
+    net = networks.build_net(S, seed=0, device=cuda, encoder="e4e")
+    img = seeded(6, (N, 3, S, S)) * 0.9
+    patch, mask = _square(N, S, 64, 100, 30)
+    _, _, p, _ = gfa_amd.patch_attack(img.to(cuda), patch.to(cuda), mask.to(cuda), net, 1)
+    gp, vp, ep = to64(_params(net))
+    # the encoder's last forward is at the composite (the final rec pass re-encodes it)
+    masks = e4e_masks(net.encoder.impl)
+    _, p_ref, _ = attack_ref.patch_attack(gp, vp, ep, img.double(), patch.double(),
+                                          mask.double(), img.double(), S, 1, dtype=torch.float64,
+                                          grad_ctx=lambda: encoder_ref.forced_masks(masks))
+    dp, dp_ref = p.cpu().double() - patch.double(), p_ref - patch.double()
+    rel = ((dp - dp_ref).norm() / dp_ref.norm()).item()
+    print(f"e4e patch step vs oracle: rel {rel:.2e}")
+    assert rel < 1e-4

@@ -298,3 +298,40 @@ def test_psp_checkpoint_split(tmp_path):
     assert torch.equal(enc["body.3.shortcut_layer.0.weight"], ep["body.3.shortcut_layer.0.weight"])
     with pytest.raises(ValueError):
         networks.psp_params_from_checkpoint({"state_dict": {}, "latent_avg": ep["latent_avg"]})
+
+
+def test_records_round_trip_and_grid_formats(tmp_path):
+    """§8(f)-4 on-disk formats (gfa_amd.records): the attack_main2.py:1097-1111 torch.save dumps
+    round-trip through weights_only loads; make_grid / save_image follow torchvision's layout and
+    quantisation; the grid reload cuts the reference's tiles (interpolation.py:1386-1394)."""
+    import torch
+    from gfa_amd import records
+    g = torch.Generator().manual_seed(0)
+    adv = [torch.rand(2, 3, 8, 8, generator=g) * 2 - 1 for _ in range(3)]
+    ben = [torch.rand(2, 3, 8, 8, generator=g) * 2 - 1 for _ in range(3)]
+    loss = [torch.rand(2, generator=g) for _ in range(3)]
+    paths = records.save_records(tmp_path / "adv", tmp_path / "benign", all_adv_inputs=adv,
+                                 all_inputs=ben, all_adv_rec_loss=loss, all_rec_loss=loss)
+    assert sorted(os.path.basename(p) for p in paths.values()) == sorted(
+        ["all_adv_inputs.npz", "all_inputs.npz", "all_adv_rec_loss.npz", "all_rec_loss.npz"])
+    r = records.load_records(tmp_path / "adv")
+    assert torch.equal(r["all_adv_inputs"], torch.cat(adv)) and r["all_adv_rec_loss"].shape == (6,)
+    # make_grid geometry: 10 tiles of 8², nrow 8 → 2 rows; 2-pixel separators, zero padding
+    x = torch.rand(10, 3, 8, 8, generator=g)
+    grid = records.make_grid(x)
+    assert grid.shape == (3, 2 * 10 + 2, 8 * 10 + 2)
+    assert torch.equal(grid[:, 2:10, 12:20], x[1]) and torch.equal(grid[:, 12:20, 2:10], x[8])
+    assert grid[:, :2].abs().sum() == 0 and grid[:, 10:12].abs().sum() == 0
+    tiles = records.grid_tiles(grid, 10, 8)
+    assert all(torch.equal(t[0], x[k]) for k, t in enumerate(tiles))
+    assert torch.equal(records.make_grid(x[:1]), x[0])
+    # save_image → PNG (lossless) → reload: the quantised grid, mapped to [-1, 1]
+    p = records.save_image(x[:5], str(tmp_path / "grid.png"))
+    back = records.load_image_tensor(p)
+    q = torch.from_numpy(records.to_uint8_hwc(records.make_grid(x[:5]))).permute(2, 0, 1)
+    assert torch.equal(back, (q.float() / 255 - 0.5) / 0.5)
+    ref_t = records.reference_tiles(back, 5, 8)
+    assert torch.equal(ref_t[0], records.grid_tiles(back, 5, 8)[0])  # offset quirk: tile 0 exact
+    assert torch.equal(ref_t[1][0], back[:, 2:10, 10:18])
+    # per-image JPEG names (attack_main2.py:164-171)
+    assert os.path.basename(records.save_image_idx(x[0] * 2 - 1, str(tmp_path), 7)) == "00007.jpg"

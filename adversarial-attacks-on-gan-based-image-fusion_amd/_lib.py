@@ -38,6 +38,7 @@ class ConvArgs(ctypes.Structure):
         ("bab_demod", P), ("bab_noise", P), ("bab_noise_w", c_float), ("bab_bias", P),
         ("bab_q", P),
         ("mask_slope", P), ("act_slope", P), ("csum", P),
+        ("w_split", P),
     ]
 
 
@@ -45,7 +46,7 @@ class ConvGroup(ctypes.Structure):
     """Mirror of ``mia_conv_group``."""
     _fields_ = [("w", P), ("kh", c_int), ("kw", c_int), ("pad_y", c_int), ("pad_x", c_int),
                 ("ho", c_int), ("wo", c_int), ("ay", c_int), ("by", c_int), ("ax", c_int),
-                ("bx", c_int)]
+                ("bx", c_int), ("w_split", P)]
 
 
 class GemmSeg(ctypes.Structure):

@@ -15,6 +15,7 @@ namespace mia {
 struct ConvGroup {
   const void* w;
   int kpad, kh, kw, pad_y, pad_x, ho, wo, ay, by, ax, bx, blk0, nbm, m;
+  const void* w_split;  // fp32 pre-split weights (mia_conv_args.w_split) or nullptr
 };
 
 struct ConvK {
@@ -74,17 +75,6 @@ template <>
 __device__ __forceinline__ f32x4 mfma_chunk<__bf16>(const bf16x8& a, const bf16x8& b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-#ifdef MIA_F32_NATIVE
-template <>
-__device__ __forceinline__ f32x4 mfma_chunk<float>(const f32x4& a, const f32x4& b, f32x4 c) {
-  // fp32: lane group q holds k = 4q..4q+3 of the chunk; step s uses k = 4q+s for both operands
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
-  return c;
-}
-#else
 // fp32 operands on the bf16 matrix pipe (the default fp32 arithmetic of libmiattack).
 // Each fp32 value splits EXACTLY into three bf16 terms, a = hi + mid + lo: hi = a with the low 16
 // mantissa bits cleared (8 significant bits), r = a − hi is exact and has ≤ 16 significant bits,
@@ -137,6 +127,18 @@ __device__ __forceinline__ f32x4 mfma_split3(const Split3& A, const Split3& B, f
   c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A.hl, B.mh, c, 0, 0, 0);        // hm + lh
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(A.hm, bhh, c, 0, 0, 0);      // hh + mh
 }
+#ifdef MIA_F32_NATIVE
+// A/B build (MIA_F32_ARITH=native): the fp32 convs on the native fp32 matrix instruction
+template <>
+__device__ __forceinline__ f32x4 mfma_chunk<float>(const f32x4& a, const f32x4& b, f32x4 c) {
+  // fp32: lane group q holds k = 4q..4q+3 of the chunk; step s uses k = 4q+s for both operands
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
+  return c;
+}
+#else
 template <>
 __device__ __forceinline__ f32x4 mfma_chunk<float>(const f32x4& a, const f32x4& b, f32x4 c) {
   return mfma_split3(split3(a), split3(b), c);
@@ -500,6 +502,9 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
   }
 }
 
+// fp32 stride-1 3×3 layers with pre-split weights, operands split once (conv_halo_x6.hip)
+bool conv_halo_x6_eligible(const ConvK& k, int dtype);
+int launch_conv_halo_x6(ConvK& k, hipStream_t st);
 // halo-tiled stride-1 3×3 path (conv_halo.hip)
 bool conv_halo_eligible(const ConvK& k, int dtype);
 int launch_conv_halo(ConvK& k, int dtype, hipStream_t st);

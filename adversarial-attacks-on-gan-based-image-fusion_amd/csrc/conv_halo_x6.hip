@@ -1,0 +1,329 @@
+// fp32 stride-1 3×3 convolution on the bf16 matrix pipe with the operands split ONCE, not per tap.
+//
+// The fp32 arithmetic of libmiattack (conv_common.h, mfma_chunk<float>) writes each fp32 operand
+// as an exact three-term bf16 sum a = hi + mid + lo and keeps the six products of order ≥ 2^-16.
+// Done on the fly, the split costs ≈ 22 VALU instructions per 4 values per fragment read, and a
+// halo kernel reads every input value 9 × (taps) × 2 (column waves) times: measured 5–8 VALU
+// instructions per MFMA, VALU-issue bound at ≈ 150 TFLOP/s. Here:
+//   * the weights come pre-split from HBM (layouts.split_f32: per 4-k quad a 16-B [hi×4 | mid×4]
+//     record in the fp32 row geometry + an 8-B lo record in a second [Cout][Kpad] bf16 plane);
+//   * the input halo of each 32-channel block is split in LDS once, after its DMA lands (modulation
+//     act(x)·s of a StyledConv applied before the split), [hi|mid] in place + lo into an L buffer;
+//   * the main loop is ds_reads + 3 MFMAs per fragment pair, no split VALU: with a lane's registers
+//     laid out (lo, hi, mid), the tuples (hi, mid) and (lo, hi) are register windows and
+//       (hi,mid)·(hi,mid) = hh + mm,  (lo,hi)·(hi,mid) = lh + hm,  (hi,mid)·(lo,hi) = hl + mh.
+// Tile: 16 × 16 output pixels × 128 channels, 8 waves (4 row waves × 2 column waves, each 4 × 4
+// fragments), one block per CU: LDS = 2 raw/[hi|mid] halo buffers (2 × 41 KB) + one lo buffer
+// (20 KB) + a 2-stage pre-split weight ring (2 × 24 KB) = 150 KB. DMA roles as conv_halo.hip:
+// waves 0–3 stream the weights one K-step ahead, waves 4–7 the next channel block's halo during
+// taps 0–3. Per channel block one extra barrier: the lo buffer is rewritten after the last tap of
+// the previous block has read it.
+#include "conv_common.h"
+#include "halo_epilogue.h"
+
+namespace mia {
+
+struct HaloX6 {
+  static constexpr int PH = 16, PW = 16, FM = 4, FN = 4, WM = 4, WN = 2, NW = 8, NT = 64 * NW;
+  static constexpr int BM = PH * PW, BN = 128, BK = 32;  // 32 fp32 channels per K-step
+  static constexpr int HSIDE = PW + 2, HROWS = (PH + 2) * HSIDE;  // 324 halo pixels
+  static constexpr int HPIECES = (HROWS + 7) / 8;                 // 1-KB pieces of 8 rows
+  static constexpr int HBUF = HPIECES * 1024;
+  static constexpr int LROWB = 64, LBUF = HROWS * LROWB;          // lo: 32 × bf16 per pixel
+  static constexpr int BHM = BN * ROWB, BL = BN * LROWB, BSTAGE = BHM + BL;
+  static constexpr int BWAVES = 4, HWAVES = 4;
+  static constexpr int B_HM_INS = BN / 8 / BWAVES;   // [hi|mid] pieces (8 rows) per B-wave
+  static constexpr int B_L_INS = BN / 16 / BWAVES;   // lo pieces (16 rows of 64 B) per B-wave
+  static constexpr int H_INS = (HPIECES + HWAVES - 1) / HWAVES;
+  static constexpr int H_PER_STEP = (H_INS + 3) / 4;  // next block's halo issued over taps 0–3
+  static constexpr int EROWS = 128, ES = BN + 4;      // shared LDS epilogue staging
+  static constexpr int LDS = 2 * HBUF + LBUF + 2 * BSTAGE;
+  static_assert(WM * FM * 16 == BM && WN * FN * 16 == BN, "");
+  static_assert(B_HM_INS * 8 * BWAVES == BN && B_L_INS * 16 * BWAVES == BN, "");
+  static_assert(LDS <= 160 * 1024, "");
+};
+
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+
+// 8-byte lo slot of logical quad q in a 64-B lo row: 2·((row >> 2) & 3) XOR keeps every window of
+// 16 consecutive rows × 2 adjacent quads on 32 distinct 8-byte bank slots (ds_read_b64), and moves
+// 16-byte pairs of slots together (the weight planes are DMA'd in 16-byte lanes).
+__device__ __forceinline__ int lsw(int row) { return ((row >> 2) & 3) << 1; }
+
+// exact split of 4 fp32 values (see conv_common.h split3): [hi×4 | mid×4] and [lo×4] as bf16
+__device__ __forceinline__ void split_quad(const f32x4& a, u32x4& hm, u32x2& lo) {
+  float h[4], m[4], l[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float x = a[e];  // scalar copy (bit_cast of a vector element reads element 0)
+    h[e] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, x) & 0xffff0000u);
+    const float r = x - h[e];
+    m[e] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, r) & 0xffff0000u);
+    l[e] = r - m[e];
+  }
+  hm = u32x4{pack_hi16(h[0], h[1]), pack_hi16(h[2], h[3]), pack_hi16(m[0], m[1]),
+             pack_hi16(m[2], m[3])};
+  lo = u32x2{pack_hi16(l[0], l[1]), pack_hi16(l[2], l[3])};
+}
+
+// the six products of one 16-k quad group: (hi,mid)(hi,mid) + (lo,hi)(hi,mid) + (hi,mid)(lo,hi)
+__device__ __forceinline__ f32x4 mfma_x6(const u32x4& ahm, const u32x2& al, const u32x4& bhm,
+                                         const u32x2& bl, f32x4 c) {
+  const bf16x8 AHM = __builtin_bit_cast(bf16x8, ahm), BHM = __builtin_bit_cast(bf16x8, bhm);
+  const bf16x8 ALH = __builtin_bit_cast(bf16x8, u32x4{al[0], al[1], ahm[0], ahm[1]});
+  const bf16x8 BLH = __builtin_bit_cast(bf16x8, u32x4{bl[0], bl[1], bhm[0], bhm[1]});
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AHM, BLH, c, 0, 0, 0);  // hl + mh
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ALH, BHM, c, 0, 0, 0);  // lh + hm
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(AHM, BHM, c, 0, 0, 0);  // hh + mm
+}
+
+template <bool PRO, int EPI>
+__global__ __launch_bounds__(HaloX6::NT, 2) void conv_halo_x6_kernel(const ConvK k) {
+  typedef HaloX6 TL;
+  constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, NT = TL::NT, BN = TL::BN, BK = TL::BK;
+  constexpr int HSIDE = TL::HSIDE, HROWS = TL::HROWS, HPIECES = TL::HPIECES, HBUF = TL::HBUF;
+  constexpr int H_INS = TL::H_INS, HPS = TL::H_PER_STEP, HWAVES = TL::HWAVES;
+  constexpr int B_HM_INS = TL::B_HM_INS, B_L_INS = TL::B_L_INS, BSTAGE = TL::BSTAGE;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const hbuf = smem;                  // 2 halo buffers: raw fp32, then [hi|mid] in place
+  char* const lbuf = smem + 2 * HBUF;       // lo of the current channel block
+  char* const bring = lbuf + TL::LBUF;      // 2 stages of pre-split weights: [hi|mid] rows, lo rows
+
+  const mia_conv_args& p = k.a;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const ConvGroup G = k.g[0];
+  const int H = p.H, W = p.W, Cin = p.Cin, Cout = p.Cout, Kpad = G.kpad;
+  const int bl = xcd_remap(blockIdx.x, k.nblk);
+  const int mt = bl / k.nbn, n0 = (bl % k.nbn) * BN;
+  const int ptx = W / TL::PW, pty = H / TL::PH;
+  const int x0 = (mt % ptx) * TL::PW;
+  const int y0 = ((mt / ptx) % pty) * TL::PH;
+  const int n = mt / (ptx * pty);
+
+  const float* __restrict__ X = (const float*)p.x;
+  const unsigned* __restrict__ Whm = (const unsigned*)G.w_split;                // [Cout][Kpad]
+  const __bf16* __restrict__ Wl = (const __bf16*)(Whm + (size_t)Cout * Kpad);   // [Cout][Kpad]
+  const char* zero = (const char*)g_zero16;
+  const bool bwave = wid < TL::BWAVES;
+  const int hw = wid - TL::BWAVES;
+  const int my_pieces = bwave ? 0 : (HPIECES - hw + HWAVES - 1) / HWAVES;
+
+  // per-lane DMA sources (byte pointers; nullptr → the zero page)
+  constexpr int NSRC = H_INS > B_HM_INS + B_L_INS ? H_INS : B_HM_INS + B_L_INS;
+  const char* src[NSRC];
+#pragma unroll
+  for (int j = 0; j < NSRC; ++j) {
+    src[j] = nullptr;
+    if (bwave) {
+      if (j < B_HM_INS) {
+        const int row = (wid * B_HM_INS + j) * 8 + (lane >> 3);
+        if (n0 + row < Cout)
+          src[j] = (const char*)(Whm + (size_t)(n0 + row) * Kpad + ((lane & 7) ^ fsw(row)) * 4);
+      } else if (j < B_HM_INS + B_L_INS) {
+        const int row = (wid * B_L_INS + j - B_HM_INS) * 16 + (lane >> 2);
+        if (n0 + row < Cout)
+          src[j] = (const char*)(Wl + (size_t)(n0 + row) * Kpad +
+                                 ((lane & 3) ^ (lsw(row) >> 1)) * 8);
+      }
+    } else if (j < H_INS) {
+      const int hr = (hw + HWAVES * j) * 8 + (lane >> 3);
+      const int hy = hr / HSIDE, hx = hr - (hr / HSIDE) * HSIDE;
+      const int y = y0 + hy - 1, x = x0 + hx - 1;
+      if (hr < HROWS && y >= 0 && y < H && x >= 0 && x < W)
+        src[j] = (const char*)(X + ((size_t)(n * H + y) * W + x) * Cin + ((lane & 7) ^ fsw(hr)) * 4);
+    }
+  }
+  const int ncb = Cin / BK, nk = 9 * ncb;
+
+  auto issue_b = [&](int s, int st) {  // B-wave: its weight pieces of K-step s = (cb, tap)
+    const int cb = s / 9, t = s - (s / 9) * 9;
+    const int koff = t * Cin + cb * BK;  // k offset (elements) of the step in a weight row
+    char* dst = bring + st * BSTAGE;
+#pragma unroll
+    for (int j = 0; j < B_HM_INS; ++j) {
+      const char* a = src[j] ? src[j] + (size_t)koff * 4 : zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)a, (lptr_t)(dst + (wid * B_HM_INS + j) * 1024), 16,
+                                       0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < B_L_INS; ++j) {
+      const char* a = src[B_HM_INS + j] ? src[B_HM_INS + j] + (size_t)koff * 2 : zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)a,
+                                       (lptr_t)(dst + TL::BHM + (wid * B_L_INS + j) * 1024), 16, 0,
+                                       0);
+    }
+  };
+  auto issue_h = [&](int cb, int j, int buf) {  // H-wave: its halo piece j of channel block cb
+    const char* a = src[j] ? src[j] + (size_t)cb * BK * 4 : zero;
+    __builtin_amdgcn_global_load_lds((gptr_t)a,
+                                     (lptr_t)(hbuf + buf * HBUF + (hw + HWAVES * j) * 1024), 16,
+                                     0, 0);
+  };
+  // split the landed raw halo of channel block cb (buffer buf) in place + lo into lbuf
+  const bool lrelu_in = p.act_in == MIA_ACT_LRELU_S2;
+  auto convert = [&](int cb, int buf) {
+    char* hb = hbuf + buf * HBUF;
+    for (int c = tid; c < HROWS * 8; c += NT) {
+      const int hr = c >> 3, pc = c & 7, lc = pc ^ fsw(hr);
+      f32x4 v = *(const f32x4*)(hb + hr * ROWB + pc * 16);
+      if constexpr (PRO) {  // x̃ = act(x)·s, rounded as the on-the-fly path (conv_common.h)
+        const float mul = lrelu_in ? SQRT2 : 1.f;
+        f32x4 s4 = {1.f, 1.f, 1.f, 1.f};
+        if (p.in_scale) s4 = *(const f32x4*)(p.in_scale + (size_t)n * Cin + cb * BK + lc * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float f = v[e];
+          if (lrelu_in) f = fmaxf(f, 0.2f * f);
+          v[e] = f * (s4[e] * mul);
+        }
+      }
+      u32x4 hm;
+      u32x2 lo;
+      split_quad(v, hm, lo);
+      *(u32x4*)(hb + hr * ROWB + pc * 16) = hm;
+      *(u32x2*)(lbuf + hr * TL::LROWB + ((lc ^ lsw(hr)) << 3)) = lo;
+    }
+  };
+
+  // ---- prologue: weights of step 0, halo of channel block 0, its split -----------------------
+  if (bwave) {
+    issue_b(0, 0);
+  } else {
+#pragma unroll
+    for (int j = 0; j < H_INS; ++j)
+      if (j < my_pieces) issue_h(0, j, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  convert(0, 0);
+  __syncthreads();
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int frow = lane & 15, fq = lane >> 4;
+  int st = 0, cb = 0, t = 0;
+  for (int s = 0; s < nk; ++s) {
+    const char* ha = hbuf + (cb & 1) * HBUF;
+    const char* sb = bring + st * BSTAGE;
+    const int dy = t >= 6 ? 2 : (t >= 3 ? 1 : 0), dx = t - 3 * dy;
+    if (bwave && s + 1 < nk) issue_b(s + 1, st ^ 1);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int ch = h * 4 + fq;  // this lane's logical 16-B quad of the K-step (k = 4·ch …)
+      u32x4 ahm[FM], bhm[FN];
+      u32x2 al[FM], blo[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int hr = (wm * FM + i + dy) * HSIDE + frow + dx;
+        ahm[i] = *(const u32x4*)(ha + hr * ROWB + ((ch ^ fsw(hr)) << 4));
+        al[i] = *(const u32x2*)(lbuf + hr * TL::LROWB + ((ch ^ lsw(hr)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * FN * 16 + 16 * j + frow;
+        bhm[j] = *(const u32x4*)(sb + row * ROWB + ((ch ^ fsw(row)) << 4));
+        blo[j] = *(const u32x2*)(sb + TL::BHM + row * TL::LROWB + ((ch ^ lsw(row)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = EPI != -2 ? mfma_x6(bhm[j], blo[j], ahm[i], al[i], acc[i][j])  // D[ch][px]
+                                : mfma_x6(ahm[i], al[i], bhm[j], blo[j], acc[i][j]);  // D[px][ch]
+      if (h == 0 && !bwave && cb + 1 < ncb) {
+        // H-waves: the next block's halo between the two MFMA halves, HPS pieces per tap 0–3
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int tt = 0; tt < (H_INS + HPS - 1) / HPS; ++tt) {
+          if (t == tt) {
+#pragma unroll
+            for (int q = 0; q < HPS; ++q) {
+              const int j = tt * HPS + q;
+              if (j < H_INS && j < my_pieces) issue_h(cb + 1, j, (cb + 1) & 1);
+            }
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    // B-wave: step s+1's weights must have landed. H-wave: the next block's halo by the last tap.
+    if (bwave || t == 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS reads of the step are done
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (t == 8 && cb + 1 < ncb) {  // every wave is past the last read of lbuf: split block cb+1
+      convert(cb + 1, (cb + 1) & 1);
+      __syncthreads();
+    }
+    st ^= 1;
+    if (++t == 9) { t = 0; ++cb; }
+  }
+  if constexpr (EPI >= 0) {
+    halo_epilogue_f<float, TL, EPI>(k, acc, n, y0, x0, n0, wm, wn, lane, -1, -1, nullptr,
+                                    k.prered ? (float*)smem : nullptr, TL::WM, TL::BN);
+  } else if constexpr (EPI == -1) {
+    halo_epilogue<float, TL>(k, acc, n, y0, x0, n0, wm, wn, lane);
+  } else {
+    __syncthreads();
+    const int img_row = n * H + y0;
+    conv_epilogue<float, TL>(k, G, acc, smem, n0, true, n, [=](int r) {
+      return (img_row + (r >> 4)) * W + x0 + (r & 15);
+    });
+  }
+}
+
+template <bool PRO, int EPI>
+static int launch_x6_(ConvK& k, hipStream_t st) {
+  typedef HaloX6 TL;
+  k.nbn = (k.a.Cout + TL::BN - 1) / TL::BN;
+  k.nblk = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW) * k.nbn;
+  size_t lds = TL::LDS;
+  lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
+  lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
+  auto fn = conv_halo_x6_kernel<PRO, EPI>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
+      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+    attr_set = true;
+  }
+  k.prered = prered_enabled() && EPI >= 0 && (EPI & epi::CSUM);
+  hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), lds, st, k);
+  return check_launch("conv_halo_x6");
+}
+
+// Eligible: fp32 with pre-split weights (mia_conv_args.w_split / mia_conv_group.w_split), one
+// group, stride 1, 3×3 pad 1, identity placement, 16-divisible maps, Cin % 32 == 0, Cout > 64.
+bool conv_halo_x6_eligible(const ConvK& k, int dtype) {
+#ifdef MIA_F32_NATIVE
+  (void)k;
+  (void)dtype;
+  return false;  // the native-fp32 A/B build keeps every fp32 conv on v_mfma_f32_16x16x4_f32
+#endif
+  const char* e = getenv("MIA_CONV_X6");  // A/B switch: 0 = the on-the-fly split kernels
+  if (e && atoi(e) == 0) return false;
+  const mia_conv_args& a = k.a;
+  const ConvGroup& G = k.g[0];
+  return dtype == MIA_F32 && G.w_split != nullptr && k.ng == 1 && k.stride == 1 && G.kh == 3 &&
+         G.kw == 3 && G.pad_y == 1 && G.pad_x == 1 && G.ho == a.H && G.wo == a.W && G.ay == 1 &&
+         G.ax == 1 && G.by == 0 && G.bx == 0 && !a.shuffle_out && a.H % 16 == 0 &&
+         a.W % 16 == 0 && a.Cin % 32 == 0 && a.Cout > 64 && k.HT == a.H && k.WT == a.W;
+}
+
+int launch_conv_halo_x6(ConvK& k, hipStream_t st) {
+  const bool pro = k.a.in_scale != nullptr || k.a.act_in != MIA_ACT_NONE;
+  const char* e = getenv("MIA_HALO_EPI");  // A/B: 0 = LDS-staged shared epilogue
+  if (e && atoi(e) == 0) return pro ? launch_x6_<true, -2>(k, st) : launch_x6_<false, -2>(k, st);
+  return pro ? launch_x6_<true, -1>(k, st) : launch_x6_<false, -1>(k, st);
+}
+
+}  // namespace mia

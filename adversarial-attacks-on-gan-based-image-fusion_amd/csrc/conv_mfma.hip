@@ -413,6 +413,7 @@ static int run_conv(ConvK& k, int dtype, hipStream_t st) {
   if (conv_thin_eligible(k, dtype)) return launch_conv_thin(k, dtype, st);
   if (conv_thin32_eligible(k, dtype)) return launch_conv_thin32(k, dtype, st);
   if (conv_wres_eligible(k, dtype)) return launch_conv_wres(k, dtype, st);
+  if (conv_halo_x6_eligible(k, dtype)) return launch_conv_halo_x6(k, st);
   if (conv_halo_eligible(k, dtype)) return launch_conv_halo(k, dtype, st);
   MIA_DISPATCH_DTYPE(dtype, T, return launch_conv<T>(k, st));
   return MIA_OK;
@@ -433,6 +434,7 @@ extern "C" int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream) {
   k.ng = 1;
   ConvGroup& G = k.g[0];
   G.w = a.w;
+  G.w_split = a.w_split;
   G.kpad = a.Kpad;
   G.kh = G.kw = 3;
   G.pad_y = G.pad_x = 1;
@@ -471,6 +473,7 @@ extern "C" int mia_conv2d(const mia_conv_args* args, int stride, const mia_conv_
     const mia_conv_group& s = groups[g];
     ConvGroup& G = k.g[g];
     G.w = s.w;
+    G.w_split = s.w_split;
     G.kh = s.kh;
     G.kw = s.kw;
     G.kpad = kpad_for(s.kh * s.kw * a.Cin, dtype);

@@ -14,6 +14,8 @@ window (tap = 3·ty + tx, offsets ty−1, tx−1). These helpers produce its wei
                         Demodulation commutes with the (per-channel, linear) blur, so the phase
                         kernels carry the original weights' demod (ModulatedConv2d upsample branch).
 """
+import weakref
+
 import torch
 
 BLUR_F = (0.25, 0.75, 0.75, 0.25)
@@ -172,3 +174,64 @@ def s2_dgrad_halo_matrix(w, dtype):
     gradient is the transposed conv mirrored: offsets +j, output phase 1 − p, kernel index
     2 − (p + 2j)). (Cout/BK, 5, 2, Cin, BK)."""
     return upconv_halo_matrix(w.double().transpose(0, 1).flip(2, 3), dtype)
+
+
+def _hi16(t):
+    """Top 16 bits of fp32 words as int64 in [0, 65535]."""
+    return (t.view(torch.int32).to(torch.int64) >> 16) & 0xFFFF
+
+
+def _pack_words(lo16, hi16):
+    """Two 16-bit fields → int32 words (bit patterns)."""
+    v = lo16 | (hi16 << 16)
+    return (v - ((v >> 31) << 32)).to(torch.int32)
+
+
+def split_f32(w):
+    """Pre-split fp32 weights for the split-once halo kernel (mia_conv_args.w_split,
+    csrc/conv_halo_x6.hip): w [Cout][Kpad] fp32 (Kpad % 4 == 0) → int32 words
+    [Cout][Kpad] of per-4-k-quad records [hi0 hi1 hi2 hi3 | mid0 mid1 mid2 mid3] (bf16), then
+    [Cout][Kpad/2] words of [lo0 lo1 lo2 lo3] (bf16) — w = hi + mid + lo exactly, hi = w with the
+    low 16 bits cleared, mid = (w − hi) likewise, lo = w − hi − mid (conv_common.h split3)."""
+    if w.dtype != torch.float32 or w.dim() != 2 or w.shape[1] % 4:
+        raise ValueError("split_f32: [Cout][Kpad] fp32 with Kpad % 4 == 0")
+    dev = w.device
+    a = w.detach().to("cpu").contiguous()
+    mask = torch.tensor(-65536, dtype=torch.int32)  # 0xffff0000
+    hi = (a.view(torch.int32) & mask).view(torch.float32)
+    r = a - hi
+    mid = (r.view(torch.int32) & mask).view(torch.float32)
+    lo = r - mid
+    cout, kpad = a.shape
+    H, M, L = (_hi16(t).reshape(cout, kpad // 4, 4) for t in (hi, mid, lo))
+    hm = torch.stack([_pack_words(H[..., 0], H[..., 1]), _pack_words(H[..., 2], H[..., 3]),
+                      _pack_words(M[..., 0], M[..., 1]), _pack_words(M[..., 2], M[..., 3])], -1)
+    lw = torch.stack([_pack_words(L[..., 0], L[..., 1]), _pack_words(L[..., 2], L[..., 3])], -1)
+    return torch.cat([hm.reshape(-1), lw.reshape(-1)]).to(dev)
+
+
+# split copies of device fp32 weight matrices, made on first use: data_ptr → (weakref to the
+# weight tensor, its version counter, split tensor). An entry is used only while the weakref still
+# names the same live tensor and its in-place version is unchanged.
+_SPLITS = {}
+
+
+def split_for(w):
+    """The split_f32 copy of a device fp32 weight matrix (cached), or None when the library's fp32
+    arithmetic is the native A/B build or w is not fp32."""
+    from . import _lib
+    if w.dtype != torch.float32 or not w.is_cuda or _lib.F32_ARITH != "bf16x6":
+        return None
+    key = w.data_ptr()
+    e = _SPLITS.get(key)
+    if e is not None and e[0]() is w and e[1] == w._version:
+        return e[2]
+    sp = split_f32(w)
+
+    def _drop(_ref, key=key):
+        cur = _SPLITS.get(key)
+        if cur is not None and cur[0] is _ref:
+            del _SPLITS[key]
+
+    _SPLITS[key] = (weakref.ref(w, _drop), w._version, sp)
+    return sp

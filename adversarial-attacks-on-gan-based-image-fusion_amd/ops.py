@@ -119,6 +119,8 @@ def conv3x3(x, w, y, *, cout, act_in=ACT_NONE, in_scale=None, out_scale=None, bi
     a.aux_x, a.act_aux, a.sdot = ptr(aux_x), act_aux, ptr(sdot)
     a.tap_a, a.tap_t, a.tap_coef, a.mask_a = ptr(tap_a), ptr(tap_t), float(tap_coef), ptr(mask_a)
     a.accumulate = int(bool(accumulate))
+    ws = layouts.split_for(w) if T == torch.float32 and not shuffle_out else None
+    a.w_split = ptr(ws)
     if bab is not None:
         a.bab_demod, a.bab_q = ptr(bab["demod"]), ptr(bab["q"])
         a.bab_noise, a.bab_noise_w = ptr(bab.get("noise")), float(bab.get("noise_w", 0.0))
@@ -699,8 +701,12 @@ def conv2d(x, groups, y, out_hw, *, cout, stride=1, bias=None, act_out=ACT_NONE,
         ho, wo = g["ho"], g["wo"]
         if ho <= 0 or wo <= 0 or ay * (ho - 1) + by >= oh or ax * (wo - 1) + bx >= ow:
             raise ValueError(f"group {i}: placement outside the output grid")
-        garr[i] = _lib.ConvGroup(ptr(g["w"]).value, kh, kw, py, px, ho, wo, ay, by, ax, bx)
+        wsp = (layouts.split_for(g["w"]) if T == torch.float32 and len(groups) == 1 and
+               stride == 1 and kh == 3 and kw == 3 else None)
+        garr[i] = _lib.ConvGroup(ptr(g["w"]).value, kh, kw, py, px, ho, wo, ay, by, ax, bx,
+                                 ptr(wsp).value if wsp is not None else None)
         keep.append(g["w"])
+        keep.append(wsp)
         mac += N * ho * wo * kh * kw * Cin * cout
     a = ConvArgs()
     a.x, a.y = ptr(x), ptr(y)

@@ -96,6 +96,11 @@ typedef struct mia_conv_args {
   const float* mask_slope; /* [Cout] or NULL (→ 0: ReLU mask) */
   const float* act_slope;  /* [Cout], required by MIA_ACT_PRELU */
   float* csum;             /* [N][Cout] fp32, accumulated with atomics, or NULL */
+  /* fp32 only, optional: the same weights pre-split for the bf16 matrix pipe (a = hi + mid + lo,
+   * exact; layouts.split_f32): [Cout][Kpad] words, per 4-k quad [hi×4 | mid×4] bf16 (16 B), then
+   * [Cout][Kpad] bf16 lo. Lets the stride-1 3×3 layers take the split-once halo kernel
+   * (conv_halo_x6.hip); NULL → the kernels split w on the fly. */
+  const void* w_split;
 } mia_conv_args;
 
 int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream);
@@ -125,6 +130,7 @@ int mia_conv_s2_dgrad_halo(const void* g, const void* w_halo, void* gx, int N, i
 typedef struct mia_conv_group {
   const void* w;
   int kh, kw, pad_y, pad_x, ho, wo, ay, by, ax, bx;
+  const void* w_split;  /* as mia_conv_args.w_split, for this group's w (or NULL) */
 } mia_conv_group;
 int mia_conv2d_kpad(int taps, int cin, int dtype);
 int mia_conv2d(const mia_conv_args* args, int stride, const mia_conv_group* groups, int ngroups,

@@ -884,7 +884,7 @@ def test_memset_fill_kernel(cuda, off, nbytes, value):
     assert torch.equal(got, want)
 
 
-@pytest.mark.parametrize("path", ["halo", "generic", "upconv"])
+@pytest.mark.parametrize("path", ["halo", "halo_otf", "generic", "upconv"])
 def test_fp32_arithmetic_is_fp32_accurate(cuda, monkeypatch, path):
     """The fp32 convs run as exact three-way bf16 splits with six products (conv_common.h,
     mfma_chunk<float>; the dropped mid·lo, lo·mid, lo·lo terms are < 2^-23·|ab|). At the largest
@@ -892,8 +892,10 @@ def test_fp32_arithmetic_is_fp32_accurate(cuda, monkeypatch, path):
     the native v_mfma_f32_16x16x4_f32 build (MIA_F32_ARITH=native, measured on these seeded
     operands: max-abs 1.12e-5 / 1.22e-5 / 5.2e-6, norm-relative 1.18e-6 / 1.19e-6 / 6.6e-7 for
     halo / generic / upconv; the split build: 1.18e-5 / 9.1e-6 / 5.6e-6 and 1.05e-6 / 1.05e-6 /
-    5.8e-7). Bound: 2× the native figures."""
+    5.8e-7). Bound: 2× the native figures. "halo" = the split-once kernel (conv_halo_x6.hip,
+    pre-split weights), "halo_otf" = the on-the-fly split halo kernel (MIA_CONV_X6=0)."""
     monkeypatch.setenv("MIA_CONV_HALO", "0" if path == "generic" else "1")
+    monkeypatch.setenv("MIA_CONV_X6", "0" if path == "halo_otf" else "1")
     g = torch.Generator().manual_seed(77)
     N, H, Cin, Cout = 2, 16, 512, 256
     x = torch.randn(N, Cin, H, H, generator=g)
@@ -914,6 +916,7 @@ def test_fp32_arithmetic_is_fp32_accurate(cuda, monkeypatch, path):
     torch.cuda.synchronize()
     err = (got - ref).abs()
     native = {"halo": (1.12e-5, 1.18e-6), "generic": (1.22e-5, 1.19e-6), "upconv": (5.2e-6, 6.6e-7)}
+    native["halo_otf"] = native["halo"]
     mx, nrm = err.max().item(), (err.norm() / ref.norm()).item()
     print(f"{path}: max-abs err {mx:.3e}, norm-relative {nrm:.3e} (native fp32 MFMA "
           f"{native[path][0]:.2e}, {native[path][1]:.2e})")

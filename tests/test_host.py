@@ -335,3 +335,33 @@ def test_records_round_trip_and_grid_formats(tmp_path):
     assert torch.equal(ref_t[1][0], back[:, 2:10, 10:18])
     # per-image JPEG names (attack_main2.py:164-171)
     assert os.path.basename(records.save_image_idx(x[0] * 2 - 1, str(tmp_path), 7)) == "00007.jpg"
+
+
+def test_split_f32_is_exact():
+    """layouts.split_f32 (the pre-split weights of the split-once fp32 halo kernel): unpacking the
+    [hi×4 | mid×4] quads and the lo plane gives hi + mid + lo == w exactly, each term a bf16
+    value, for normal, tiny, negative and zero weights."""
+    import torch
+    from gfa_amd import layouts
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(8, 64, generator=g) * torch.logspace(-30, 3, 64)[None, :]
+    w[0, :4] = torch.tensor([0.0, -0.0, 1.0, -3.1415927])
+    sp = layouts.split_f32(w)
+    cout, kpad = w.shape
+    words = sp.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+    hm = words[:cout * kpad].reshape(cout, kpad // 4, 4)
+    lw = words[cout * kpad:].reshape(cout, kpad // 4, 2)
+
+    def halves(x):  # int64 words → (low16, high16) as fp32 values of bf16 fields
+        lo16, hi16 = x & 0xFFFF, x >> 16
+        f = lambda h: (h << 16).to(torch.int32).view(torch.float32).double()  # noqa: E731
+        return f(lo16), f(hi16)
+
+    parts = []
+    for src in (hm[..., 0:2], hm[..., 2:4], lw):
+        a0, a1 = halves(src[..., 0])
+        a2, a3 = halves(src[..., 1])
+        parts.append(torch.stack([a0, a1, a2, a3], -1).reshape(cout, kpad))
+    h, m, l = parts
+    assert torch.equal(h + m + l, w.double())
+    assert (h.abs() >= m.abs()).all() and (m.abs() >= l.abs()).all()

@@ -163,11 +163,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16"])
+    ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16", "fp32"])
     ap.add_argument("--only", default="")
     ap.add_argument("vars", nargs="*")
     a = ap.parse_args()
-    dtype = torch.float16 if a.dtype == "fp16" else torch.bfloat16
+    dtype = {"fp16": torch.float16, "bf16": torch.bfloat16, "fp32": torch.float32}[a.dtype]
     dev = torch.device("cuda:0")
     keys = [v.split("=")[0] for v in a.vars]
     vals = [v.split("=")[1].split(",") for v in a.vars]

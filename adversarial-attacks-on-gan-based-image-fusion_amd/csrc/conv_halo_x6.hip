@@ -43,41 +43,6 @@ struct HaloX6 {
   static_assert(LDS <= 160 * 1024, "");
 };
 
-typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
-typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
-
-// 8-byte lo slot of logical quad q in a 64-B lo row: 2·((row >> 2) & 3) XOR keeps every window of
-// 16 consecutive rows × 2 adjacent quads on 32 distinct 8-byte bank slots (ds_read_b64), and moves
-// 16-byte pairs of slots together (the weight planes are DMA'd in 16-byte lanes).
-__device__ __forceinline__ int lsw(int row) { return ((row >> 2) & 3) << 1; }
-
-// exact split of 4 fp32 values (see conv_common.h split3): [hi×4 | mid×4] and [lo×4] as bf16
-__device__ __forceinline__ void split_quad(const f32x4& a, u32x4& hm, u32x2& lo) {
-  float h[4], m[4], l[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float x = a[e];  // scalar copy (bit_cast of a vector element reads element 0)
-    h[e] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, x) & 0xffff0000u);
-    const float r = x - h[e];
-    m[e] = __builtin_bit_cast(float, __builtin_bit_cast(unsigned, r) & 0xffff0000u);
-    l[e] = r - m[e];
-  }
-  hm = u32x4{pack_hi16(h[0], h[1]), pack_hi16(h[2], h[3]), pack_hi16(m[0], m[1]),
-             pack_hi16(m[2], m[3])};
-  lo = u32x2{pack_hi16(l[0], l[1]), pack_hi16(l[2], l[3])};
-}
-
-// the six products of one 16-k quad group: (hi,mid)(hi,mid) + (lo,hi)(hi,mid) + (hi,mid)(lo,hi)
-__device__ __forceinline__ f32x4 mfma_x6(const u32x4& ahm, const u32x2& al, const u32x4& bhm,
-                                         const u32x2& bl, f32x4 c) {
-  const bf16x8 AHM = __builtin_bit_cast(bf16x8, ahm), BHM = __builtin_bit_cast(bf16x8, bhm);
-  const bf16x8 ALH = __builtin_bit_cast(bf16x8, u32x4{al[0], al[1], ahm[0], ahm[1]});
-  const bf16x8 BLH = __builtin_bit_cast(bf16x8, u32x4{bl[0], bl[1], bhm[0], bhm[1]});
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AHM, BLH, c, 0, 0, 0);  // hl + mh
-  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ALH, BHM, c, 0, 0, 0);  // lh + hm
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(AHM, BHM, c, 0, 0, 0);  // hh + mm
-}
-
 template <bool PRO, int EPI>
 __global__ __launch_bounds__(HaloX6::NT, 2) void conv_halo_x6_kernel(const ConvK k) {
   typedef HaloX6 TL;

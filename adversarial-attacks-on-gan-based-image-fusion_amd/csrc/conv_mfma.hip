@@ -49,7 +49,20 @@ __device__ __forceinline__ void wait_dma_steps(int steps) {
 // EPI: −2 = LDS-staged shared epilogue (conv_epilogue); ≥ 0 = the register epilogue specialised
 // for feature mask EPI (halo_epilogue_f; MFMAs computed transposed, D[channel][pixel]), for
 // single-image tiles of whole 16-pixel rows with identity placement (see reg_epi_ok).
-template <typename T, typename TL, bool PRO, bool SMALLC, int EPI = -2>
+// X6B (fp32 only): the weights come pre-split from HBM (mia_conv_group.w_split): a B stage holds
+// [hi|mid] rows (the fp32 row geometry) + 64-B lo rows, B fragments are read pre-split, and only
+// the A fragments are split on the fly (conv_common.h split_quad) — half the split VALU of the
+// mfma_chunk<float> path, whose VALU bound this lowers.
+template <typename T, int BM, int BN, bool X6B>
+struct StageBytes {
+  static constexpr int v = (BM + BN) * ROWB;
+};
+template <int BM, int BN>
+struct StageBytes<float, BM, BN, true> {
+  static constexpr int v = BM * ROWB + BN * (ROWB + 64);
+};
+
+template <typename T, typename TL, bool PRO, bool SMALLC, int EPI = -2, bool X6B = false>
 __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 128 ? 4 : 2) : 1) void conv_kernel(
     const ConvK k) {
   typedef typename Vec<T>::type VT;
@@ -57,7 +70,10 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
   constexpr int BK = ROWB / (int)sizeof(T);
   constexpr int WN = TL::WN, FM = TL::FM, FN = TL::FN, NT = TL::NT;
   constexpr int BM = TL::BM, BN = TL::BN, A_INS = TL::A_INS, B_INS = TL::B_INS;
-  constexpr int STAGE = TL::STAGE, STAGES = TL::STAGES;
+  constexpr bool X6 = X6B && std::is_same<T, float>::value;
+  constexpr int STAGE = StageBytes<T, BM, BN, X6>::v, STAGES = TL::STAGES;
+  constexpr int B_L_INS = X6 ? BN / (16 * TL::NW) : 0;  // lo-row pieces (16 rows) per wave
+  static_assert(!X6 || B_L_INS * 16 * TL::NW == BN, "");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -78,7 +94,8 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
   const int ntap = G.kh * G.kw;
 
   const T* __restrict__ X = (const T*)p.x;
-  const T* __restrict__ Wt = (const T*)G.w;
+  // X6: the [hi|mid] words of the pre-split weights have the fp32 row geometry (4 B per k)
+  const T* __restrict__ Wt = X6 ? (const T*)G.w_split : (const T*)G.w;
   const T* zero = (const T*)g_zero16;
 
   // ---- per-lane DMA source state -----------------------------------------------------------
@@ -112,6 +129,18 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
     const int row = (wid * B_INS + j) * 8 + (lane >> 3);
     const int c = n0 + row;
     b_ptr[j] = c < p.Cout ? Wt + (size_t)c * G.kpad + ((lane & 7) ^ fsw(row)) * VEC : zero;
+  }
+  const char* bl_ptr[B_L_INS > 0 ? B_L_INS : 1];
+  if constexpr (X6) {
+    const __bf16* Wl = (const __bf16*)((const unsigned*)G.w_split + (size_t)p.Cout * G.kpad);
+#pragma unroll
+    for (int j = 0; j < B_L_INS; ++j) {
+      const int row = (wid * B_L_INS + j) * 16 + (lane >> 2);
+      const int c = n0 + row;
+      bl_ptr[j] = c < p.Cout ? (const char*)(Wl + (size_t)c * G.kpad +
+                                             ((lane & 3) ^ (lsw(row) >> 1)) * 8)
+                             : nullptr;
+    }
   }
 
   // K-step state for the DMA issue (uniform across the block)
@@ -150,6 +179,14 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
       __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(sb + (wid * B_INS + j) * 1024), 16,
                                        0, 0);
     }
+    if constexpr (X6) {
+#pragma unroll
+      for (int j = 0; j < B_L_INS; ++j) {
+        const char* src = bl_ptr[j] ? bl_ptr[j] + (size_t)kb * BK * 2 : (const char*)zero;
+        __builtin_amdgcn_global_load_lds(
+            (gptr_t)src, (lptr_t)(sb + BN * ROWB + (wid * B_L_INS + j) * 1024), 16, 0, 0);
+      }
+    }
   };
 
   // ---- modulation table (PRO): s[n][ci] (·√2 for lrelu inputs) for the images of this tile ----
@@ -185,6 +222,7 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
   if constexpr (STAGES == 2) {
     __syncthreads();
   } else {
+    static_assert(!X6, "X6B: 2-stage tiles only");
     // retire step 0 (the later prologue steps may stay in flight), then make every wave's DMA
     // visible
     wait_dma_steps<A_INS + B_INS>(min(nk, STAGES - 1) - 1);
@@ -206,6 +244,25 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
       for (int i = 0; i < FM; ++i) {
         const int row = wm * FM * 16 + 16 * i + frow;
         af[i] = *(const VT*)(sa + row * ROWB + ((ch ^ fsw(row)) << 4));
+      }
+      if constexpr (X6) {
+        u32x4 ahm[FM], bhm[FN];
+        u32x2 alo[FM], blo[FN];
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int row = wn * FN * 16 + 16 * j + frow;
+          bhm[j] = *(const u32x4*)(sb + row * ROWB + ((ch ^ fsw(row)) << 4));
+          blo[j] = *(const u32x2*)(sb + BN * ROWB + row * 64 + ((ch ^ lsw(row)) << 3));
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) split_quad(af[i], ahm[i], alo[i]);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = EPI == -2 ? mfma_x6(ahm[i], alo[i], bhm[j], blo[j], acc[i][j])
+                                  : mfma_x6(bhm[j], blo[j], ahm[i], alo[i], acc[i][j]);
+        continue;
       }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -258,7 +315,7 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
   }
 }
 
-template <typename T, typename TL, bool PRO, bool SMALLC, int EPI = -2>
+template <typename T, typename TL, bool PRO, bool SMALLC, int EPI = -2, bool X6B = false>
 static int launch_tile(ConvK& k, hipStream_t st) {
   k.nbn = (k.a.Cout + TL::BN - 1) / TL::BN;
   int blk = 0;
@@ -268,12 +325,12 @@ static int launch_tile(ConvK& k, hipStream_t st) {
     blk += k.g[g].nbm * k.nbn;
   }
   k.nblk = blk;
-  size_t lds = (size_t)TL::STAGES * TL::STAGE;
+  size_t lds = (size_t)TL::STAGES * StageBytes<T, TL::BM, TL::BN, X6B>::v;
   if (PRO) lds += (size_t)k.n_first_max * k.a.Cin * sizeof(T);
   lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
   lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
   if (lds > 160 * 1024) return set_error("conv: LDS budget exceeded");
-  auto fn = conv_kernel<T, TL, PRO, SMALLC, EPI>;
+  auto fn = conv_kernel<T, TL, PRO, SMALLC, EPI, X6B>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -352,8 +409,28 @@ static int launch_bn(ConvK& k, hipStream_t st) {
   return launch_tile<T, Tile128x128, PRO, SMALLC>(k, st);
 }
 
+// fp32, every group pre-split, unmodulated, Cin ≥ 32, Cout > 64: the X6B 128×128 tile (2 stages,
+// exactly 80 KB of LDS, 2 blocks per CU): e4e style-head convs 155 / 175 TFLOP/s vs 142 / 150 on
+// the on-the-fly split (64²→32² / 32²→16², 512 → 512). At Cout ≤ 64 (128×64 tile, two B
+// fragments per wave) it measured 2–11 % slower and is not used. MIA_CONV_X6=0 disables (A/B).
+static bool x6b_ok(const ConvK& k) {
+#ifdef MIA_F32_NATIVE
+  (void)k;
+  return false;
+#else
+  const char* e = getenv("MIA_CONV_X6");
+  if (e && atoi(e) == 0) return false;
+  for (int g = 0; g < k.ng; ++g)
+    if (!k.g[g].w_split) return false;
+  return k.a.in_scale == nullptr && k.a.act_in == MIA_ACT_NONE && k.a.Cin >= 32 && k.a.Cout > 64;
+#endif
+}
+
 template <typename T>
 static int launch_conv(ConvK& k, hipStream_t st) {
+  if constexpr (std::is_same<T, float>::value) {
+    if (x6b_ok(k)) return launch_tile<T, Tile128x128, false, false, -2, true>(k, st);
+  }
   const bool pro = k.a.in_scale != nullptr || k.a.act_in != MIA_ACT_NONE;
   const bool small = k.a.Cin < ROWB / (int)sizeof(T);
   if (pro) return small ? launch_bn<T, true, true>(k, st) : launch_bn<T, true, false>(k, st);

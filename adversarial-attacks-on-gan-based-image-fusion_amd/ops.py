@@ -701,8 +701,7 @@ def conv2d(x, groups, y, out_hw, *, cout, stride=1, bias=None, act_out=ACT_NONE,
         ho, wo = g["ho"], g["wo"]
         if ho <= 0 or wo <= 0 or ay * (ho - 1) + by >= oh or ax * (wo - 1) + bx >= ow:
             raise ValueError(f"group {i}: placement outside the output grid")
-        wsp = (layouts.split_for(g["w"]) if T == torch.float32 and len(groups) == 1 and
-               stride == 1 and kh == 3 and kw == 3 else None)
+        wsp = layouts.split_for(g["w"]) if T == torch.float32 else None
         garr[i] = _lib.ConvGroup(ptr(g["w"]).value, kh, kw, py, px, ho, wo, ay, by, ax, bx,
                                  ptr(wsp).value if wsp is not None else None)
         keep.append(g["w"])

@@ -48,6 +48,7 @@ SHAPES = [
     ("e4e mask+slope 32² 256→256", 32, 256, 256, "mslope"),
     ("e4e acc 32² 256→256", 32, 256, 256, "acc"),
     # e4e GradualStyleBlock convs (stride 2, bias + LeakyReLU(0.01)); H = output side
+    ("head s2 →32² 512→512", 32, 512, 512, "head"),
     ("head s2 →16² 512→512", 16, 512, 512, "head"),
     ("head s2 →8² 512→512", 8, 512, 512, "head"),
     ("head s2 →4² 512→512", 4, 512, 512, "head"),

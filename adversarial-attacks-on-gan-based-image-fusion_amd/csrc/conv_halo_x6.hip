@@ -18,6 +18,12 @@
 // waves 0–3 stream the weights one K-step ahead, waves 4–7 the next channel block's halo during
 // taps 0–3. Per channel block one extra barrier: the lo buffer is rewritten after the last tap of
 // the previous block has read it.
+// Measured dead end: each wave owning 16 channels × all 256 pixels with its weights loaded from
+// L2 straight into VGPRs (no weight ring, no per-K-step barrier, 9 VALU per 96 MFMAs with
+// padded [hi|mid] / [lo|hi] planes read as single ds_read_b128 tuples) ran 4–13 % SLOWER than
+// this kernel: the per-K-step barrier is not the limiter. At ≈ 200 TFLOP/s these layers run
+// ≈ 0.75 of the six-product rate at the ≈ 1.6 GHz the chip holds under this MFMA load
+// (2500 × 1.6 / 2.4 / 6 ≈ 278 TFLOP/s).
 #include "conv_common.h"
 #include "halo_epilogue.h"
 
@@ -245,211 +251,6 @@ __global__ __launch_bounds__(HaloX6::NT, 2) void conv_halo_x6_kernel(const ConvK
   }
 }
 
-// ---- v2: weights straight into VGPRs, no per-K-step barrier ----------------------------------
-// Same patch (16 × 16 pixels × 128 channels, 8 waves, one block per CU), but every wave owns 16
-// output channels × all 256 pixels (16 pixel-row fragments × 1 channel fragment), so no two waves
-// need the same weight fragment: each wave loads its own pre-split weights for the next K-step
-// from global memory (L2) into registers (global_load_dwordx4 + _dwordx2 per half step) while it
-// computes the current one. Only the halo goes through LDS and the only barriers are the two per
-// 32-channel block around its split (v1: one per K-step, stalling all 8 waves every 96 MFMAs).
-// LDS: the raw halo (DMA target, 128-B rows) and its split image as two padded planes of 16-B
-// quad records per pixel, [hi×4 | mid×4] and [lo×4 | hi×4]: each A operand tuple of the three
-// MFMAs is ONE ds_read_b128 (no register moves), rows padded to 160 B (conflict-free for the
-// b128 lane groups at any start row, checked exhaustively), so every fragment address of a tap
-// is a base + compile-time offset. The raw buffer is refilled with the next block during the 9
-// taps of the current one.
-struct HaloX6R {
-  static constexpr int PH = 16, PW = 16, FM = 16, FN = 1, WM = 1, WN = 8, NW = 8, NT = 64 * NW;
-  static constexpr int BM = PH * PW, BN = 128, BK = 32;
-  static constexpr int HSIDE = PW + 2, HROWS = (PH + 2) * HSIDE;
-  static constexpr int HPIECES = (HROWS + 7) / 8;
-  static constexpr int RAW = HPIECES * 1024;       // raw fp32 halo, 128-B rows
-  static constexpr int SROW = 160, SPLANE = HROWS * SROW;  // split planes, padded rows
-  static constexpr int H_INS = (HPIECES + NW - 1) / NW;    // halo pieces per wave
-  static constexpr int LDS = RAW + 2 * SPLANE;
-  static_assert(WN * FN * 16 == BN && WM * FM * 16 == BM, "");
-  static_assert(LDS <= 160 * 1024 && (FM - 1) * HSIDE * SROW + 2 * SROW + 64 < 65536, "");
-};
-
-template <bool PRO, int EPI>
-__global__ __launch_bounds__(HaloX6R::NT, 2) void conv_halo_x6r_kernel(const ConvK k) {
-  typedef HaloX6R TL;
-  constexpr int FM = TL::FM, NT = TL::NT, BK = TL::BK, NW = TL::NW;
-  constexpr int HSIDE = TL::HSIDE, HROWS = TL::HROWS, HPIECES = TL::HPIECES;
-  constexpr int H_INS = TL::H_INS, SROW = TL::SROW;
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* const raw = smem;                      // DMA target: raw fp32 halo of the next block
-  char* const phm = smem + TL::RAW;            // [hi|mid] plane of the current block
-  char* const plh = phm + TL::SPLANE;          // [lo|hi] plane of the current block
-
-  const mia_conv_args& p = k.a;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const ConvGroup G = k.g[0];
-  const int H = p.H, W = p.W, Cin = p.Cin, Cout = p.Cout, Kpad = G.kpad;
-  const int bl = xcd_remap(blockIdx.x, k.nblk);
-  const int mt = bl / k.nbn, n0 = (bl % k.nbn) * TL::BN;
-  const int ptx = W / TL::PW, pty = H / TL::PH;
-  const int x0 = (mt % ptx) * TL::PW;
-  const int y0 = ((mt / ptx) % pty) * TL::PH;
-  const int n = mt / (ptx * pty);
-  const int frow = lane & 15, fq = lane >> 4;
-
-  const float* __restrict__ X = (const float*)p.x;
-  // this lane's weight row (output channel) and quad: k = 4·(h·4 + fq) … of each K-step
-  const int co = n0 + wid * 16 + frow;
-  const unsigned* Whm = (const unsigned*)G.w_split;
-  const __bf16* Wl = (const __bf16*)(Whm + (size_t)Cout * Kpad);
-  const bool cok = co < Cout;
-  const unsigned* whm = cok ? Whm + (size_t)co * Kpad + fq * 4 : (const unsigned*)g_zero16;
-  const __bf16* wl = cok ? Wl + (size_t)co * Kpad + fq * 4 : (const __bf16*)g_zero16;
-  const int wstep = cok ? 1 : 0;  // the zero page does not advance
-
-  const char* src[H_INS];
-#pragma unroll
-  for (int j = 0; j < H_INS; ++j) {
-    src[j] = nullptr;
-    const int hr = (wid + NW * j) * 8 + (lane >> 3);
-    const int hy = hr / HSIDE, hx = hr - (hr / HSIDE) * HSIDE;
-    const int y = y0 + hy - 1, x = x0 + hx - 1;
-    if (hr < HROWS && y >= 0 && y < H && x >= 0 && x < W)
-      src[j] = (const char*)(X + ((size_t)(n * H + y) * W + x) * Cin + (lane & 7) * 4);
-  }
-  const int my_pieces = (HPIECES - wid + NW - 1) / NW;
-  const int ncb = Cin / BK, nk = 9 * ncb;
-  auto issue_h = [&](int cb) {  // raw halo of channel block cb (lane-linear rows)
-#pragma unroll
-    for (int j = 0; j < H_INS; ++j) {
-      if (j < my_pieces) {
-        const char* a = src[j] ? src[j] + (size_t)cb * BK * 4 : (const char*)g_zero16;
-        __builtin_amdgcn_global_load_lds((gptr_t)a, (lptr_t)(raw + (wid + NW * j) * 1024), 16,
-                                         0, 0);
-      }
-    }
-  };
-  auto load_w = [&](int s, u32x4 (&hm)[2], u32x2 (&lo)[2]) {  // weights of K-step s = (cb, tap)
-    const int cb = s / 9, t = s - (s / 9) * 9;
-    const size_t koff = (size_t)(t * Cin + cb * BK) * wstep;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      hm[h] = *(const u32x4*)(whm + koff + h * 16 * wstep);
-      lo[h] = *(const u32x2*)(wl + koff + h * 16 * wstep);
-    }
-  };
-  const bool lrelu_in = p.act_in == MIA_ACT_LRELU_S2;
-  auto convert = [&](int cb) {  // raw → the two split planes (modulation first for a StyledConv)
-    for (int c = tid; c < HROWS * 8; c += NT) {
-      const int hr = c >> 3, q = c & 7;
-      f32x4 v = *(const f32x4*)(raw + hr * ROWB + q * 16);
-      if constexpr (PRO) {
-        const float mul = lrelu_in ? SQRT2 : 1.f;
-        f32x4 s4 = {1.f, 1.f, 1.f, 1.f};
-        if (p.in_scale) s4 = *(const f32x4*)(p.in_scale + (size_t)n * Cin + cb * BK + q * 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float f = v[e];
-          if (lrelu_in) f = fmaxf(f, 0.2f * f);
-          v[e] = f * (s4[e] * mul);
-        }
-      }
-      u32x4 hm;
-      u32x2 lo;
-      split_quad(v, hm, lo);
-      *(u32x4*)(phm + hr * SROW + q * 16) = hm;
-      *(u32x4*)(plh + hr * SROW + q * 16) = u32x4{lo[0], lo[1], hm[0], hm[1]};
-    }
-  };
-
-  // ---- prologue ------------------------------------------------------------------------------
-  u32x4 whm_cur[2], whm_nxt[2];
-  u32x2 wlo_cur[2], wlo_nxt[2];
-  load_w(0, whm_cur, wlo_cur);
-  issue_h(0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  convert(0);
-  __syncthreads();
-  if (ncb > 1) issue_h(1);
-
-  f32x4 acc[FM][1];
-#pragma unroll
-  for (int i = 0; i < FM; ++i) acc[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  int cb = 0, t = 0;
-  for (int s = 0; s < nk; ++s) {
-    if (s + 1 < nk) load_w(s + 1, whm_nxt, wlo_nxt);
-    const int dy = t >= 6 ? 2 : (t >= 3 ? 1 : 0), dx = t - 3 * dy;
-    const int base = ((dy * HSIDE + dx + frow) * SROW) + fq * 16;  // this lane's tap base
-    const char* bhm = phm + base;
-    const char* blh = plh + base;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      // (hi,mid)·(hi,mid) + (lo,hi)·(hi,mid) + (hi,mid)·(lo,hi), weights as the MFMA A operand
-      const bf16x8 WHM = __builtin_bit_cast(bf16x8, whm_cur[h]);
-      const bf16x8 WLH = __builtin_bit_cast(
-          bf16x8, u32x4{wlo_cur[h][0], wlo_cur[h][1], whm_cur[h][0], whm_cur[h][1]});
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const bf16x8 XHM = *(const bf16x8*)(bhm + i * HSIDE * SROW + h * 64);
-        const bf16x8 XLH = *(const bf16x8*)(blh + i * HSIDE * SROW + h * 64);
-        f32x4 c = acc[i][0];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(WHM, XLH, c, 0, 0, 0);  // hl + mh
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(WLH, XHM, c, 0, 0, 0);  // lh + hm
-        acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(WHM, XHM, c, 0, 0, 0);  // hh + mm
-      }
-    }
-    if (++t == 9) {
-      // end of a channel block: every wave is past its reads of the planes and the next block's
-      // raw halo has landed; split it, publish, and start the DMA of the block after it
-      if (cb + 1 < ncb) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        convert(cb + 1);
-        __syncthreads();
-        if (cb + 2 < ncb) issue_h(cb + 2);
-      }
-      t = 0;
-      ++cb;
-    } else if (t == 1 && cb > 0 && cb + 1 < ncb) {
-      // the halo DMA of this block was issued before the weights of step s+1: wait for those
-      // weights only (vmcnt retires in order), the halo may stay in flight
-      wait_vmcnt(TL::H_INS);
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      whm_cur[h] = whm_nxt[h];
-      wlo_cur[h] = wlo_nxt[h];
-    }
-  }
-  if constexpr (EPI >= 0) {
-    halo_epilogue_f<float, TL, EPI>(k, acc, n, y0, x0, n0, 0, wid, lane, -1, -1, nullptr,
-                                    nullptr, TL::WM, TL::BN);
-  } else {
-    halo_epilogue<float, TL>(k, acc, n, y0, x0, n0, 0, wid, lane);
-  }
-}
-
-template <bool PRO, int EPI>
-static int launch_x6r_(ConvK& k, hipStream_t st) {
-  typedef HaloX6R TL;
-  k.nbn = (k.a.Cout + TL::BN - 1) / TL::BN;
-  k.nblk = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW) * k.nbn;
-  auto fn = conv_halo_x6r_kernel<PRO, EPI>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
-      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-    attr_set = true;
-  }
-  k.prered = 0;
-  hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), (size_t)TL::LDS, st, k);
-  return check_launch("conv_halo_x6r");
-}
-
 template <bool PRO, int EPI>
 static int launch_x6_(ConvK& k, hipStream_t st) {
   typedef HaloX6 TL;
@@ -491,8 +292,6 @@ bool conv_halo_x6_eligible(const ConvK& k, int dtype) {
 
 int launch_conv_halo_x6(ConvK& k, hipStream_t st) {
   const bool pro = k.a.in_scale != nullptr || k.a.act_in != MIA_ACT_NONE;
-  const char* v = getenv("MIA_X6_VARIANT");  // A/B: 1 = weight ring in LDS, 2 = weights in VGPRs
-  if (!v || atoi(v) == 2) return pro ? launch_x6r_<true, -1>(k, st) : launch_x6r_<false, -1>(k, st);
   const char* e = getenv("MIA_HALO_EPI");  // A/B: 0 = LDS-staged shared epilogue
   if (e && atoi(e) == 0) return pro ? launch_x6_<true, -2>(k, st) : launch_x6_<false, -2>(k, st);
   return pro ? launch_x6_<true, -1>(k, st) : launch_x6_<false, -1>(k, st);

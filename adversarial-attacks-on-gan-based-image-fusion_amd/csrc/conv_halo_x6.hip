@@ -29,9 +29,13 @@
 
 namespace mia {
 
+// BN_ = 128: 4 row waves × 2 column waves of 4 × 4 fragments; BN_ = 64 (the 64-channel layers):
+// 8 row waves of 2 × 4 fragments.
+template <int BN_>
 struct HaloX6 {
-  static constexpr int PH = 16, PW = 16, FM = 4, FN = 4, WM = 4, WN = 2, NW = 8, NT = 64 * NW;
-  static constexpr int BM = PH * PW, BN = 128, BK = 32;  // 32 fp32 channels per K-step
+  static constexpr int PH = 16, PW = 16, NW = 8, NT = 64 * NW;
+  static constexpr int WN = BN_ == 128 ? 2 : 1, WM = NW / WN, FM = 16 / WM, FN = 4;
+  static constexpr int BM = PH * PW, BN = BN_, BK = 32;  // 32 fp32 channels per K-step
   static constexpr int HSIDE = PW + 2, HROWS = (PH + 2) * HSIDE;  // 324 halo pixels
   static constexpr int HPIECES = (HROWS + 7) / 8;                 // 1-KB pieces of 8 rows
   static constexpr int HBUF = HPIECES * 1024;
@@ -49,9 +53,9 @@ struct HaloX6 {
   static_assert(LDS <= 160 * 1024, "");
 };
 
-template <bool PRO, int EPI>
-__global__ __launch_bounds__(HaloX6::NT, 2) void conv_halo_x6_kernel(const ConvK k) {
-  typedef HaloX6 TL;
+template <int BN_, bool PRO, int EPI>
+__global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const ConvK k) {
+  typedef HaloX6<BN_> TL;
   constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, NT = TL::NT, BN = TL::BN, BK = TL::BK;
   constexpr int HSIDE = TL::HSIDE, HROWS = TL::HROWS, HPIECES = TL::HPIECES, HBUF = TL::HBUF;
   constexpr int H_INS = TL::H_INS, HPS = TL::H_PER_STEP, HWAVES = TL::HWAVES;
@@ -251,15 +255,15 @@ __global__ __launch_bounds__(HaloX6::NT, 2) void conv_halo_x6_kernel(const ConvK
   }
 }
 
-template <bool PRO, int EPI>
+template <int BN_, bool PRO, int EPI>
 static int launch_x6_(ConvK& k, hipStream_t st) {
-  typedef HaloX6 TL;
+  typedef HaloX6<BN_> TL;
   k.nbn = (k.a.Cout + TL::BN - 1) / TL::BN;
   k.nblk = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW) * k.nbn;
   size_t lds = TL::LDS;
   lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
   lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
-  auto fn = conv_halo_x6_kernel<PRO, EPI>;
+  auto fn = conv_halo_x6_kernel<BN_, PRO, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -273,7 +277,7 @@ static int launch_x6_(ConvK& k, hipStream_t st) {
 }
 
 // Eligible: fp32 with pre-split weights (mia_conv_args.w_split / mia_conv_group.w_split), one
-// group, stride 1, 3×3 pad 1, identity placement, 16-divisible maps, Cin % 32 == 0, Cout > 64.
+// group, stride 1, 3×3 pad 1, identity placement, 16-divisible maps, Cin % 32 == 0, Cout ≥ 64.
 bool conv_halo_x6_eligible(const ConvK& k, int dtype) {
 #ifdef MIA_F32_NATIVE
   (void)k;
@@ -287,14 +291,23 @@ bool conv_halo_x6_eligible(const ConvK& k, int dtype) {
   return dtype == MIA_F32 && G.w_split != nullptr && k.ng == 1 && k.stride == 1 && G.kh == 3 &&
          G.kw == 3 && G.pad_y == 1 && G.pad_x == 1 && G.ho == a.H && G.wo == a.W && G.ay == 1 &&
          G.ax == 1 && G.by == 0 && G.bx == 0 && !a.shuffle_out && a.H % 16 == 0 &&
-         a.W % 16 == 0 && a.Cin % 32 == 0 && a.Cout > 64 && k.HT == a.H && k.WT == a.W;
+         a.W % 16 == 0 && a.Cin % 32 == 0 && k.HT == a.H && k.WT == a.W &&
+         // 64 channels: the 64-column tile, where the epilogue reads no per-pixel aux tensor
+         // (with tap / mask / accumulate operands it measured 6–9 % slower than the generic
+         // tile: one block per CU leaves that epilogue exposed; without them 2–11 % faster)
+         (a.Cout > 64 || (a.Cout == 64 && !a.tap_a && !a.mask_a && !a.accumulate));
 }
 
 int launch_conv_halo_x6(ConvK& k, hipStream_t st) {
   const bool pro = k.a.in_scale != nullptr || k.a.act_in != MIA_ACT_NONE;
   const char* e = getenv("MIA_HALO_EPI");  // A/B: 0 = LDS-staged shared epilogue
-  if (e && atoi(e) == 0) return pro ? launch_x6_<true, -2>(k, st) : launch_x6_<false, -2>(k, st);
-  return pro ? launch_x6_<true, -1>(k, st) : launch_x6_<false, -1>(k, st);
+  const bool lds_epi = e && atoi(e) == 0;
+  if (k.a.Cout == 64) {
+    if (lds_epi) return pro ? launch_x6_<64, true, -2>(k, st) : launch_x6_<64, false, -2>(k, st);
+    return pro ? launch_x6_<64, true, -1>(k, st) : launch_x6_<64, false, -1>(k, st);
+  }
+  if (lds_epi) return pro ? launch_x6_<128, true, -2>(k, st) : launch_x6_<128, false, -2>(k, st);
+  return pro ? launch_x6_<128, true, -1>(k, st) : launch_x6_<128, false, -1>(k, st);
 }
 
 }  // namespace mia

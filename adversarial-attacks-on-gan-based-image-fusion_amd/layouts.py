@@ -188,15 +188,17 @@ def _pack_words(lo16, hi16):
 
 
 def split_f32(w):
-    """Pre-split fp32 weights for the split-once halo kernel (mia_conv_args.w_split,
-    csrc/conv_halo_x6.hip): w [Cout][Kpad] fp32 (Kpad % 4 == 0) → int32 words
+    """Pre-split fp32 weights for the split-once kernels (mia_conv_args.w_split,
+    csrc/conv_halo_x6.hip; the packed up-conv / stride-2-adjoint weights viewed as rows of their
+    last dimension): w [Cout][Kpad] fp32 (Kpad % 4 == 0) → int32 words
     [Cout][Kpad] of per-4-k-quad records [hi0 hi1 hi2 hi3 | mid0 mid1 mid2 mid3] (bf16), then
     [Cout][Kpad/2] words of [lo0 lo1 lo2 lo3] (bf16) — w = hi + mid + lo exactly, hi = w with the
     low 16 bits cleared, mid = (w − hi) likewise, lo = w − hi − mid (conv_common.h split3)."""
-    if w.dtype != torch.float32 or w.dim() != 2 or w.shape[1] % 4:
-        raise ValueError("split_f32: [Cout][Kpad] fp32 with Kpad % 4 == 0")
+    if w.dtype != torch.float32 or w.dim() < 2 or w.shape[-1] % 4:
+        raise ValueError("split_f32: [...][Kpad] fp32 with Kpad % 4 == 0 (rows = all but the last "
+                         "dimension)")
     dev = w.device
-    a = w.detach().to("cpu").contiguous()
+    a = w.detach().to("cpu").contiguous().reshape(-1, w.shape[-1])
     mask = torch.tensor(-65536, dtype=torch.int32)  # 0xffff0000
     hi = (a.view(torch.int32) & mask).view(torch.float32)
     r = a - hi

@@ -19,7 +19,7 @@ from collections import defaultdict
 
 # every kernel a conv API call of the attack launches (ops.conv3x3 / upconv_fwd / upconv_dgrad):
 # the implicit-GEMM tiles, the halo tiles, the halo up-conv and the thin-channel VGG input layer
-CONV = re.compile(r"conv_(halo_|wres_)?kernel|upconv_halo_kernel|conv_thin_(in|out)_kernel")
+CONV = re.compile(r"conv_(halo_|wres_|halo_x6_)?kernel|upconv_halo_kernel|conv_thin(_in|_out|32)_kernel")
 # (e4e: mia_conv2d launches conv_kernel / conv_halo_kernel; mia_conv_s2_dgrad_halo launches the
 # up-conv halo kernel in DG mode)
 # mia_upconv_fwd_halo is ONE API call that launches TWO kernels (upconv_halo_kernel for the

@@ -1,4 +1,5 @@
-// Thin-channel 3×3 convolutions (stride 1, pad 1, NHWC, 2-byte types): the VGG input layer
+// Thin-channel 3×3 convolutions (stride 1, pad 1, NHWC; MFMA for 2-byte types, fp32 VALU for
+// fp32): the VGG input layer
 // conv1_1 (code/vgg.py:45, 3 → 64 channels; the image is padded to 8 channels) and its input
 // gradient (64 → 8 channels, 3 real). Both move far more bytes than they compute (forward: 16 B
 // read and 128 B written per pixel for 27·64 MACs; gradient: 128 B read and 16 B written), so they
@@ -338,6 +339,238 @@ static int grid_for(int64_t groups, int waves_per_cu = 32) {
   return (int)std::max<int64_t>(1, (waves + 3) / 4);
 }
 
+// ---- fp32 thin layers on the fp32 VALU ------------------------------------------------------
+// In fp32 the two input layers are HBM-bound with ≈ 1.7 k real MACs per pixel (3 real image
+// channels): on the fp32 VALU (v_fma_f32, fp32 products, no operand split) the FMAs take
+// ≈ 0.5 ms per 128 × 256² images against ≈ 0.5 ms of HBM traffic, where the split-MFMA tiles ran
+// at 1.3 ms (forward) / 3.5 ms (gradient). The padded image channels have all-zero weights; each
+// block finds them from the weights (a channel with a nonzero weight is "real") and skips them —
+// exact, since the skipped terms are products with zero weights (and the padded input channels
+// are zero). Both kernels give each 16-lane group of a wave one 4-pixel row segment, so every
+// global access is a contiguous 256-B pixel record (lane = 4 channels) and the segment's
+// 3 × 6 input pixels are loaded once for its 4 × 9 taps.
+__device__ __forceinline__ int64_t thin_seg_origin(int64_t seg, int H, int W, int& n, int& yy,
+                                                   int& x0) {
+  const int spr = W / 4;  // 4-pixel segments per row
+  const int64_t row = seg / spr;
+  x0 = (int)(seg - row * spr) * 4;
+  n = (int)(row / H);
+  yy = (int)(row - (int64_t)n * H);
+  return row * W + x0;  // first pixel index of the segment
+}
+
+// forward, Cin = 8 → 64, + bias, act. Lane q of a group owns output channels 4q … 4q+3; the
+// weights are transposed into LDS as [k][64] (one 16-B read per (tap, channel) serves the
+// segment's 4 pixels × 4 channels). CM: the real input channels as a compile-time mask (0x07, the
+// RGB image), or 0xff with the runtime mask cmask.
+template <int CM>
+__device__ __forceinline__ void thin_in_f32_body(const float* __restrict__ x,
+                                                 const float* __restrict__ wl, int cmask,
+                                                 const f32x4 bs, const f32x4 sl, int act,
+                                                 float* __restrict__ y, int N, int H, int W) {
+  constexpr int CIN = 8, COUT = 64;
+  const int tid = threadIdx.x, c0 = 4 * (tid & 15);
+  const bool hi4 = (cmask >> 4) != 0;  // a real channel among 4 … 7: load the second half too
+  const int64_t nseg = (int64_t)N * H * (W / 4);
+  for (int64_t seg = (int64_t)blockIdx.x * 16 + (tid >> 4); seg < nseg;
+       seg += (int64_t)gridDim.x * 16) {
+    int n, yy, x0;
+    const int64_t pix0 = thin_seg_origin(seg, H, W, n, yy, x0);
+    f32x4 acc[4] = {bs, bs, bs, bs};
+#pragma unroll
+    for (int ty = 0; ty < 3; ++ty) {
+      const int sy = yy + ty - 1;
+      if (sy < 0 || sy >= H) continue;
+      f32x4 xa[6], xb[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const int sx = x0 + c - 1;
+        const bool ok = sx >= 0 && sx < W;
+        const float* xp = x + ((size_t)(n * H + sy) * W + (ok ? sx : 0)) * CIN;
+        xa[c] = ok ? *(const f32x4*)xp : f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (CM >> 4) xb[c] = ok && hi4 ? *(const f32x4*)(xp + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int tx = 0; tx < 3; ++tx)
+#pragma unroll
+        for (int ci = 0; ci < CIN; ++ci) {
+          if (!((CM >> ci) & 1)) continue;
+          if (CM == 0xff && !((cmask >> ci) & 1)) continue;
+          const f32x4 wv = *(const f32x4*)(wl + ((3 * ty + tx) * CIN + ci) * COUT + c0);
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const float xv = ci < 4 ? xa[p + tx][ci & 3] : xb[p + tx][ci & 3];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[p][e] = fmaf(xv, wv[e], acc[p][e]);
+          }
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      f32x4 o = acc[p];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (act == MIA_ACT_PRELU) o[e] = o[e] > 0.f ? o[e] : sl[e] * o[e];
+        else o[e] = apply_act(o[e], act);
+      }
+      *(f32x4*)(y + (size_t)(pix0 + p) * COUT + c0) = o;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void conv_thin_in_f32_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, int kpad,
+    const float* __restrict__ bias, int act, const float* __restrict__ slope,
+    float* __restrict__ y, int N, int H, int W) {
+  constexpr int CIN = 8, COUT = 64, K = 9 * CIN;
+  __shared__ __attribute__((aligned(16))) float wl[K * COUT];
+  __shared__ int cmask_s;
+  const int tid = threadIdx.x;
+  if (tid == 0) cmask_s = 0;
+  __syncthreads();
+  int cm = 0;
+  for (int i = tid; i < K * COUT; i += 256) {
+    const int co = i / K, kk = i - co * K;
+    const float v = w[(size_t)co * kpad + kk];
+    wl[kk * COUT + co] = v;
+    if (v != 0.f) cm |= 1 << (kk % CIN);
+  }
+  if (cm) atomicOr(&cmask_s, cm);
+  __syncthreads();
+  const int cmask = __builtin_amdgcn_readfirstlane(cmask_s);
+  const int c0 = 4 * (tid & 15);
+  f32x4 bs = {0.f, 0.f, 0.f, 0.f}, sl = {0.f, 0.f, 0.f, 0.f};
+  if (bias) bs = *(const f32x4*)(bias + c0);
+  if (act == MIA_ACT_PRELU) sl = *(const f32x4*)(slope + c0);
+  if (cmask == 0x07) thin_in_f32_body<0x07>(x, wl, cmask, bs, sl, act, y, N, H, W);
+  else thin_in_f32_body<0xff>(x, wl, cmask, bs, sl, act, y, N, H, W);
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float a) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, a), CTRL,
+                                                               0xf, 0xf, false));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]: every lane holds its quad's sum
+  v += dpp_f<0x141>(v);  // row_half_mirror: lane i ↔ 7 − i of its 8-lane half
+  return v + dpp_f<0x140>(v);  // row_mirror: lane i ↔ 15 − i
+}
+
+// input gradient, Cin = 64 → 8 output channels (store or accumulate). Lane q of a group holds
+// the input channels 4q … 4q+3 of every tap and the weights of output channels 0 … 3 for them
+// in VGPRs; the segment's 4 pixels × 4 output channels are reduced over the 16 lanes by DPP.
+// Real output channels ≥ 4 (never the case for an RGB image) take a slower path with the weights
+// as wave-uniform scalar loads, one pixel per lane.
+template <bool ACC>
+__global__ __launch_bounds__(256) void conv_thin_out_f32_kernel(
+    const float* __restrict__ g, const float* __restrict__ w, int kpad, float* __restrict__ y,
+    int N, int H, int W) {
+  constexpr int CIN = 64, COUT = 8, K = 9 * CIN;
+  __shared__ int cmask_s;
+  const int tid = threadIdx.x;
+  if (tid == 0) cmask_s = 0;
+  __syncthreads();
+  int cm = 0;
+  for (int i = tid; i < COUT * K; i += 256) {
+    const int co = i / K;
+    if (w[(size_t)co * kpad + (i - co * K)] != 0.f) cm |= 1 << co;
+  }
+  if (cm) atomicOr(&cmask_s, cm);
+  __syncthreads();
+  const int cmask = __builtin_amdgcn_readfirstlane(cmask_s);
+  if (cmask >> 4) {  // general path
+    const int64_t npix = (int64_t)N * H * W;
+    for (int64_t pix = (int64_t)blockIdx.x * 256 + tid; pix < npix;
+         pix += (int64_t)gridDim.x * 256) {
+      const int n = (int)(pix / ((int64_t)H * W));
+      const int rem = (int)(pix - (int64_t)n * H * W);
+      const int yy = rem / W, xx = rem - (rem / W) * W;
+      float acc[COUT];
+#pragma unroll
+      for (int co = 0; co < COUT; ++co) acc[co] = 0.f;
+      for (int t = 0; t < 9; ++t) {
+        const int sy = yy + t / 3 - 1, sx = xx + t % 3 - 1;
+        if (sy < 0 || sy >= H || sx < 0 || sx >= W) continue;
+        const float* gp = g + ((size_t)(n * H + sy) * W + sx) * CIN;
+        for (int c4 = 0; c4 < CIN / 4; ++c4) {
+          const f32x4 gv = *(const f32x4*)(gp + 4 * c4);
+#pragma unroll
+          for (int co = 0; co < COUT; ++co) {
+            const float* wr = w + (size_t)co * kpad + t * CIN + 4 * c4;  // wave-uniform
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[co] = fmaf(gv[e], wr[e], acc[co]);
+          }
+        }
+      }
+      float* yp = y + (size_t)pix * COUT;
+#pragma unroll
+      for (int co = 0; co < COUT; ++co) yp[co] = ACC ? yp[co] + acc[co] : acc[co];
+    }
+    return;
+  }
+  const int q = tid & 15;
+  float wv[9][4][4];  // [tap][input channel 4q + e][output channel]
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int co = 0; co < 4; ++co) wv[t][e][co] = w[(size_t)co * kpad + t * CIN + 4 * q + e];
+  const int64_t nseg = (int64_t)N * H * (W / 4);
+  for (int64_t seg = (int64_t)blockIdx.x * 16 + (tid >> 4); seg < nseg;
+       seg += (int64_t)gridDim.x * 16) {
+    int n, yy, x0;
+    const int64_t pix0 = thin_seg_origin(seg, H, W, n, yy, x0);
+    float acc[4][4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int co = 0; co < 4; ++co) acc[p][co] = 0.f;
+#pragma unroll
+    for (int ty = 0; ty < 3; ++ty) {
+      const int sy = yy + ty - 1;
+      if (sy < 0 || sy >= H) continue;
+      f32x4 gr[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const int sx = x0 + c - 1;
+        const bool ok = sx >= 0 && sx < W;
+        gr[c] = ok ? *(const f32x4*)(g + ((size_t)(n * H + sy) * W + sx) * CIN + 4 * q)
+                   : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int tx = 0; tx < 3; ++tx)
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int co = 0; co < 4; ++co)
+              acc[p][co] = fmaf(gr[p + tx][e], wv[3 * ty + tx][e][co], acc[p][co]);
+    }
+    // lanes 2p, 2p + 1 of the group write pixel p's channels 0–3 / 4–7 (zero, or unchanged)
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int co = 0; co < 4; ++co) {
+        const float s = row16_sum(acc[p][co]);
+        if (q == 2 * p) o[co] = s;
+      }
+    if (q < 8) {
+      float* yp = y + (size_t)(pix0 + (q >> 1)) * COUT + 4 * (q & 1);
+      if constexpr (ACC) {
+        const f32x4 a = *(const f32x4*)yp;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] += a[e];
+      }
+      *(f32x4*)yp = o;
+    }
+  }
+}
+
 // 32 → 32 layers: 2-byte type, one group, stride 1, 3×3 pad 1, identity placement, W % 16 == 0,
 // an epilogue feature mask with a specialisation (the StyledConv forward and input gradient).
 // MIA_CONV_THIN32=0 disables (A/B switch, read per launch).
@@ -398,15 +631,15 @@ int launch_conv_thin32(ConvK& k, int dtype, hipStream_t st) {
   return set_error("conv_thin32: no specialisation for this launch");
 }
 
-// Eligible launches (checked by run_conv): 2-byte type, one group, stride 1, 3×3 pad 1, identity
-// output placement, W % 16 == 0, and either (Cin 8 → Cout 64, epilogue = bias + ReLU / PReLU: the
-// VGG and e4e input layers) or (Cin 64 → Cout 8, plain or accumulating: their input gradients).
+// Eligible launches (checked by run_conv): any dtype (fp32 on the VALU kernels above), one
+// group, stride 1, 3×3 pad 1, identity output placement, W % 16 == 0, and either (Cin 8 → Cout
+// 64, epilogue = bias + ReLU / PReLU: the VGG and e4e input layers) or (Cin 64 → Cout 8, plain or accumulating: their input gradients).
 bool conv_thin_eligible(const ConvK& k, int dtype) {
   const char* e = getenv("MIA_CONV_THIN");  // tuning / A-B switch: 0 disables the thin kernels
   if (e && atoi(e) == 0) return false;
   const mia_conv_args& a = k.a;
   const ConvGroup& G = k.g[0];
-  if (dtype == MIA_F32 || k.ng != 1 || k.stride != 1 || G.kh != 3 || G.kw != 3 || G.pad_y != 1 ||
+  if (k.ng != 1 || k.stride != 1 || G.kh != 3 || G.kw != 3 || G.pad_y != 1 ||
       G.pad_x != 1 || G.ho != a.H || G.wo != a.W || G.ay != 1 || G.ax != 1 || G.by != 0 ||
       G.bx != 0 || a.shuffle_out || a.W % 16 != 0 || k.HT != a.H || k.WT != a.W ||
       k.ystride != a.Cout || a.act_in != MIA_ACT_NONE || a.in_scale || a.out_scale || a.noise ||
@@ -420,6 +653,23 @@ bool conv_thin_eligible(const ConvK& k, int dtype) {
 int launch_conv_thin(ConvK& k, int dtype, hipStream_t st) {
   const mia_conv_args& a = k.a;
   const int grid = grid_for((int64_t)a.N * a.H * (a.W / 16));  // ≤ 8 waves per SIMD
+  if (dtype == MIA_F32) {  // the fp32 VALU kernels (one pixel per thread / per 16 threads)
+    const int64_t npix = (int64_t)a.N * a.H * a.W;
+    if (a.Cin == 8) {
+      hipLaunchKernelGGL(conv_thin_in_f32_kernel, dim3(grid_for(npix / 16, 8)), dim3(256), 0, st,
+                         (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, a.bias,
+                         a.act_out, a.act_slope, (float*)a.y, a.N, a.H, a.W);
+    } else if (a.accumulate) {
+      hipLaunchKernelGGL(conv_thin_out_f32_kernel<true>, dim3(grid_for(npix / 16, 8)), dim3(256), 0,
+                         st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
+                         a.N, a.H, a.W);
+    } else {
+      hipLaunchKernelGGL(conv_thin_out_f32_kernel<false>, dim3(grid_for(npix / 16, 8)), dim3(256), 0,
+                         st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
+                         a.N, a.H, a.W);
+    }
+    return check_launch("conv_thin_f32");
+  }
   MIA_DISPATCH_DTYPE(dtype, T, {
     if constexpr (sizeof(T) == 2) {
       if (a.Cin == 8) {
@@ -436,7 +686,7 @@ int launch_conv_thin(ConvK& k, int dtype, hipStream_t st) {
       return check_launch("conv_thin");
     }
   });
-  return set_error("conv_thin: 2-byte types only");
+  return set_error("conv_thin: unknown dtype");
 }
 
 }  // namespace mia

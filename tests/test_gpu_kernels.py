@@ -604,15 +604,19 @@ def test_fused_backward_front_epilogue(cuda, dtype, N, H, Cin, Cout, up):
     assert rel_err(sd2, sd1) < 1e-4
 
 
-@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 17, 16), (3, 16, 64)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 17, 16), (3, 16, 64), (9, 256, 256)])
 @pytest.mark.parametrize("thin", ["1", "0"])
 @pytest.mark.parametrize("e4e", [False, True])
 def test_conv_thin_vgg_input_layer(cuda, monkeypatch, dtype, N, H, W, thin, e4e):
     """VGG conv1_1 forward (8-channel padded image → 64, bias, ReLU) and its input gradient
     (64 → 8 channels, 3 real) on the thin-channel kernels (conv_thin.hip; MIA_CONV_THIN=0 = the
     implicit-GEMM tiles), against torch fp64 on the same rounded operands. e4e: the encoder's
-    input layer — bias + PReLU forward, gradient accumulated into an existing one (mia_conv2d)."""
+    input layer — bias + PReLU forward, gradient accumulated into an existing one (mia_conv2d).
+    fp32 runs on the VALU kernels (the padded channels skipped by their zero weights); 9 × 256²
+    pixels exceed one pass of their persistent grid."""
+    if (N, H, W) == (9, 256, 256) and dtype != torch.float32:
+        pytest.skip("the persistent-loop shape is checked for the fp32 VALU kernels")
     monkeypatch.setenv("MIA_CONV_THIN", thin)
     if e4e:
         return _thin_e4e_input_layer(cuda, dtype, N, H, W)

@@ -135,6 +135,8 @@ SIGNATURES = {
                            c_int, c_int, c_int, P]),
     "mia_conv_s2_dgrad_halo": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, c_int,
                                        P]),
+    "mia_conv_s2_dgrad_halo_multi": (c_int, [P, c_int, P, P, P, c_int, c_int, c_int, c_int, P, P,
+                                             c_int, c_int, P]),
     "mia_se_fwd": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
     "mia_se_apply": (c_int, [P, P, P, c_int, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_chan_dot": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P]),

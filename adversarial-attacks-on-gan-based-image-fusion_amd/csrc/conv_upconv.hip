@@ -57,6 +57,7 @@ __device__ __forceinline__ constexpr int up_phase(int st, int slot) {
   return st == 0 ? slot : st == 1 ? 2 + slot : st == 2 ? 2 * slot : st == 3 ? slot : (slot ? -1 : 0);
 }
 
+constexpr int UP_MAX_SRC = 8;
 struct UpK {
   const void* x;
   const void* w;  // packed [Cin/BK][5][2][Cout][BK]
@@ -65,6 +66,12 @@ struct UpK {
   const void* mask_a;       // DG: (N, 2R, 2R, Cout) or NULL
   const float* mask_slope;  // DG: [Cout] or NULL (→ 0)
   int N, R, Cin, Cout, act_in, nbn, nblk, accumulate;
+  // the input as nsrc tensors (N, R, R, cin_src) concatenated along channels (Cin = nsrc·cin_src):
+  // DG mode sums the input gradients of several stride-2 convs reading the same tensor (the e4e
+  // style heads on one FPN map) in one K loop; xs[0] = x otherwise
+  const void* xs[UP_MAX_SRC];
+  int cin_src;
+  const void* w_split;  // fp32: split_f32 of w (the split-once DG kernel), or NULL
 };
 
 template <typename T, bool PRO, bool DG>
@@ -99,11 +106,14 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
   const int hw = wid - BWAVES;
 
   // per-lane DMA sources: B-wave w owns weight rows (w·B_INS + j)·8 + lane/8 = slot·64 + channel;
-  // H-wave hw owns halo pieces hw + 2·j
+  // H-wave hw owns halo pieces hw + 2·j (element offsets into a source tensor, −1 → zero page)
+  const int csrc = k.cin_src, cbs = csrc / BK;  // channel blocks per source tensor
   const T* src[H_INS];
+  int hoff[H_INS];
 #pragma unroll
   for (int j = 0; j < H_INS; ++j) {
     src[j] = nullptr;
+    hoff[j] = -1;
     if (bwave) {
       if (j < B_INS) {
         const int row = (wid * B_INS + j) * 8 + (lane >> 3);
@@ -115,9 +125,10 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
       const int hy = hr / HSIDE, hx = hr - (hr / HSIDE) * HSIDE;
       const int y = y0 + hy - (DG ? 0 : 1), x = x0 + hx - (DG ? 0 : 1);
       if (hr < HROWS && y >= 0 && y < R && x >= 0 && x < R)
-        src[j] = X + ((size_t)(n * R + y) * R + x) * Cin + ((lane & 7) ^ fsw(hr)) * VEC;
+        hoff[j] = ((n * R + y) * R + x) * csrc + ((lane & 7) ^ fsw(hr)) * VEC;
     }
   }
+  (void)X;
   const int ncb = Cin / BK, nk = TL::NSTEP * ncb;
   const size_t wstep = (size_t)2 * Cout * BK;  // elements per K-step of the packed weights
 
@@ -129,7 +140,8 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
                                        (lptr_t)(dst + (wid * B_INS + j) * 1024), 16, 0, 0);
   };
   auto issue_h = [&](int cb, int j, int buf) {
-    const T* a = src[j] ? src[j] + cb * BK : zero;
+    const int sc = cb / cbs;  // source tensor of channel block cb (wave-uniform)
+    const T* a = hoff[j] >= 0 ? (const T*)k.xs[sc] + hoff[j] + (cb - sc * cbs) * BK : zero;
     __builtin_amdgcn_global_load_lds((gptr_t)a,
                                      (lptr_t)(hbuf + buf * HBUF + (hw + HWAVES * j) * 1024), 16,
                                      0, 0);
@@ -348,6 +360,7 @@ int launch_upconv_halo(const void* x, const void* w_up, void* t, int N, int R, i
   UpK k = {};
   k.x = x; k.w = w_up; k.t = t; k.style = style;
   k.N = N; k.R = R; k.Cin = Cin; k.Cout = Cout; k.act_in = act_in;
+  k.xs[0] = x; k.cin_src = Cin;
   const bool pro = style != nullptr || act_in != MIA_ACT_NONE;
   MIA_DISPATCH_DTYPE(dtype, T, {
     return pro ? launch_upconv_halo<T, true, false>(k, st)
@@ -356,35 +369,331 @@ int launch_upconv_halo(const void* x, const void* w_up, void* t, int N, int R, i
   return set_error("upconv_halo: unknown dtype");
 }
 
+// ---- fp32 stride-2 input gradient with the operands split once (bf16 matrix pipe) -------------
+// DG mode of the kernel above for fp32 (conv_common.h mfma_x6, as conv_halo_x6.hip): the packed
+// weights come pre-split from HBM (layouts.split_f32 of the packed tensor: per row of BK = 32 k a
+// 128-B [hi|mid] record, then a 64-B lo record), each 32-channel block of the g halo is split in LDS
+// once after its DMA lands ([hi|mid] in place + lo into an L buffer) and the main loop is ds_reads
+// + 3 MFMAs per fragment pair with no split VALU (the kernel above splits both operands per
+// fragment read: ≈ 145 TFLOP/s). Tile: a 16 × 16 patch of g × 64 output channels × the 4 output
+// phases, 8 waves (4 row waves of 4 patch rows × 2 column waves of 32 channels), one block per CU:
+// LDS = 2 halo buffers (2 × 37 KB, 17 × 17 pixels) + lo (18.5 KB) + a 2-stage pre-split weight ring
+// (2 × 24 KB: two phase slots × 64 channels) = 140 KB. DMA roles as conv_halo_x6.hip: waves 0–3
+// stream the weights one K-step ahead, waves 4–7 the next channel block's halo during steps 0–3;
+// the next block's split follows the last step of the current one. The prologue and epilogue are
+// not hidden behind a second block, so the kernel pays off on long K loops: the concatenated
+// first-conv input gradients of the e4e style heads (K = 9 × 7 × 512 for the 7 fine heads).
+struct DgX6 {
+  static constexpr int PH = 16, PW = 16, NW = 8, NT = 64 * NW;
+  static constexpr int WM = 4, WN = 2, FM = 4, FN = 2;
+  static constexpr int BN = WN * FN * 16, BK = 32;              // 64 output channels
+  static constexpr int HSIDE = PW + 1, HROWS = (PH + 1) * HSIDE;  // 289 halo pixels
+  static constexpr int HPIECES = (HROWS + 7) / 8;                 // 37 pieces of 8 rows
+  static constexpr int HBUF = HPIECES * 1024;
+  static constexpr int LROWB = 64, LBUF = HROWS * LROWB;
+  static constexpr int BROWS = 2 * BN;                            // two phase slots per K-step
+  static constexpr int BHM = BROWS * ROWB, BSTAGE = BHM + BROWS * LROWB;
+  static constexpr int BWAVES = 4, HWAVES = 4;
+  static constexpr int B_HM_INS = BROWS / 8 / BWAVES;             // 4 [hi|mid] pieces per B-wave
+  static constexpr int B_L_INS = BROWS / 16 / BWAVES;             // 2 lo pieces per B-wave
+  static constexpr int H_INS = (HPIECES + HWAVES - 1) / HWAVES;   // 10
+  static constexpr int HPS = (H_INS + 3) / 4;                     // issued over steps 0–3
+  static constexpr int NSTEP = 5;
+  static constexpr int LDS = 2 * HBUF + LBUF + 2 * BSTAGE;
+  static_assert(WM * FM == PH && WN * FN * 16 == BN, "");
+  static_assert(B_HM_INS * 8 * BWAVES == BROWS && B_L_INS * 16 * BWAVES == BROWS, "");
+  static_assert(LDS <= 160 * 1024, "");
+};
+
+__global__ __launch_bounds__(DgX6::NT, 1) void s2dg_x6_kernel(const UpK k) {
+  typedef DgX6 TL;
+  constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, BN = TL::BN, BK = TL::BK, NT = TL::NT;
+  constexpr int HSIDE = TL::HSIDE, HROWS = TL::HROWS, HPIECES = TL::HPIECES, HBUF = TL::HBUF;
+  constexpr int H_INS = TL::H_INS, HPS = TL::HPS, HWAVES = TL::HWAVES, BSTAGE = TL::BSTAGE;
+  constexpr int B_HM_INS = TL::B_HM_INS, B_L_INS = TL::B_L_INS;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const hbuf = smem;                  // 2 halo buffers: raw fp32, then [hi|mid] in place
+  char* const lbuf = smem + 2 * HBUF;       // lo of the current channel block
+  char* const bring = lbuf + TL::LBUF;      // 2 stages of pre-split weights: [hi|mid] rows, lo rows
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int R = k.R, Cin = k.Cin, Cout = k.Cout;
+  const int bl = xcd_remap(blockIdx.x, k.nblk);
+  const int mt = bl / k.nbn, n0 = (bl % k.nbn) * BN;
+  const int ptx = R / TL::PW, pty = R / TL::PH;
+  const int x0 = (mt % ptx) * TL::PW;
+  const int y0 = ((mt / ptx) % pty) * TL::PH;
+  const int n = mt / (ptx * pty);
+  const int ncb = Cin / BK, nk = TL::NSTEP * ncb;
+  const int csrc = k.cin_src, cbs = csrc / BK;
+  // packed rows: ((cb·5 + step)·2 + slot)·Cout + channel; [hi|mid] 128 B per row, then lo 64 B
+  const char* Whm = (const char*)k.w_split;
+  const char* Wl = Whm + (size_t)nk * 2 * Cout * ROWB;
+  const size_t hm_step = (size_t)2 * Cout * ROWB, l_step = (size_t)2 * Cout * TL::LROWB;
+  const char* zero = (const char*)g_zero16;
+  const bool bwave = wid < TL::BWAVES;
+  const int hw = wid - TL::BWAVES;
+
+  // per-lane DMA sources: B-waves byte offsets of their weight pieces within a K-step's rows;
+  // H-waves element offsets of their halo pieces in a source tensor (−1 → zero page)
+  constexpr int NSRC = H_INS > B_HM_INS + B_L_INS ? H_INS : B_HM_INS + B_L_INS;
+  int off[NSRC];  // (< 2^31: checked at the API)
+#pragma unroll
+  for (int j = 0; j < NSRC; ++j) {
+    off[j] = -1;
+    if (bwave) {
+      if (j < B_HM_INS) {
+        const int row = (wid * B_HM_INS + j) * 8 + (lane >> 3);
+        const int slot = row / BN, c = n0 + row % BN;
+        off[j] = (slot * Cout + c) * ROWB + ((lane & 7) ^ fsw(row)) * 16;
+      } else if (j < B_HM_INS + B_L_INS) {
+        const int row = (wid * B_L_INS + j - B_HM_INS) * 16 + (lane >> 2);
+        const int slot = row / BN, c = n0 + row % BN;
+        off[j] = (slot * Cout + c) * TL::LROWB + ((lane & 3) ^ (lsw(row) >> 1)) * 16;
+      }
+    } else if (j < H_INS) {
+      const int hr = (hw + HWAVES * j) * 8 + (lane >> 3);
+      const int hy = hr / HSIDE, hx = hr - (hr / HSIDE) * HSIDE;
+      const int y = y0 + hy, x = x0 + hx;
+      if (hr < HROWS && y < R && x < R)
+        off[j] = ((n * R + y) * R + x) * csrc + ((lane & 7) ^ fsw(hr)) * 4;
+    }
+  }
+
+  // (the offsets pass through an opaque copy at each use: hoisted out of the loops, the 64-bit
+  // per-lane addresses spill)
+  auto opaque = [](int v) __attribute__((always_inline)) {
+    asm volatile("" : "+v"(v));
+    return v;
+  };
+  auto issue_b = [&](int s, int stg) {
+    char* dst = bring + stg * BSTAGE;
+    const char* hm = Whm + s * hm_step;
+    const char* lo = Wl + s * l_step;
+#pragma unroll
+    for (int j = 0; j < B_HM_INS; ++j)
+      __builtin_amdgcn_global_load_lds((gptr_t)(hm + opaque(off[j])),
+                                       (lptr_t)(dst + (wid * B_HM_INS + j) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < B_L_INS; ++j)
+      __builtin_amdgcn_global_load_lds((gptr_t)(lo + opaque(off[B_HM_INS + j])),
+                                       (lptr_t)(dst + TL::BHM + (wid * B_L_INS + j) * 1024), 16,
+                                       0, 0);
+  };
+  auto issue_h = [&](int cb, int j, int buf) {
+    const int sc = cb / cbs;  // source tensor of channel block cb (wave-uniform)
+    const float* xb = (const float*)k.xs[sc] + (cb - sc * cbs) * BK;
+    const int o = opaque(off[j]);
+    const char* a = o >= 0 ? (const char*)(xb + o) : zero;
+    __builtin_amdgcn_global_load_lds((gptr_t)a,
+                                     (lptr_t)(hbuf + buf * HBUF + (hw + HWAVES * j) * 1024), 16,
+                                     0, 0);
+  };
+  auto convert = [&](int buf) {  // split the landed raw halo in place + lo into lbuf
+    char* hb = hbuf + buf * HBUF;
+    for (int c = tid; c < HROWS * 8; c += NT) {
+      const int hr = c >> 3, pc = c & 7, lc = pc ^ fsw(hr);
+      const f32x4 v = *(const f32x4*)(hb + hr * ROWB + pc * 16);
+      u32x4 hm;
+      u32x2 lo;
+      split_quad(v, hm, lo);
+      *(u32x4*)(hb + hr * ROWB + pc * 16) = hm;
+      *(u32x2*)(lbuf + hr * TL::LROWB + ((lc ^ lsw(hr)) << 3)) = lo;
+    }
+  };
+
+  if (bwave) {
+    issue_b(0, 0);
+  } else {
+#pragma unroll
+    for (int j = 0; j < H_INS; ++j)
+      if (hw + HWAVES * j < HPIECES) issue_h(0, j, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  convert(0);
+  __syncthreads();
+
+  f32x4 acc[4][FM][FN];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[q][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int cb = 0; cb < ncb; ++cb) {
+    const char* ha = hbuf + (cb & 1) * HBUF;
+#pragma unroll
+    for (int st = 0; st < TL::NSTEP; ++st) {
+      const int ln = opaque(lane);  // the fragment addresses are recomputed per K-step
+      const int frow = ln & 15, fq = ln >> 4;
+      const int s = cb * TL::NSTEP + st;
+      const char* sb = bring + (s & 1) * BSTAGE;
+      if (bwave && s + 1 < nk) issue_b(s + 1, (s & 1) ^ 1);
+      const int jy = up_jy(st), jx = up_jx(st);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ch = h * 4 + fq;  // this lane's logical 16-B quad of the K-step
+        u32x4 ahm[FM];
+        u32x2 al[FM];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int hr = (wm * FM + i + jy) * HSIDE + frow + jx;
+          ahm[i] = *(const u32x4*)(ha + hr * ROWB + ((ch ^ fsw(hr)) << 4));
+          al[i] = *(const u32x2*)(lbuf + hr * TL::LROWB + ((ch ^ lsw(hr)) << 3));
+        }
+#pragma unroll
+        for (int slot = 0; slot < 2; ++slot) {
+          const int ph = up_phase(st, slot);
+          if (ph < 0) continue;
+          u32x4 bhm[FN];
+          u32x2 blo[FN];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int row = slot * BN + wn * FN * 16 + 16 * j + frow;
+            bhm[j] = *(const u32x4*)(sb + row * ROWB + ((ch ^ fsw(row)) << 4));
+            blo[j] = *(const u32x2*)(sb + TL::BHM + row * TL::LROWB + ((ch ^ lsw(row)) << 3));
+          }
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)  // D[channel][pixel]
+              acc[ph][i][j] = mfma_x6(bhm[j], blo[j], ahm[i], al[i], acc[ph][i][j]);
+        }
+        if (h == 0 && !bwave && st < 4 && cb + 1 < ncb) {
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int q = 0; q < HPS; ++q) {
+            const int j = st * HPS + q;
+            if (j < H_INS && hw + HWAVES * j < HPIECES) issue_h(cb + 1, j, (cb + 1) & 1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      // B-wave: step s+1's weights landed; H-wave: the next block's halo before the split
+      if (bwave || st == TL::NSTEP - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS reads of the step done
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (st == TL::NSTEP - 1 && cb + 1 < ncb) {  // every wave is past its last read of lbuf
+        convert((cb + 1) & 1);
+        __syncthreads();
+      }
+    }
+  }
+
+  // epilogue: phase (py, px) of g position (y, x) → gx(2y + 1 − py, 2x + 1 − px); lane (frow, fq)
+  // holds channels 4·fq … 4·fq+3 of fragment j for pixel x0 + frow
+  const int frow = lane & 15, fq = lane >> 4;
+  float* __restrict__ Y = (float*)k.t;
+  const int TS = 2 * R;
+  float msl[FN][4];  // slope of the mask per channel of this lane
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      msl[j][e] = k.mask_slope ? k.mask_slope[n0 + wn * FN * 16 + 16 * j + 4 * fq + e] : 0.f;
+#pragma unroll
+  for (int ph = 0; ph < 4; ++ph) {
+    const int py = ph >> 1, px = ph & 1;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int ty = 2 * (y0 + wm * FM + i) + 1 - py;
+      const int tx = 2 * (x0 + frow) + 1 - px;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = n0 + wn * FN * 16 + 16 * j + 4 * fq;
+        const size_t o = ((size_t)(n * TS + ty) * TS + tx) * Cout + c;
+        f32x4 v = acc[ph][i][j];
+        if (k.mask_a) {
+          const f32x4 m = *(const f32x4*)((const float*)k.mask_a + o);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = m[e] > 0.f ? v[e] : msl[j][e] * v[e];
+        }
+        if (k.accumulate) {
+          const f32x4 a = *(const f32x4*)(Y + o);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += a[e];
+        }
+        *(f32x4*)(Y + o) = v;
+      }
+    }
+  }
+}
+
+static int launch_s2dg_x6(UpK& k, hipStream_t st) {
+  typedef DgX6 TL;
+  k.nbn = k.Cout / TL::BN;
+  k.nblk = k.N * (k.R / TL::PH) * (k.R / TL::PW) * k.nbn;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)s2dg_x6_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(s2dg_x6_kernel, dim3(k.nblk), dim3(TL::NT), TL::LDS, st, k);
+  return check_launch("s2dg_x6");
+}
+
+// the split-once kernel: fp32 with pre-split weights, R % 16 == 0, Cx % 64 == 0, and a K loop of
+// at least MIA_S2DG_X6_MINCIN input channels (default 1024: the concatenated head gradients;
+// 0 disables — A/B switch, read per launch)
+static bool s2dg_x6_ok(const UpK& k, int dtype) {
+#ifdef MIA_F32_NATIVE
+  (void)k;
+  (void)dtype;
+  return false;
+#else
+  const char* e = getenv("MIA_S2DG_X6_MINCIN");
+  const int minc = e ? atoi(e) : 1024;
+  return dtype == MIA_F32 && k.w_split && minc > 0 && k.Cin >= minc && k.R % DgX6::PH == 0 &&
+         k.Cout % DgX6::BN == 0 && k.cin_src % DgX6::BK == 0;
+#endif
+}
+
 bool s2_dgrad_halo_eligible(int dtype, int R, int Cg, int Cx) {
   const char* e = getenv("MIA_S2DG_HALO");  // tuning / A-B switch: 0 = generic phase GEMMs
   if (e && atoi(e) == 0) return false;
+  (void)dtype;
   return R % 16 == 0 && Cg % 64 == 0 && Cx % HaloUp::BN == 0 &&
          (int64_t)4 * R * R < (1LL << 31);
-}
-
-int launch_s2_dgrad_halo(const void* g, const void* w, void* gx, int N, int R, int Cg, int Cx,
-                         const void* mask_a, const float* mask_slope, int accumulate, int dtype,
-                         hipStream_t st) {
-  UpK k = {};
-  k.x = g; k.w = w; k.t = gx; k.mask_a = mask_a; k.mask_slope = mask_slope;
-  k.N = N; k.R = R; k.Cin = Cg; k.Cout = Cx; k.accumulate = accumulate;
-  MIA_DISPATCH_DTYPE(dtype, T, return launch_upconv_halo<T, false, true>(k, st));
-  return set_error("s2_dgrad_halo: unknown dtype");
 }
 
 }  // namespace mia
 
 using namespace mia;
 
-extern "C" int mia_conv_s2_dgrad_halo(const void* g, const void* w_halo, void* gx, int N, int R,
-                                      int Cg, int Cx, const void* mask_a, const float* mask_slope,
-                                      int accumulate, int dtype, void* stream) {
-  MIA_CHECK_ARG(g && w_halo && gx && N > 0, "bad args");
+extern "C" int mia_conv_s2_dgrad_halo_multi(const void* const* g, int ng, const void* w_halo,
+                                            const void* w_split, void* gx, int N, int R, int Cg,
+                                            int Cx, const void* mask_a, const float* mask_slope,
+                                            int accumulate, int dtype, void* stream) {
+  MIA_CHECK_ARG(g && ng >= 1 && ng <= UP_MAX_SRC && w_halo && gx && N > 0, "bad args");
+  for (int i = 0; i < ng; ++i) MIA_CHECK_ARG(g[i], "null source tensor");
   MIA_CHECK_ARG(s2_dgrad_halo_eligible(dtype, R, Cg, Cx),
                 "needs R % 16 == 0, Cg % 64 == 0, Cx % 64 == 0 "
                 "(use mia_conv2d phase groups otherwise)");
   MIA_CHECK_ARG((int64_t)N * R * R * Cg < (1LL << 31), "input too large for 32-bit offsets");
-  return launch_s2_dgrad_halo(g, w_halo, gx, N, R, Cg, Cx, mask_a, mask_slope, accumulate, dtype,
-                              (hipStream_t)stream);
+  UpK k = {};
+  k.x = g[0]; k.w = w_halo; k.t = gx; k.mask_a = mask_a; k.mask_slope = mask_slope;
+  k.N = N; k.R = R; k.Cin = ng * Cg; k.Cout = Cx; k.accumulate = accumulate;
+  for (int i = 0; i < ng; ++i) k.xs[i] = g[i];
+  k.cin_src = Cg;
+  k.w_split = w_split;
+  if (s2dg_x6_ok(k, dtype)) return launch_s2dg_x6(k, (hipStream_t)stream);
+  MIA_DISPATCH_DTYPE(dtype, T, return launch_upconv_halo<T, false, true>(k, (hipStream_t)stream));
+  return set_error("s2_dgrad_halo: unknown dtype");
+}
+
+
+extern "C" int mia_conv_s2_dgrad_halo(const void* g, const void* w_halo, void* gx, int N, int R,
+                                      int Cg, int Cx, const void* mask_a, const float* mask_slope,
+                                      int accumulate, int dtype, void* stream) {
+  const void* gs[1] = {g};
+  return mia_conv_s2_dgrad_halo_multi(gs, 1, w_halo, nullptr, gx, N, R, Cg, Cx, mask_a,
+                                      mask_slope, accumulate, dtype, stream);
 }

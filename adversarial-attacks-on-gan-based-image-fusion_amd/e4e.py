@@ -161,6 +161,16 @@ class E4EEncoder:
             self.heads.append(dict(convs=convs, src=src,
                                    lw=dd(p[f"styles.{i}.linear.weight"].double() * inv),
                                    lb=dd(p[f"styles.{i}.linear.bias"])))
+        # the heads whose first conv reads the same FPN map (7 on p1, 4 on p2): their first-conv
+        # input gradients run as ONE multi-source launch with the packed matrices concatenated
+        # along K (mia_conv_s2_dgrad_halo_multi) — one write of the source gradient instead of
+        # one accumulate per head
+        self.src_heads = {}
+        for src in ("c3", "p2", "p1"):
+            idx = [i for i, hd in enumerate(self.heads) if hd["src"] == src]
+            if len(idx) > 1 and all(self.heads[i]["convs"][0]["wdh"] is not None for i in idx):
+                self.src_heads[src] = (idx, torch.cat([self.heads[i]["convs"][0]["wdh"]
+                                                       for i in idx]).contiguous())
         # w = w0 + delta_i: the linear biases of rows i ≥ 1 include style 0's; the backward of
         # style 0 reads the sum of every row (mia_sum_slices)
         b0l = self.heads[0]["lb"]
@@ -367,8 +377,17 @@ class E4EEncoder:
                 heads_g[i], heads_ev[i] = g, st.record_event()
         src_stream = {src: side[k % len(side)] for k, src in enumerate(("c3", "p2", "p1"))}
         seen = set()
+        for src, (idx, wcat) in self.src_heads.items():
+            st = src_stream[src]
+            for i in idx:
+                st.wait_event(heads_ev[i])
+            with torch.cuda.stream(st):
+                ops.s2_dgrad_halo([heads_g[i] for i in idx], wcat, gfeat[src])
+            seen.add(src)
         for i in reversed(range(self.n_latent)):
             hd = self.heads[i]
+            if hd["src"] in self.src_heads:
+                continue
             st = src_stream[hd["src"]]
             st.wait_event(heads_ev[i])
             with torch.cuda.stream(st):

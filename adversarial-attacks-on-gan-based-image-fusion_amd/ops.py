@@ -148,7 +148,8 @@ def _prof_call(name, flops, *args):
     if prof is not None:
         e1.record()
         prof.append((e0, e1, flops))
-        _tag(f"{name} {args[4:7] if name != 'mia_conv_s2_dgrad_halo' else ''}")
+        _tag(f"{name} " + (f"R{args[6]} x{args[1]}" if name == "mia_conv_s2_dgrad_halo_multi"
+                             else f"{args[4:7]}"))
 
 
 def upconv_kpad(cin, phase, dtype):
@@ -830,23 +831,33 @@ def cast(x, y, scale=1.0):
 
 
 def s2_dgrad_halo(g, w_halo, gx, mask_a=None, mask_slope=None, accumulate=False, flops=None):
-    """mia_conv_s2_dgrad_halo: gx (N,2R,2R,Cx) ← input gradient of a stride-2 3×3 conv from
-    g (N,R,R,Cg) (+ slope mask, + accumulate)."""
-    N, R, R2, Cg = g.shape
+    """mia_conv_s2_dgrad_halo(_multi): gx (N,2R,2R,Cx) ← input gradient of a stride-2 3×3 conv from
+    g (N,R,R,Cg) (+ slope mask, + accumulate). ``g`` may be a list of up to 8 output gradients of
+    convs reading the same tensor, with ``w_halo`` their packed matrices concatenated along dim 0:
+    the sum of their input gradients in one K loop. fp32 passes the split_f32 copy of w_halo (the
+    split-once kernel takes long K loops)."""
+    gs = list(g) if isinstance(g, (list, tuple)) else [g]
+    if not 1 <= len(gs) <= 8:
+        raise ValueError("s2_dgrad_halo: 1..8 source gradients")
+    N, R, R2, Cg = gs[0].shape
+    for t in gs[1:]:
+        _need(t, gs[0].shape, gs[0].dtype, "g[i]")
     Cx = gx.shape[-1]
-    T = g.dtype
+    T = gs[0].dtype
     if R != R2:
         raise ValueError("square inputs only")
     bk = layouts.halo_bk(T)
-    _need(w_halo, (Cg // bk, 5, 2, Cx, bk), T, "w_halo")
+    _need(w_halo, (len(gs) * Cg // bk, 5, 2, Cx, bk), T, "w_halo")
     _need(gx, (N, 2 * R, 2 * R, Cx), T, "gx")
     if mask_a is not None:
         _need(mask_a, gx.shape, T, "mask_a")
     _numel_ok(mask_slope, Cx, torch.float32, "mask_slope")
-    _prof_call("mia_conv_s2_dgrad_halo",
-               flops if flops is not None else 2 * N * R * R * 9 * Cg * Cx,
-               ptr(g), ptr(w_halo), ptr(gx), N, R, Cg, Cx, ptr(mask_a), ptr(mask_slope),
-               int(bool(accumulate)), dt(T), stream())
+    gp = (ctypes.c_void_p * len(gs))(*[ptr(t).value for t in gs])
+    ws = layouts.split_for(w_halo) if T == torch.float32 else None
+    _prof_call("mia_conv_s2_dgrad_halo_multi",
+               flops if flops is not None else 2 * N * R * R * 9 * len(gs) * Cg * Cx,
+               gp, len(gs), ptr(w_halo), ptr(ws), ptr(gx), N, R, Cg, Cx, ptr(mask_a),
+               ptr(mask_slope), int(bool(accumulate)), dt(T), stream())
     return gx
 
 

@@ -119,13 +119,24 @@ int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream);
  * 1×1 stride-1/2 (FPN lateral, shortcut), and the 4-phase sub-pixel adjoint of a stride-2 conv.
  */
 /* Input gradient of a stride-2, pad-1 3×3 conv as ONE halo-tiled launch (the halo up-conv kernel
- * mirrored; fp16/bf16, R % 16 == 0, Cg % 64 == 0, Cx % 64 == 0): g (N,R,R,Cg) → gx (N,2R,2R,Cx),
+ * mirrored; R % 16 == 0, Cg % 64 == 0, Cx % 64 == 0): g (N,R,R,Cg) → gx (N,2R,2R,Cx),
  * gx = mask(Σ ...) (+ gx if accumulate), mask as mia_conv_args.mask_a / mask_slope.
- * w_halo = layouts.s2_dgrad_halo_matrix(W): [Cg/64][5][2][Cx][64]. Replaces the same e4e strided
+ * w_halo = layouts.s2_dgrad_halo_matrix(W): [Cg/BK][5][2][Cx][BK] (BK = 64, fp32 32). Replaces the same e4e strided
  * conv backward as the mia_conv2d phase groups (bottleneck conv2, GradualStyleBlock convs). */
 int mia_conv_s2_dgrad_halo(const void* g, const void* w_halo, void* gx, int N, int R, int Cg,
                            int Cx, const void* mask_a, const float* mask_slope, int accumulate,
                            int dtype, void* stream);
+/* The summed input gradients of ng ≤ 8 stride-2 3×3 convs that read the same tensor (the e4e
+ * GradualStyleBlocks whose first conv reads one FPN map: 7 heads on p1, 4 on p2, psp_encoders
+ * GradualStyleBlock.forward, reached through net.encoder at code/attack/attack_main2.py:597,622)
+ * as ONE K loop: g[i] (N,R,R,Cg) are the convs' output gradients, w_halo the heads' packed
+ * matrices concatenated along the first dimension ([ng·Cg/BK][5][2][Cx][BK]); gx as
+ * mia_conv_s2_dgrad_halo (the sum, masked, + gx if accumulate). w_split (fp32 only, optional):
+ * layouts.split_f32(w_halo) — with ng·Cg ≥ 1024 the split-once fp32 kernel runs. */
+int mia_conv_s2_dgrad_halo_multi(const void* const* g, int ng, const void* w_halo,
+                                 const void* w_split, void* gx, int N, int R, int Cg, int Cx,
+                                 const void* mask_a, const float* mask_slope, int accumulate,
+                                 int dtype, void* stream);
 
 typedef struct mia_conv_group {
   const void* w;

@@ -98,6 +98,39 @@ def test_s2_dgrad_halo_vs_autograd(cuda, dtype, R, cg, cx):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("N,R,ng,cg,cx", [(1, 32, 7, 512, 512), (2, 16, 2, 512, 128),
+                                          (2, 16, 3, 64, 64), (1, 16, 4, 256, 192)])
+@pytest.mark.parametrize("mask", [False, True])
+@pytest.mark.parametrize("x6", ["1024", "0"])
+def test_s2_dgrad_halo_multi_source(cuda, monkeypatch, dtype, N, R, ng, cg, cx, mask, x6):
+    """mia_conv_s2_dgrad_halo_multi: the summed input gradients of ng stride-2 convs reading the
+    same tensor (the e4e style heads on one FPN map) in one K loop, vs autograd of the sum. fp32
+    with ng·Cg ≥ 1024 runs the split-once kernel (MIA_S2DG_X6_MINCIN=1024, the default; 0 = the
+    on-the-fly split kernel); the 7 × 512 case is the fine heads' shape at batch 1."""
+    monkeypatch.setenv("MIA_S2DG_X6_MINCIN", x6)
+    ws = [rnd((cg, cx, 3, 3), 80 + i, math.sqrt(2 / (9 * cx))) for i in range(ng)]
+    gs = [rnd((N, cg, R, R), 90 + i) for i in range(ng)]
+    a_below = rnd((N, cx, 2 * R, 2 * R), 98)
+    base = rnd((N, cx, 2 * R, 2 * R), 99)
+    sl = torch.full((cx,), 0.25, device=cuda)
+    xx = torch.zeros(N, cx, 2 * R, 2 * R, dtype=torch.float64, requires_grad=True)
+    loss = sum((F.conv2d(xx, w.to(dtype).double(), stride=2, padding=1) * g.to(dtype).double()).sum()
+               for w, g in zip(ws, gs))
+    (gref,) = torch.autograd.grad(loss, xx)
+    if mask:
+        gref = torch.where(a_below.to(dtype).double() > 0, gref, 0.25 * gref)
+    gref = gref + base.to(dtype).double()
+    wcat = torch.cat([layouts.s2_dgrad_halo_matrix(w, dtype) for w in ws]).to(cuda)
+    gx = nhwc(base, dtype, cuda)
+    ops.s2_dgrad_halo([nhwc(g, dtype, cuda) for g in gs], wcat, gx,
+                      mask_a=nhwc(a_below, dtype, cuda) if mask else None,
+                      mask_slope=sl if mask else None, accumulate=True)
+    torch.cuda.synchronize()
+    tol = {torch.float32: 2e-5, torch.float16: 2e-2}[dtype]
+    assert rel_err(nchw(gx), gref) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 def test_conv2d_1x1_stride2_and_placed_adjoint(cuda, dtype):
     N, H, cin, cout = 2, 32, 64, 128
     x = rnd((N, cin, H, H), 6)

@@ -79,6 +79,8 @@ SIGNATURES = {
     "mia_upconv_kpad": (c_int, [c_int, c_int, c_int]),
     "mia_upconv_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, P]),
     "mia_upconv_fwd_halo": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, P]),
+    "mia_upconv_fwd_halo_split": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int,
+                                          P]),
     "mia_upconv_blur_fwd": (c_int, [P, P, P, P, c_float, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_upconv_blur_bwd": (c_int, [P, P, c_int, c_int, c_int, c_int, P]),
     "mia_upconv_dgrad": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, c_int, P, P, c_int,

@@ -550,8 +550,9 @@ bool conv_halo_eligible(const ConvK& k, int dtype);
 int launch_conv_halo(ConvK& k, int dtype, hipStream_t st);
 // up-sampling StyledConv forward, halo-tiled interior (conv_upconv.hip)
 bool upconv_halo_eligible(int dtype, int R, int Cin, int Cout);
-int launch_upconv_halo(const void* x, const void* w_up, void* t, int N, int R, int Cin, int Cout,
-                       int act_in, const float* style, int dtype, hipStream_t st);
+int launch_upconv_halo(const void* x, const void* w_up, const void* w_up_split, void* t, int N,
+                       int R, int Cin, int Cout, int act_in, const float* style, int dtype,
+                       hipStream_t st);
 // 64 → 64-channel stride-1 layers, weights resident in VGPRs, persistent (conv_wres.hip)
 bool conv_wres_eligible(const ConvK& k, int dtype);
 int launch_conv_wres(ConvK& k, int dtype, hipStream_t st);

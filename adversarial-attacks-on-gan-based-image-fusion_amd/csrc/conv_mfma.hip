@@ -608,12 +608,20 @@ extern "C" int mia_upconv_fwd(const void* x, const void* const* w_phase, void* t
 extern "C" int mia_upconv_fwd_halo(const void* x, const void* const* w_phase, const void* w_up,
                                    void* t_out, int N, int R, int Cin, int Cout, int act_in,
                                    const float* style, int dtype, void* stream) {
+  return mia_upconv_fwd_halo_split(x, w_phase, w_up, nullptr, t_out, N, R, Cin, Cout, act_in, style,
+                                   dtype, stream);
+}
+
+extern "C" int mia_upconv_fwd_halo_split(const void* x, const void* const* w_phase,
+                                         const void* w_up, const void* w_up_split, void* t_out,
+                                         int N, int R, int Cin, int Cout, int act_in,
+                                         const float* style, int dtype, void* stream) {
   if (!w_up || !upconv_halo_eligible(dtype, R, Cin, Cout))
     return mia_upconv_fwd(x, w_phase, t_out, N, R, Cin, Cout, act_in, style, dtype, stream);
   MIA_CHECK_ARG(x && w_phase && t_out && N > 0 && Cout % 8 == 0, "bad args");
   MIA_CHECK_ARG((int64_t)N * R * R * Cin < (1LL << 31), "input too large for 32-bit offsets");
-  const int rc = launch_upconv_halo(x, w_up, t_out, N, R, Cin, Cout, act_in, style, dtype,
-                                    (hipStream_t)stream);
+  const int rc = launch_upconv_halo(x, w_up, w_up_split, t_out, N, R, Cin, Cout, act_in, style,
+                                    dtype, (hipStream_t)stream);
   if (rc) return rc;
   // the last row / column of the even phase grids (y = R or x = R): four one-row / one-column
   // groups on the generic kernel; the group's input window starts at R − 1 (pad = 1 − R) and its

@@ -74,6 +74,15 @@ struct UpK {
   const void* w_split;  // fp32: split_f32 of w (the split-once DG kernel), or NULL
 };
 
+// k.xs[i] for a wave-uniform i as a select chain over constant indices (a dynamic index into the
+// by-value kernel argument would copy the array to scratch)
+__device__ __forceinline__ const char* up_src(const UpK& k, int i) {
+  const void* p = k.xs[0];
+#pragma unroll
+  for (int j = 1; j < UP_MAX_SRC; ++j) p = i == j ? k.xs[j] : p;
+  return (const char*)p;
+}
+
 template <typename T, bool PRO, bool DG>
 __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
   typedef HaloUp TL;
@@ -106,14 +115,12 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
   const int hw = wid - BWAVES;
 
   // per-lane DMA sources: B-wave w owns weight rows (w·B_INS + j)·8 + lane/8 = slot·64 + channel;
-  // H-wave hw owns halo pieces hw + 2·j (element offsets into a source tensor, −1 → zero page)
+  // H-wave hw owns halo pieces hw + 2·j (in source tensor 0; another source is a uniform delta)
   const int csrc = k.cin_src, cbs = csrc / BK;  // channel blocks per source tensor
   const T* src[H_INS];
-  int hoff[H_INS];
 #pragma unroll
   for (int j = 0; j < H_INS; ++j) {
     src[j] = nullptr;
-    hoff[j] = -1;
     if (bwave) {
       if (j < B_INS) {
         const int row = (wid * B_INS + j) * 8 + (lane >> 3);
@@ -125,10 +132,9 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
       const int hy = hr / HSIDE, hx = hr - (hr / HSIDE) * HSIDE;
       const int y = y0 + hy - (DG ? 0 : 1), x = x0 + hx - (DG ? 0 : 1);
       if (hr < HROWS && y >= 0 && y < R && x >= 0 && x < R)
-        hoff[j] = ((n * R + y) * R + x) * csrc + ((lane & 7) ^ fsw(hr)) * VEC;
+        src[j] = X + ((size_t)(n * R + y) * R + x) * csrc + ((lane & 7) ^ fsw(hr)) * VEC;
     }
   }
-  (void)X;
   const int ncb = Cin / BK, nk = TL::NSTEP * ncb;
   const size_t wstep = (size_t)2 * Cout * BK;  // elements per K-step of the packed weights
 
@@ -140,8 +146,16 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
                                        (lptr_t)(dst + (wid * B_INS + j) * 1024), 16, 0, 0);
   };
   auto issue_h = [&](int cb, int j, int buf) {
+    if constexpr (!DG) {  // one source tensor
+      const T* a = src[j] ? src[j] + cb * BK : zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)a,
+                                       (lptr_t)(hbuf + buf * HBUF + (hw + HWAVES * j) * 1024), 16,
+                                       0, 0);
+      return;
+    }
     const int sc = cb / cbs;  // source tensor of channel block cb (wave-uniform)
-    const T* a = hoff[j] >= 0 ? (const T*)k.xs[sc] + hoff[j] + (cb - sc * cbs) * BK : zero;
+    const int64_t delta = up_src(k, sc) - (const char*)X;
+    const T* a = src[j] ? (const T*)((const char*)(src[j] + (cb - sc * cbs) * BK) + delta) : zero;
     __builtin_amdgcn_global_load_lds((gptr_t)a,
                                      (lptr_t)(hbuf + buf * HBUF + (hw + HWAVES * j) * 1024), 16,
                                      0, 0);
@@ -355,13 +369,21 @@ bool upconv_halo_eligible(int dtype, int R, int Cin, int Cout) {
          (int64_t)(2 * R + 1) * (2 * R + 1) < (1LL << 31);
 }
 
-int launch_upconv_halo(const void* x, const void* w_up, void* t, int N, int R, int Cin, int Cout,
-                       int act_in, const float* style, int dtype, hipStream_t st) {
+template <bool DG, bool PRO>
+static int launch_upconv_x6(UpK& k, hipStream_t st);
+static bool upconv_x6_ok(const UpK& k, int dtype);
+
+int launch_upconv_halo(const void* x, const void* w_up, const void* w_up_split, void* t, int N,
+                       int R, int Cin, int Cout, int act_in, const float* style, int dtype,
+                       hipStream_t st) {
   UpK k = {};
   k.x = x; k.w = w_up; k.t = t; k.style = style;
   k.N = N; k.R = R; k.Cin = Cin; k.Cout = Cout; k.act_in = act_in;
   k.xs[0] = x; k.cin_src = Cin;
+  k.w_split = w_up_split;
   const bool pro = style != nullptr || act_in != MIA_ACT_NONE;
+  if (upconv_x6_ok(k, dtype))
+    return pro ? launch_upconv_x6<false, true>(k, st) : launch_upconv_x6<false, false>(k, st);
   MIA_DISPATCH_DTYPE(dtype, T, {
     return pro ? launch_upconv_halo<T, true, false>(k, st)
                : launch_upconv_halo<T, false, false>(k, st);
@@ -381,8 +403,8 @@ int launch_upconv_halo(const void* x, const void* w_up, void* t, int N, int R, i
 // (2 × 24 KB: two phase slots × 64 channels) = 140 KB. DMA roles as conv_halo_x6.hip: waves 0–3
 // stream the weights one K-step ahead, waves 4–7 the next channel block's halo during steps 0–3;
 // the next block's split follows the last step of the current one. The prologue and epilogue are
-// not hidden behind a second block, so the kernel pays off on long K loops: the concatenated
-// first-conv input gradients of the e4e style heads (K = 9 × 7 × 512 for the 7 fine heads).
+// not hidden behind a second block; the longest K loops gain most: the concatenated first-conv
+// input gradients of the e4e style heads (K = 9 × 7 × 512 for the 7 fine heads).
 struct DgX6 {
   static constexpr int PH = 16, PW = 16, NW = 8, NT = 64 * NW;
   static constexpr int WM = 4, WN = 2, FM = 4, FN = 2;
@@ -405,7 +427,8 @@ struct DgX6 {
   static_assert(LDS <= 160 * 1024, "");
 };
 
-__global__ __launch_bounds__(DgX6::NT, 1) void s2dg_x6_kernel(const UpK k) {
+template <bool DG, bool PRO>
+__global__ __launch_bounds__(DgX6::NT, 1) void upconv_x6_kernel(const UpK k) {
   typedef DgX6 TL;
   constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, BN = TL::BN, BK = TL::BK, NT = TL::NT;
   constexpr int HSIDE = TL::HSIDE, HROWS = TL::HROWS, HPIECES = TL::HPIECES, HBUF = TL::HBUF;
@@ -457,8 +480,8 @@ __global__ __launch_bounds__(DgX6::NT, 1) void s2dg_x6_kernel(const UpK k) {
     } else if (j < H_INS) {
       const int hr = (hw + HWAVES * j) * 8 + (lane >> 3);
       const int hy = hr / HSIDE, hx = hr - (hr / HSIDE) * HSIDE;
-      const int y = y0 + hy, x = x0 + hx;
-      if (hr < HROWS && y < R && x < R)
+      const int y = y0 + hy - (DG ? 0 : 1), x = x0 + hx - (DG ? 0 : 1);
+      if (hr < HROWS && y >= 0 && y < R && x >= 0 && x < R)
         off[j] = ((n * R + y) * R + x) * csrc + ((lane & 7) ^ fsw(hr)) * 4;
     }
   }
@@ -485,18 +508,32 @@ __global__ __launch_bounds__(DgX6::NT, 1) void s2dg_x6_kernel(const UpK k) {
   };
   auto issue_h = [&](int cb, int j, int buf) {
     const int sc = cb / cbs;  // source tensor of channel block cb (wave-uniform)
-    const float* xb = (const float*)k.xs[sc] + (cb - sc * cbs) * BK;
+    const float* xb = (const float*)up_src(k, sc) + (cb - sc * cbs) * BK;
     const int o = opaque(off[j]);
     const char* a = o >= 0 ? (const char*)(xb + o) : zero;
     __builtin_amdgcn_global_load_lds((gptr_t)a,
                                      (lptr_t)(hbuf + buf * HBUF + (hw + HWAVES * j) * 1024), 16,
                                      0, 0);
   };
-  auto convert = [&](int buf) {  // split the landed raw halo in place + lo into lbuf
-    char* hb = hbuf + buf * HBUF;
+  // split the landed raw halo of channel block cb in place + lo into lbuf (PRO: x̃ = act(x)·s
+  // first, rounded as the on-the-fly path)
+  const bool lrelu_in = k.act_in == MIA_ACT_LRELU_S2;
+  auto convert = [&](int cb) {
+    char* hb = hbuf + (cb & 1) * HBUF;
     for (int c = tid; c < HROWS * 8; c += NT) {
       const int hr = c >> 3, pc = c & 7, lc = pc ^ fsw(hr);
-      const f32x4 v = *(const f32x4*)(hb + hr * ROWB + pc * 16);
+      f32x4 v = *(const f32x4*)(hb + hr * ROWB + pc * 16);
+      if constexpr (PRO) {
+        const float mul = lrelu_in ? SQRT2 : 1.f;
+        f32x4 s4 = {1.f, 1.f, 1.f, 1.f};
+        if (k.style) s4 = *(const f32x4*)(k.style + (size_t)n * Cin + cb * BK + lc * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float f = v[e];
+          if (lrelu_in) f = fmaxf(f, 0.2f * f);
+          v[e] = f * (s4[e] * mul);
+        }
+      }
       u32x4 hm;
       u32x2 lo;
       split_quad(v, hm, lo);
@@ -542,7 +579,8 @@ __global__ __launch_bounds__(DgX6::NT, 1) void s2dg_x6_kernel(const UpK k) {
         u32x2 al[FM];
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
-          const int hr = (wm * FM + i + jy) * HSIDE + frow + jx;
+          const int hr = DG ? (wm * FM + i + jy) * HSIDE + frow + jx
+                            : (wm * FM + i + 1 - jy) * HSIDE + frow + 1 - jx;
           ahm[i] = *(const u32x4*)(ha + hr * ROWB + ((ch ^ fsw(hr)) << 4));
           al[i] = *(const u32x2*)(lbuf + hr * TL::LROWB + ((ch ^ lsw(hr)) << 3));
         }
@@ -580,17 +618,18 @@ __global__ __launch_bounds__(DgX6::NT, 1) void s2dg_x6_kernel(const UpK k) {
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
       if (st == TL::NSTEP - 1 && cb + 1 < ncb) {  // every wave is past its last read of lbuf
-        convert((cb + 1) & 1);
+        convert(cb + 1);
         __syncthreads();
       }
     }
   }
 
-  // epilogue: phase (py, px) of g position (y, x) → gx(2y + 1 − py, 2x + 1 − px); lane (frow, fq)
-  // holds channels 4·fq … 4·fq+3 of fragment j for pixel x0 + frow
+  // epilogue: phase (py, px) of input position (y, x) → T(2y + py, 2x + px) (DG: g position →
+  // gx(2y + 1 − py, 2x + 1 − px)); lane (frow, fq) holds channels 4·fq … 4·fq+3 of fragment j
+  // for pixel x0 + frow
   const int frow = lane & 15, fq = lane >> 4;
   float* __restrict__ Y = (float*)k.t;
-  const int TS = 2 * R;
+  const int TS = DG ? 2 * R : 2 * R + 1;
   float msl[FN][4];  // slope of the mask per channel of this lane
 #pragma unroll
   for (int j = 0; j < FN; ++j)
@@ -602,19 +641,19 @@ __global__ __launch_bounds__(DgX6::NT, 1) void s2dg_x6_kernel(const UpK k) {
     const int py = ph >> 1, px = ph & 1;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const int ty = 2 * (y0 + wm * FM + i) + 1 - py;
-      const int tx = 2 * (x0 + frow) + 1 - px;
+      const int ty = 2 * (y0 + wm * FM + i) + (DG ? 1 - py : py);
+      const int tx = 2 * (x0 + frow) + (DG ? 1 - px : px);
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int c = n0 + wn * FN * 16 + 16 * j + 4 * fq;
         const size_t o = ((size_t)(n * TS + ty) * TS + tx) * Cout + c;
         f32x4 v = acc[ph][i][j];
-        if (k.mask_a) {
+        if (DG && k.mask_a) {
           const f32x4 m = *(const f32x4*)((const float*)k.mask_a + o);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = m[e] > 0.f ? v[e] : msl[j][e] * v[e];
         }
-        if (k.accumulate) {
+        if (DG && k.accumulate) {
           const f32x4 a = *(const f32x4*)(Y + o);
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += a[e];
@@ -625,34 +664,53 @@ __global__ __launch_bounds__(DgX6::NT, 1) void s2dg_x6_kernel(const UpK k) {
   }
 }
 
-static int launch_s2dg_x6(UpK& k, hipStream_t st) {
+template <bool DG, bool PRO>
+static int launch_upconv_x6(UpK& k, hipStream_t st) {
   typedef DgX6 TL;
   k.nbn = k.Cout / TL::BN;
   k.nblk = k.N * (k.R / TL::PH) * (k.R / TL::PW) * k.nbn;
+  auto fn = upconv_x6_kernel<DG, PRO>;
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)s2dg_x6_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024) != hipSuccess)
       return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     attr_set = true;
   }
-  hipLaunchKernelGGL(s2dg_x6_kernel, dim3(k.nblk), dim3(TL::NT), TL::LDS, st, k);
-  return check_launch("s2dg_x6");
+  hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), TL::LDS, st, k);
+  return check_launch("upconv_x6");
 }
 
-// the split-once kernel: fp32 with pre-split weights, R % 16 == 0, Cx % 64 == 0, and a K loop of
-// at least MIA_S2DG_X6_MINCIN input channels (default 1024: the concatenated head gradients;
-// 0 disables — A/B switch, read per launch)
+// the split-once kernel: fp32 with pre-split weights, R % 16 == 0, Cx % 64 == 0 (MIA_S2DG_X6=0
+// disables: A/B switch, read per launch). Measured against the on-the-fly split kernel (fp32,
+// 128 images, tools/layer_table.py): the 7 concatenated fine heads 146 → 210 TFLOP/s, single
+// 512-channel heads at 16² 133 → 197, the bottleneck units (Cg 64 / 128 / 256) 69 / 97 / 122 →
+// 96 / 147 / 176 — faster at every shape of the attack despite the exposed prologue / epilogue.
+// the split-once kernel for the up-sampling conv forward (fp32, w_up_split given; the last row /
+// column still goes to the generic kernel). MIA_UPCONV_X6=0 disables (A/B switch, per launch).
+static bool upconv_x6_ok(const UpK& k, int dtype) {
+#ifdef MIA_F32_NATIVE
+  (void)k;
+  (void)dtype;
+  return false;
+#else
+  const char* e = getenv("MIA_UPCONV_X6");
+  if (e && atoi(e) == 0) return false;
+  return dtype == MIA_F32 && k.w_split && k.R % DgX6::PH == 0 && k.Cout % DgX6::BN == 0 &&
+         k.Cin % DgX6::BK == 0;
+#endif
+}
+
 static bool s2dg_x6_ok(const UpK& k, int dtype) {
 #ifdef MIA_F32_NATIVE
   (void)k;
   (void)dtype;
   return false;
 #else
-  const char* e = getenv("MIA_S2DG_X6_MINCIN");
-  const int minc = e ? atoi(e) : 1024;
-  return dtype == MIA_F32 && k.w_split && minc > 0 && k.Cin >= minc && k.R % DgX6::PH == 0 &&
-         k.Cout % DgX6::BN == 0 && k.cin_src % DgX6::BK == 0;
+  const char* e = getenv("MIA_S2DG_X6");
+  if (e && atoi(e) == 0) return false;
+  return dtype == MIA_F32 && k.w_split && k.R % DgX6::PH == 0 && k.Cout % DgX6::BN == 0 &&
+         k.cin_src % DgX6::BK == 0;
 #endif
 }
 
@@ -684,7 +742,7 @@ extern "C" int mia_conv_s2_dgrad_halo_multi(const void* const* g, int ng, const 
   for (int i = 0; i < ng; ++i) k.xs[i] = g[i];
   k.cin_src = Cg;
   k.w_split = w_split;
-  if (s2dg_x6_ok(k, dtype)) return launch_s2dg_x6(k, (hipStream_t)stream);
+  if (s2dg_x6_ok(k, dtype)) return launch_upconv_x6<true, false>(k, (hipStream_t)stream);
   MIA_DISPATCH_DTYPE(dtype, T, return launch_upconv_halo<T, false, true>(k, (hipStream_t)stream));
   return set_error("s2_dgrad_halo: unknown dtype");
 }

@@ -149,6 +149,7 @@ def _prof_call(name, flops, *args):
         e1.record()
         prof.append((e0, e1, flops))
         _tag(f"{name} " + (f"R{args[6]} x{args[1]}" if name == "mia_conv_s2_dgrad_halo_multi"
+                             else f"{args[5:8]}" if name == "mia_upconv_fwd_halo_split"
                              else f"{args[4:7]}"))
 
 
@@ -179,8 +180,9 @@ def upconv_fwd(x, w_phases, t_out, cout, act_in=ACT_NONE, style=None, flops=None
     if w_up is not None:
         bk = layouts.halo_bk(T)
         _need(w_up, (Cin // bk, 5, 2, cout, bk), T, "w_up")
-        _prof_call("mia_upconv_fwd_halo", fl, ptr(x), wp, ptr(w_up), ptr(t_out), N, R, Cin, cout,
-                   act_in, ptr(style), dt(T), stream())
+        ws = layouts.split_for(w_up) if T == torch.float32 else None
+        _prof_call("mia_upconv_fwd_halo_split", fl, ptr(x), wp, ptr(w_up), ptr(ws), ptr(t_out), N,
+                   R, Cin, cout, act_in, ptr(style), dt(T), stream())
         return t_out
     _prof_call("mia_upconv_fwd", fl, ptr(x), wp, ptr(t_out), N, R, Cin, cout, act_in, ptr(style),
                dt(T), stream())

@@ -132,7 +132,7 @@ int mia_conv_s2_dgrad_halo(const void* g, const void* w_halo, void* gx, int N, i
  * as ONE K loop: g[i] (N,R,R,Cg) are the convs' output gradients, w_halo the heads' packed
  * matrices concatenated along the first dimension ([ng·Cg/BK][5][2][Cx][BK]); gx as
  * mia_conv_s2_dgrad_halo (the sum, masked, + gx if accumulate). w_split (fp32 only, optional):
- * layouts.split_f32(w_halo) — with ng·Cg ≥ 1024 the split-once fp32 kernel runs. */
+ * layouts.split_f32(w_halo) — the split-once fp32 kernel (csrc/conv_upconv.hip s2dg_x6_kernel). */
 int mia_conv_s2_dgrad_halo_multi(const void* const* g, int ng, const void* w_halo,
                                  const void* w_split, void* gx, int N, int R, int Cg, int Cx,
                                  const void* mask_a, const float* mask_slope, int accumulate,
@@ -189,6 +189,11 @@ int mia_upconv_fwd(const void* x, const void* const* w_phase, void* t_out, int N
 int mia_upconv_fwd_halo(const void* x, const void* const* w_phase, const void* w_up, void* t_out,
                         int N, int R, int Cin, int Cout, int act_in, const float* style,
                         int dtype, void* stream);
+/* mia_upconv_fwd_halo with the split_f32 copy of w_up (fp32: the split-once interior kernel,
+ * csrc/conv_upconv.hip upconv_x6_kernel; NULL → as mia_upconv_fwd_halo). */
+int mia_upconv_fwd_halo_split(const void* x, const void* const* w_phase, const void* w_up,
+                              const void* w_up_split, void* t_out, int N, int R, int Cin, int Cout,
+                              int act_in, const float* style, int dtype, void* stream);
 /* pre = demod·Blur(T) + noise_w·noise + bias, (N, 2R, 2R, C) (rosinality Blur pad (1,1));
  * act_out = MIA_ACT_LRELU_S2 stores the StyledConv activation lrelu(pre)·√2 instead. */
 int mia_upconv_blur_fwd(const void* t, void* pre, const float* demod, const float* noise,

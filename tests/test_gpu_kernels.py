@@ -649,10 +649,15 @@ def test_conv_thin_vgg_input_layer(cuda, monkeypatch, dtype, N, H, W, thin, e4e)
 @pytest.mark.parametrize("N,cin,cout,R", [(2, 64, 64, 16), (1, 128, 192, 32), (2, 256, 128, 16),
                                           (1, 64, 64, 8)])
 @pytest.mark.parametrize("lrelu_in", [False, True])
-def test_upconv_halo_fwd(cuda, dtype, N, cin, cout, R, lrelu_in):
-    """mia_upconv_fwd_halo (halo-tiled interior + generic last row / column) against the
+@pytest.mark.parametrize("x6", ["1", "0"])
+def test_upconv_halo_fwd(cuda, monkeypatch, dtype, N, cin, cout, R, lrelu_in, x6):
+    """mia_upconv_fwd_halo(_split) (halo-tiled interior + generic last row / column) against the
     transposed conv in fp64 on the same rounded operands, and against the phase-GEMM path
-    (R = 8: the library falls back to it)."""
+    (R = 8: the library falls back to it). fp32: the split-once kernel (MIA_UPCONV_X6=1, the
+    default) and the on-the-fly split kernel (0)."""
+    if x6 == "0" and dtype != torch.float32:
+        pytest.skip("the split-once kernel exists for fp32 only")
+    monkeypatch.setenv("MIA_UPCONV_X6", x6)
     g = torch.Generator().manual_seed(N + cin + cout + R)
     x = torch.randn(N, cin, R, R, generator=g)
     w = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(9 * cin)

@@ -87,6 +87,8 @@ SIGNATURES = {
                                  P]),
     "mia_upconv_dgrad_fused": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P, P, c_int, P, P,
                                        c_float, P, P, c_int, P]),
+    "mia_upconv_dgrad_fused_split": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, P, P, P, c_int,
+                                             P, P, c_float, P, P, c_int, P]),
     "mia_bias_act_fwd": (c_int, [P, P, c_float, P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_bias_act_bwd": (c_int, [P, P, P, c_float, P, P, P, P, c_int, c_int, c_int, c_int, c_int,
                                  c_int, c_int, P]),

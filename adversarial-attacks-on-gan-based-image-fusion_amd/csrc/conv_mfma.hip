@@ -354,7 +354,8 @@ typedef Tile<2, 2, 2, 2, 2> Tile64x64;
 // MIA_CONV_REGEPI=0 disables (A/B switch, read per launch).
 static int reg_epi_mask(const ConvK& k, int bytes) {
   const char* e = getenv("MIA_CONV_REGEPI");
-  if ((e && atoi(e) == 0) || bytes != 2 || k.ng != 1 || k.a.shuffle_out) return -1;
+  (void)bytes;
+  if ((e && atoi(e) == 0) || k.ng != 1 || k.a.shuffle_out) return -1;
   const ConvGroup& G = k.g[0];
   if (G.ay != 1 || G.ax != 1 || G.by != 0 || G.bx != 0 || G.ho != k.HT || G.wo != k.WT ||
       (G.ho * G.wo) % 128 != 0)
@@ -429,7 +430,23 @@ static bool x6b_ok(const ConvK& k) {
 template <typename T>
 static int launch_conv(ConvK& k, hipStream_t st) {
   if constexpr (std::is_same<T, float>::value) {
-    if (x6b_ok(k)) return launch_tile<T, Tile128x128, false, false, -2, true>(k, st);
+    if (x6b_ok(k)) {
+      // the specialised register epilogues where they apply (the up-conv adjoints with their
+      // fused backward front, the style-head convs), else the LDS-staged one
+      using namespace epi;
+      switch (reg_epi_mask(k, 4)) {
+        case OSC | SDOT: return launch_tile<T, Tile128x128, false, false, OSC | SDOT, true>(k, st);
+        case OSC | SDOT | ACC:
+          return launch_tile<T, Tile128x128, false, false, OSC | SDOT | ACC, true>(k, st);
+        case OSC | SDOT | BAB:
+          return launch_tile<T, Tile128x128, false, false, OSC | SDOT | BAB, true>(k, st);
+        case OSC | SDOT | ACC | BAB:
+          return launch_tile<T, Tile128x128, false, false, OSC | SDOT | ACC | BAB, true>(k, st);
+        case BIAS | PRELU: return launch_tile<T, Tile128x128, false, false, BIAS | PRELU, true>(k, st);
+        default: break;
+      }
+      return launch_tile<T, Tile128x128, false, false, -2, true>(k, st);
+    }
   }
   const bool pro = k.a.in_scale != nullptr || k.a.act_in != MIA_ACT_NONE;
   const bool small = k.a.Cin < ROWB / (int)sizeof(T);
@@ -680,7 +697,20 @@ extern "C" int mia_upconv_dgrad_fused(const void* g_t, const void* w_t, void* gx
                                       const float* bab_noise, float bab_noise_w,
                                       const float* bab_bias, float* bab_q, int dtype,
                                       void* stream) {
+  return mia_upconv_dgrad_fused_split(g_t, w_t, nullptr, gx, N, R, Cout, Cin, x_fwd, style, sdot,
+                                      accumulate, bab_demod, bab_noise, bab_noise_w, bab_bias,
+                                      bab_q, dtype, stream);
+}
+
+extern "C" int mia_upconv_dgrad_fused_split(const void* g_t, const void* w_t,
+                                            const void* w_t_split, void* gx, int N, int R,
+                                            int Cout, int Cin, const void* x_fwd,
+                                            const float* style, float* sdot, int accumulate,
+                                            const float* bab_demod, const float* bab_noise,
+                                            float bab_noise_w, const float* bab_bias, float* bab_q,
+                                            int dtype, void* stream) {
   mia_conv_args a = {};
+  a.w_split = w_t_split;
   a.x = g_t; a.y = gx; a.N = N; a.H = 2 * R + 1; a.W = 2 * R + 1; a.Cin = Cout; a.Cout = Cin;
   a.out_scale = style; a.aux_x = x_fwd; a.act_aux = MIA_ACT_NONE; a.sdot = sdot;
   a.accumulate = accumulate;
@@ -697,6 +727,7 @@ static int upconv_dgrad_impl(const mia_conv_args& a, const void* w_t, int N, int
   k.ng = 1;
   ConvGroup& G = k.g[0];
   G.w = w_t;
+  G.w_split = a.w_split;
   G.kh = G.kw = 3;
   G.kpad = kpad_for(9 * Cout, dtype);
   G.pad_y = G.pad_x = 0;

@@ -149,7 +149,7 @@ def _prof_call(name, flops, *args):
         e1.record()
         prof.append((e0, e1, flops))
         _tag(f"{name} " + (f"R{args[6]} x{args[1]}" if name == "mia_conv_s2_dgrad_halo_multi"
-                             else f"{args[5:8]}" if name == "mia_upconv_fwd_halo_split"
+                             else f"{args[5:8]}" if name.endswith("_split")
                              else f"{args[4:7]}"))
 
 
@@ -241,9 +241,11 @@ def upconv_dgrad_fused(g_t, w_t, gx, cin, x_fwd, style, sdot, bab, accumulate, f
     _numel_ok(bab["q"], N * cin, torch.float32, "bab.q")
     _numel_ok(bab.get("noise"), R * R, torch.float32, "bab.noise")
     _numel_ok(bab.get("bias"), cin, torch.float32, "bab.bias")
-    _prof_call("mia_upconv_dgrad_fused",
+    ws = layouts.split_for(w_t) if T == torch.float32 else None
+    _prof_call("mia_upconv_dgrad_fused_split",
                flops if flops is not None else 2 * N * R * R * 9 * Cout * cin,
-               ptr(g_t), ptr(w_t), ptr(gx), N, R, Cout, cin, ptr(x_fwd), ptr(style), ptr(sdot),
+               ptr(g_t), ptr(w_t), ptr(ws), ptr(gx), N, R, Cout, cin, ptr(x_fwd), ptr(style),
+               ptr(sdot),
                int(bool(accumulate)), ptr(bab["demod"]), ptr(bab.get("noise")),
                float(bab.get("noise_w", 0.0)), ptr(bab.get("bias")), ptr(bab["q"]), dt(T),
                stream())

@@ -215,6 +215,13 @@ int mia_upconv_dgrad_fused(const void* g_t, const void* w_t, void* gx, int N, in
                            int accumulate, const float* bab_demod, const float* bab_noise,
                            float bab_noise_w, const float* bab_bias, float* bab_q, int dtype,
                            void* stream);
+/* mia_upconv_dgrad_fused with the split_f32 copy of w_t (fp32: the X6B tile, weights pre-split,
+ * csrc/conv_mfma.hip; NULL → as mia_upconv_dgrad_fused). */
+int mia_upconv_dgrad_fused_split(const void* g_t, const void* w_t, const void* w_t_split, void* gx,
+                                 int N, int R, int Cout, int Cin, const void* x_fwd,
+                                 const float* style, float* sdot, int accumulate,
+                                 const float* bab_demod, const float* bab_noise, float bab_noise_w,
+                                 const float* bab_bias, float* bab_q, int dtype, void* stream);
 
 /* ---- elementwise / reduction kernels ----------------------------------------------------- */
 /* FusedLeakyReLU + NoiseInjection forward, standalone (K4): y = lrelu(x + nw·noise + b)·√2 (NHWC). */

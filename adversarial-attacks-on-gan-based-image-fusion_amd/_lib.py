@@ -49,6 +49,11 @@ class ConvGroup(ctypes.Structure):
                 ("bx", c_int), ("w_split", P)]
 
 
+class ConvBatch(ctypes.Structure):
+    """Mirror of ``mia_conv_batch``."""
+    _fields_ = [("n_in", c_int), ("n_out", c_int), ("c_off", c_int)]
+
+
 class GemmSeg(ctypes.Structure):
     """Mirror of ``mia_gemm_seg``."""
     _fields_ = [("A", P), ("B", P), ("sam", c_int64), ("sak", c_int64), ("sbk", c_int64),
@@ -137,6 +142,8 @@ SIGNATURES = {
     "mia_conv2d_kpad": (c_int, [c_int, c_int, c_int]),
     "mia_conv2d": (c_int, [ctypes.POINTER(ConvArgs), c_int, ctypes.POINTER(ConvGroup), c_int,
                            c_int, c_int, c_int, P]),
+    "mia_conv2d_batched": (c_int, [ctypes.POINTER(ConvArgs), c_int, ctypes.POINTER(ConvGroup),
+                                   ctypes.POINTER(ConvBatch), c_int, c_int, c_int, c_int, P]),
     "mia_conv_s2_dgrad_halo": (c_int, [P, P, P, c_int, c_int, c_int, c_int, P, P, c_int, c_int,
                                        P]),
     "mia_conv_s2_dgrad_halo_multi": (c_int, [P, c_int, P, P, P, c_int, c_int, c_int, c_int, P, P,

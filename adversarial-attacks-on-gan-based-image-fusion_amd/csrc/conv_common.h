@@ -16,7 +16,12 @@ struct ConvGroup {
   const void* w;
   int kpad, kh, kw, pad_y, pad_x, ho, wo, ay, by, ax, bx, blk0, nbm, m;
   const void* w_split;  // fp32 pre-split weights (mia_conv_args.w_split) or nullptr
+  // batched independent convs (mia_conv2d_batched): this group reads images n_in … n_in + N − 1
+  // of x, writes images n_out … of y (and the per-pixel aux operands), and reads the per-channel
+  // operands (bias, act_slope, mask_slope) at channel offset c_off; 0 otherwise
+  int n_in, n_out, c_off;
 };
+constexpr int MIA_MAX_GROUPS = 16;
 
 struct ConvK {
   mia_conv_args a;  // x, y, N, H/W = INPUT dims, Cin, Cout and the epilogue fields
@@ -27,7 +32,8 @@ struct ConvK {
                                  // LDS before the atomics; on for the channel sum (SE pool) only:
                                  // measured, the extra barrier costs more than it saves for the
                                  // sdot / q sums of the StyledConv dgrads (MIA_EPI_PRERED=0: off)
-  ConvGroup g[4];
+  int batched;                   // groups carry image / channel offsets: LDS-staged epilogue only
+  ConvGroup g[MIA_MAX_GROUPS];
 };
 
 typedef const __attribute__((address_space(1))) void* gptr_t;
@@ -324,8 +330,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
   const bool prelu = p.act_out == MIA_ACT_PRELU;
 #pragma unroll
   for (int e = 0; e < 8; ++e) aslope8[e] = mslope8[e] = 0.f;
-  if (prelu && col_ok) load8f(p.act_slope + col, aslope8);
-  if (p.mask_slope && col_ok) load8f(p.mask_slope + col, mslope8);
+  if (prelu && col_ok) load8f(p.act_slope + G.c_off + col, aslope8);
+  if (p.mask_slope && col_ok) load8f(p.mask_slope + G.c_off + col, mslope8);
   const bool bab = p.bab_demod != nullptr;
   float bbias8[8];
   if (bab) {
@@ -340,7 +346,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
   // per-column epilogue constants, loaded once (single-image tiles: out_scale too)
   float bias8[8], osc8[8];
   const int cm0 = p.shuffle_out ? col % k.cout_mod : col;
-  if (p.bias && col_ok) load8f(p.bias + cm0, bias8);
+  n_single += G.n_out;  // batched groups: the group's first output image
+  if (p.bias && col_ok) load8f(p.bias + G.c_off + cm0, bias8);
   if (p.out_scale && single && col_ok) load8f(p.out_scale + (size_t)n_single * k.cout_mod + cm0, osc8);
   constexpr int ITERS = EROWS / RPP;
   static_assert(ITERS * RPP == EROWS, "");
@@ -365,9 +372,10 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
       if (row >= 0 && col_ok) {
         float v[8];
         load8f(tile + rr * ES + cc * 8, v);
-        const int n = single ? n_single : row / HWo;
+        const int ng = row / HWo;  // image within the group
+        const int n = single ? n_single : ng + G.n_out;
         // output placement (aux operands share the output's pixel grid, channel stride Cout)
-        const int pix = row - n * HWo;
+        const int pix = row - ng * HWo;
         const int y = pix / G.wo, x = pix - (pix / G.wo) * G.wo;
         int cm = col, yo, xo;
         if (p.shuffle_out) {

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
   const int bl = xcd_remap(blockIdx.x, k.nblk);
   int gi = 0;
 #pragma unroll
-  for (int g = 1; g < 4; ++g)
+  for (int g = 1; g < MIA_MAX_GROUPS; ++g)
     if (g < k.ng && bl >= k.g[g].blk0) gi = g;
   const ConvGroup G = k.g[gi];  // by value: scalar registers for the whole kernel
   const int b = bl - G.blk0;
@@ -108,8 +108,9 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
     const int m = m0 + row;
     int msk = 0, base = 0;
     if (m < G.m) {
-      const int n = m / HWo;
-      const int rem = m - n * HWo;
+      const int ng = m / HWo;  // image within the group
+      const int rem = m - ng * HWo;
+      const int n = ng + G.n_in;
       const int y = rem / G.wo, x = rem - (rem / G.wo) * G.wo;
       const int iy0 = k.stride * y - G.pad_y, ix0 = k.stride * x - G.pad_x;
       base = ((n * Hin + iy0) * Win + ix0) * Cin;
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
     const int cnt = (n_last - n_first + 1) * Cin;
     const float mul = lrelu_in ? SQRT2 : 1.f;
     for (int i = tid; i < cnt; i += NT) {
-      const float sv = p.in_scale ? p.in_scale[(size_t)n_first * Cin + i] : 1.f;
+      const float sv = p.in_scale ? p.in_scale[(size_t)(n_first + G.n_in) * Cin + i] : 1.f;
       stab[i] = from_f<T>(sv * mul);
     }
 #pragma unroll
@@ -355,7 +356,7 @@ typedef Tile<2, 2, 2, 2, 2> Tile64x64;
 static int reg_epi_mask(const ConvK& k, int bytes) {
   const char* e = getenv("MIA_CONV_REGEPI");
   (void)bytes;
-  if ((e && atoi(e) == 0) || k.ng != 1 || k.a.shuffle_out) return -1;
+  if ((e && atoi(e) == 0) || k.ng != 1 || k.batched || k.a.shuffle_out) return -1;
   const ConvGroup& G = k.g[0];
   if (G.ay != 1 || G.ax != 1 || G.by != 0 || G.bx != 0 || G.ho != k.HT || G.wo != k.WT ||
       (G.ho * G.wo) % 128 != 0)
@@ -483,7 +484,7 @@ static int run_conv(ConvK& k, int dtype, hipStream_t st) {
                 "aux inputs need un-shuffled output");
   MIA_CHECK_ARG((int64_t)a.N * a.H * a.W * a.Cin < (1LL << 31), "input too large for 32-bit offsets");
   MIA_CHECK_ARG(a.in_scale == nullptr || a.Cin <= 2048, "modulated Cin ≤ 2048");
-  MIA_CHECK_ARG(k.ng >= 1 && k.ng <= 4, "1..4 groups");
+  MIA_CHECK_ARG(k.ng >= 1 && k.ng <= (k.batched ? MIA_MAX_GROUPS : 4), "1..4 groups (16 batched)");
   for (int g = 0; g < k.ng; ++g) {
     const ConvGroup& G = k.g[g];
     MIA_CHECK_ARG(G.w, "w is required");
@@ -504,6 +505,11 @@ static int run_conv(ConvK& k, int dtype, hipStream_t st) {
   for (int g = 0; g < k.ng; ++g) hw_min = std::min(hw_min, k.g[g].ho * k.g[g].wo);
   k.n_first_max = std::min(a.N, (256 + hw_min - 1) / hw_min + 1);
 
+  if (k.batched) {  // the generic tile only (its LDS-staged epilogue applies the offsets)
+    MIA_CHECK_ARG(!a.shuffle_out && !a.sdot && !a.bab_demod && !a.csum,
+                  "batched groups: no shuffle_out / sdot / bab / csum");
+    MIA_DISPATCH_DTYPE(dtype, T, return launch_conv<T>(k, st));
+  }
   if (conv_thin_eligible(k, dtype)) return launch_conv_thin(k, dtype, st);
   if (conv_thin32_eligible(k, dtype)) return launch_conv_thin32(k, dtype, st);
   if (conv_wres_eligible(k, dtype)) return launch_conv_wres(k, dtype, st);
@@ -546,10 +552,32 @@ extern "C" int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream) {
 
 extern "C" int mia_conv2d_kpad(int taps, int cin, int dtype) { return kpad_for(taps * cin, dtype); }
 
+static int conv2d_impl(const mia_conv_args* args, int stride, const mia_conv_group* groups,
+                       const mia_conv_batch* batch, int ngroups, int out_h, int out_w, int dtype,
+                       void* stream);
+
 extern "C" int mia_conv2d(const mia_conv_args* args, int stride, const mia_conv_group* groups,
                           int ngroups, int out_h, int out_w, int dtype, void* stream) {
-  MIA_CHECK_ARG(args != nullptr && groups != nullptr, "null args");
   MIA_CHECK_ARG(ngroups >= 1 && ngroups <= 4, "1..4 groups");
+  return conv2d_impl(args, stride, groups, nullptr, ngroups, out_h, out_w, dtype, stream);
+}
+
+extern "C" int mia_conv2d_batched(const mia_conv_args* args, int stride,
+                                  const mia_conv_group* groups, const mia_conv_batch* batch,
+                                  int ngroups, int out_h, int out_w, int dtype, void* stream) {
+  MIA_CHECK_ARG(batch != nullptr, "null batch");
+  MIA_CHECK_ARG(ngroups >= 1 && ngroups <= MIA_MAX_GROUPS, "1..16 groups");
+  for (int g = 0; g < ngroups; ++g)
+    MIA_CHECK_ARG(batch[g].n_in >= 0 && batch[g].n_out >= 0 && batch[g].c_off >= 0 &&
+                      batch[g].c_off % 8 == 0,
+                  "batch offsets must be ≥ 0 (c_off a multiple of 8)");
+  return conv2d_impl(args, stride, groups, batch, ngroups, out_h, out_w, dtype, stream);
+}
+
+static int conv2d_impl(const mia_conv_args* args, int stride, const mia_conv_group* groups,
+                       const mia_conv_batch* batch, int ngroups, int out_h, int out_w, int dtype,
+                       void* stream) {
+  MIA_CHECK_ARG(args != nullptr && groups != nullptr, "null args");
   MIA_CHECK_ARG(stride == 1 || stride == 2, "stride 1 or 2");
   MIA_CHECK_ARG(out_h > 0 && out_w > 0, "empty output");
   MIA_CHECK_ARG(!args->shuffle_out, "shuffle_out is a mia_conv3x3 feature");
@@ -558,6 +586,7 @@ extern "C" int mia_conv2d(const mia_conv_args* args, int stride, const mia_conv_
   k.a = a;
   k.stride = stride;
   k.ng = ngroups;
+  k.batched = batch != nullptr;
   k.HT = out_h;
   k.WT = out_w;
   k.cout_mod = a.Cout;
@@ -580,6 +609,11 @@ extern "C" int mia_conv2d(const mia_conv_args* args, int stride, const mia_conv_
     G.ax = s.ax;
     G.bx = s.bx;
     G.m = a.N * s.ho * s.wo;
+    if (batch) {
+      G.n_in = batch[g].n_in;
+      G.n_out = batch[g].n_out;
+      G.c_off = batch[g].c_off;
+    }
   }
   return run_conv(k, dtype, (hipStream_t)stream);
 }

@@ -32,16 +32,12 @@ adjoint in the PGD update. Stored for the backward: per unit a1 = PReLU(conv1), 
 the SE vectors u, s; the head activations; nothing else.
 """
 import math
-import os
 
 import torch
 
 from . import layouts, ops
 from .ops import ACT_PRELU
 
-# side streams for the style heads: 3 + the caller's = GPU_MAX_HW_QUEUES (4 on the box); measured
-# 55.9 / 55.7 img/s vs 55.6 / 55.6 with 4; MIA_HEAD_STREAMS overrides it (A/B switch)
-HEAD_STREAMS = max(1, int(os.environ.get("MIA_HEAD_STREAMS", "3")))
 from .vgg import CPAD
 from .weights import (E4E_COARSE, E4E_MIDDLE, E4E_SE_REDUCTION, STYLE_DIM, e4e_style_spatial,
                       e4e_units, n_latent_for)
@@ -158,9 +154,32 @@ class E4EEncoder:
                                   wdh=mt(layouts.s2_dgrad_halo_matrix(w, T)) if halo else None,
                                   b=dd(p[f"styles.{i}.convs.{2 * j}.bias"])))
                 h = ho
-            self.heads.append(dict(convs=convs, src=src,
+            self.heads.append(dict(convs=convs, src=src, h0=self.R // {"c3": 16, "p2": 8,
+                                                                     "p1": 4}[src],
                                    lw=dd(p[f"styles.{i}.linear.weight"].double() * inv),
                                    lb=dd(p[f"styles.{i}.linear.bias"])))
+        # Level batching: every head activation of resolution r lives in ONE stacked buffer
+        # (S_r·N, r, r, 512), head i at slot slot[r][i]; the non-first convs of all heads with the
+        # same input resolution run as ONE mia_conv2d_batched launch (group = head: its weights,
+        # its image range in and out, its bias at channel offset c_off), their input gradients as
+        # one batched launch per sub-pixel phase. Per head the 8²…1² convs are a few tiles each
+        # with a 144-step K loop, latency-bound: batched, the 14 heads share that latency.
+        outs = {}
+        for i, hd in enumerate(self.heads):
+            r = hd["h0"]
+            hd["res"] = []
+            for _ in hd["convs"]:
+                r = _s2_out(r)
+                hd["res"].append(r)
+                outs.setdefault(r, []).append(i)
+        self.slot = {r: {i: k for k, i in enumerate(sorted(v))} for r, v in outs.items()}
+        self.levels = []  # (r_in, r_out, [(head, conv index)], bias cat)
+        for r_in in sorted({r for hd in self.heads for r in hd["res"][:-1]}, reverse=True):
+            mem = [(i, j) for i, hd in enumerate(self.heads) for j in range(1, len(hd["convs"]))
+                   if hd["res"][j - 1] == r_in]
+            bcat = torch.cat([self.heads[i]["convs"][j]["b"] for i, j in mem]).contiguous()
+            self.levels.append((r_in, _s2_out(r_in), mem, bcat))
+        self.slope_cat = torch.full((16 * STYLE_DIM,), 0.01, dtype=f32, device=dev)
         # the heads whose first conv reads the same FPN map (7 on p1, 4 on p2): their first-conv
         # input gradients run as ONE multi-source launch with the packed matrices concatenated
         # along K (mia_conv_s2_dgrad_halo_multi) — one write of the source gradient instead of
@@ -176,15 +195,19 @@ class E4EEncoder:
         b0l = self.heads[0]["lb"]
         self.lin_bias = [b0l] + [(h["lb"] + b0l).contiguous() for h in self.heads[1:]]
         self.flops_fwd_per_image = self._count_flops()
-        self._side = None
 
-    def _side_streams(self):
-        """The 14 GradualStyleBlocks are independent chains of small stride-2 convs (8²…1²
-        outputs: a few tiles each, latency-bound on their K loop), so they run concurrently on
-        HEAD_STREAMS side streams forked from / joined into the caller's stream."""
-        if self._side is None:
-            self._side = [torch.cuda.Stream(device=self.device) for _ in range(HEAD_STREAMS)]
-        return self._side
+    def _level_buf(self, ws, kind, r, N):
+        """Stacked head activations ('a') or their gradients ('g') at resolution r."""
+        return self._buf(ws, f"h{kind}{r}", (len(self.slot[r]) * N, r, r, STYLE_DIM))
+
+    def _head_view(self, ws, kind, i, j, N):
+        r = self.heads[i]["res"][j]
+        k = self.slot[r][i]
+        return self._level_buf(ws, kind, r, N)[k * N:(k + 1) * N]
+
+    def _feat_stack(self, ws, name, N):
+        """(n_latent, N, 512) fp32: the heads' 512-vectors (f) or their gradients (gf)."""
+        return self._buf(ws, name, (self.n_latent, N, STYLE_DIM), torch.float32)
 
     # ------------------------------------------------------------------------------------------
     def _count_flops(self):
@@ -272,28 +295,29 @@ class E4EEncoder:
                    bias=self.lat_b[1], accumulate=True)
         feats.update(p2=p2, p1=p1)
         self._feats = feats
-        main = torch.cuda.current_stream()
-        side = self._side_streams()
-        for st in side:
-            st.wait_stream(main)
+        # style heads: the first conv of each head from its FPN map into the head's slot of the
+        # stacked level buffer, then one batched launch per resolution level
         for i, hd in enumerate(self.heads):
             x = feats[hd["src"]]
-            h = x.shape[1]
-            acts = []
-            with torch.cuda.stream(side[i % len(side)]):
-                for j, cv in enumerate(hd["convs"]):
-                    ho = _s2_out(h)
-                    a = self._buf(ws, f"h{i}_{j}", (N, ho, ho, STYLE_DIM))
-                    ops.conv2d(x, [_g3(cv["w"], ho)], a, (ho, ho), cout=STYLE_DIM, stride=2,
-                               bias=cv["b"], act_out=ACT_PRELU, act_slope=self.slope001)
-                    acts.append(a)
-                    x, h = a, ho
-                if h != 1:
-                    raise ValueError("GradualStyleBlock must end at 1×1 (encoder input R = 256)")
-                hd["_acts"] = acts
-                ops.cast(x, self._buf(ws, f"f{i}", (N, STYLE_DIM), f32))
-        for st in side:
-            main.wait_stream(st)
+            cv = hd["convs"][0]
+            r = hd["res"][0]
+            ops.conv2d(x, [_g3(cv["w"], r)], self._head_view(ws, "a", i, 0, N), (r, r),
+                       cout=STYLE_DIM, stride=2, bias=cv["b"], act_out=ACT_PRELU,
+                       act_slope=self.slope001)
+        for r_in, r_out, mem, bcat in self.levels:
+            groups = [dict(_g3(self.heads[i]["convs"][j]["w"], r_out),
+                           n_in=self.slot[r_in][i] * N, n_out=self.slot[r_out][i] * N,
+                           c_off=k * STYLE_DIM) for k, (i, j) in enumerate(mem)]
+            ops.conv2d_batched(self._level_buf(ws, "a", r_in, N), groups,
+                               self._level_buf(ws, "a", r_out, N), (r_out, r_out), n=N,
+                               cout=STYLE_DIM, stride=2, bias=bcat, act_out=ACT_PRELU,
+                               act_slope=self.slope_cat)
+        for i, hd in enumerate(self.heads):
+            if hd["res"][-1] != 1:
+                raise ValueError("GradualStyleBlock must end at 1×1 (encoder input R = 256)")
+            hd["_acts"] = [self._head_view(ws, "a", i, j, N) for j in range(len(hd["convs"]))]
+        # the 1×1 activations of all heads (stacked in head order) → the fp32 feature stack
+        ops.cast(self._level_buf(ws, "a", 1, N), self._feat_stack(ws, "fst", N))
         lat = ws.get(f"{tag}.lat", (N, self.n_latent, STYLE_DIM), f32)
         self._plan(ws, N, "fwd", lat).run()
         return lat
@@ -309,7 +333,7 @@ class E4EEncoder:
         f32 = torch.float32
         S, D = self.n_latent, STYLE_DIM
         plan = ops.GemmPlan()
-        f = [self._buf(ws, f"f{i}", (N, D), f32) for i in range(S)]
+        f = list(self._feat_stack(ws, "fst", N).unbind(0))  # head i = slot i at 1×1
         if kind == "fwd":  # lat[:, i] = f_i·W_iᵀ (+ f_0·W_0ᵀ) + b
             for i, hd in enumerate(self.heads):
                 segs = [(f[i], D, 1, hd["lw"], 1, D, D)]
@@ -317,7 +341,7 @@ class E4EEncoder:
                     segs.append((f[0], D, 1, self.heads[0]["lw"], 1, D, D))
                 plan.add(lat[:, i, :], S * D, 1, N, D, segs, bias=self.lin_bias[i])
         else:  # ∂f_i = ∂lat[:, i]·W_i (i ≥ 1); ∂f_0 = Σ_i ∂lat[:, i]·W_0
-            gf = [self._buf(ws, f"gf{i}", (N, D), f32) for i in range(S)]
+            gf = list(self._feat_stack(ws, "gfst", N).unbind(0))
             gsum = self._buf(ws, "gsum", (N, D), f32)  # Σ_i ∂lat[:, i] (backward_nhwc)
             plan.add(gf[0], D, 1, N, D, [(gsum, D, 1, self.heads[0]["lw"], D, 1, D)])
             for i in range(1, S):
@@ -351,52 +375,48 @@ class E4EEncoder:
         ops.sum_slices(g_lat, self._buf(ws, "gsum", (N, D), f32))
         self._plan(ws, N, "bwd", g_lat).run()
         gfeat = {k: self._buf(ws, "g" + k, feats[k].shape) for k in ("c3", "p2", "p1")}
-        # style heads, fine first (their gradient feeds p1 → p2 → c3): every head's chain down to
-        # its first conv's output gradient runs concurrently on the side streams; the first convs
-        # (input gradients into the shared source-feature gradient, the later ones accumulating)
-        # run in the same head order on one side stream per source
-        main = torch.cuda.current_stream()
-        side = self._side_streams()
-        for st in side:
-            main_ev = main.record_event()
-            st.wait_event(main_ev)
-        heads_g, heads_ev = {}, {}
-        for i in reversed(range(self.n_latent)):
-            hd = self.heads[i]
-            acts = hd["_acts"]
-            st = side[i % len(side)]
-            with torch.cuda.stream(st):
-                g = self._buf(ws, f"gh{i}", acts[-1].shape)
-                ops.cast(self._buf(ws, f"gf{i}", (N, D), f32), g)
-                ops.prelu_bwd_scale(g, acts[-1], self.slope001, g)
-                for j in reversed(range(1, len(hd["convs"]))):
-                    cv = hd["convs"][j]
-                    y = self._buf(ws, f"ghh{i}_{j - 1}", acts[j - 1].shape)
-                    self._s2_dgrad(g, cv["wd"], cv["wdh"], y, acts[j - 1], self.slope001, False)
-                    g = y
-                heads_g[i], heads_ev[i] = g, st.record_event()
-        src_stream = {src: side[k % len(side)] for k, src in enumerate(("c3", "p2", "p1"))}
+        # style heads: the 1×1 gradients of all heads in one cast + LeakyReLU' pass, then the
+        # batched levels top-down (one launch per sub-pixel phase; the 32² → 16² level of the fine
+        # heads per head on the split-once halo kernel), then the first convs' input gradients
+        # into the FPN maps (one multi-source launch per map where the halo kernel applies)
+        g1 = self._level_buf(ws, "g", 1, N)
+        ops.cast(self._feat_stack(ws, "gfst", N), g1)
+        ops.prelu_bwd_scale(g1, self._level_buf(ws, "a", 1, N), self.slope001, g1)
+        for r_in, r_out, mem, _ in reversed(self.levels):
+            gin, gout = self._level_buf(ws, "g", r_out, N), self._level_buf(ws, "g", r_in, N)
+            mask = self._level_buf(ws, "a", r_in, N)
+            cv0 = self.heads[mem[0][0]]["convs"][mem[0][1]]
+            if cv0["wdh"] is not None and all(self.heads[i]["convs"][j]["wdh"] is not None
+                                              for i, j in mem):
+                for i, j in mem:
+                    ops.s2_dgrad_halo(self._head_view(ws, "g", i, j, N),
+                                      self.heads[i]["convs"][j]["wdh"],
+                                      self._head_view(ws, "g", i, j - 1, N),
+                                      mask_a=self._head_view(ws, "a", i, j - 1, N),
+                                      mask_slope=self.slope001)
+                continue
+            for ph in range(4):
+                groups = []
+                for k, (i, j) in enumerate(mem):
+                    pg = _phase_groups([self.heads[i]["convs"][j]["wd"][ph]], r_in)
+                    if pg:
+                        groups.append(dict(pg[0], n_in=self.slot[r_out][i] * N,
+                                           n_out=self.slot[r_in][i] * N, c_off=k * STYLE_DIM))
+                if groups:
+                    ops.conv2d_batched(gin, groups, gout, (r_in, r_in), n=N, cout=STYLE_DIM,
+                                       mask_a=mask, mask_slope=self.slope_cat)
         seen = set()
         for src, (idx, wcat) in self.src_heads.items():
-            st = src_stream[src]
-            for i in idx:
-                st.wait_event(heads_ev[i])
-            with torch.cuda.stream(st):
-                ops.s2_dgrad_halo([heads_g[i] for i in idx], wcat, gfeat[src])
+            ops.s2_dgrad_halo([self._head_view(ws, "g", i, 0, N) for i in idx], wcat, gfeat[src])
             seen.add(src)
         for i in reversed(range(self.n_latent)):
             hd = self.heads[i]
             if hd["src"] in self.src_heads:
                 continue
-            st = src_stream[hd["src"]]
-            st.wait_event(heads_ev[i])
-            with torch.cuda.stream(st):
-                cv = hd["convs"][0]
-                self._s2_dgrad(heads_g[i], cv["wd"], cv["wdh"], gfeat[hd["src"]], None,
-                               self.slope001, hd["src"] in seen)
+            cv = hd["convs"][0]
+            self._s2_dgrad(self._head_view(ws, "g", i, 0, N), cv["wd"], cv["wdh"],
+                           gfeat[hd["src"]], None, self.slope001, hd["src"] in seen)
             seen.add(hd["src"])
-        for st in side:
-            main.wait_stream(st)
         dbg = getattr(self, "debug", None)  # tests: dict to receive intermediate gradients
         if dbg is not None:
             dbg.update({"heads." + k: v.clone() for k, v in gfeat.items()})

@@ -732,6 +732,73 @@ def conv2d(x, groups, y, out_hw, *, cout, stride=1, bias=None, act_out=ACT_NONE,
     return y
 
 
+def conv2d_batched(x, groups, y, out_hw, *, n, cout, stride=1, bias=None, act_out=ACT_NONE,
+                   act_slope=None, mask_a=None, mask_slope=None, accumulate=False, flops=None):
+    """mia_conv2d_batched: up to 16 independent convs of one launch. x (Sx·n, H, W, Cin) and y
+    (Sy·n, out_h, out_w, Cout) hold the groups' images stacked along N; each group dict is as in
+    conv2d plus n_in / n_out (first input / output image) and c_off (channel offset into the
+    concatenated per-channel operands bias, act_slope, mask_slope). mask_a lives on y's grid."""
+    _, H, W, Cin = x.shape
+    T = x.dtype
+    oh, ow = out_hw
+    if Cin % VEC[T]:
+        raise ValueError("Cin must be a multiple of the 16-byte vector")
+    if not 1 <= len(groups) <= 16:
+        raise ValueError("1..16 groups")
+    if y.dim() != 4 or tuple(y.shape[1:]) != (oh, ow, cout) or y.dtype != T:
+        raise ValueError(f"y: (S·n, {oh}, {ow}, {cout}) {T} required")
+    if mask_a is not None and (mask_a.shape != y.shape or mask_a.dtype != T):
+        raise ValueError("mask_a must match y")
+    if act_out == ACT_PRELU and act_slope is None:
+        raise ValueError("ACT_PRELU needs act_slope")
+    garr = (_lib.ConvGroup * len(groups))()
+    barr = (_lib.ConvBatch * len(groups))()
+    keep = []
+    mac = 0
+    for i, g in enumerate(groups):
+        kh, kw = g["kh"], g["kw"]
+        _need(g["w"], (cout, conv2d_kpad(kh * kw, Cin, T)), T, f"w[{i}]")
+        py, px = g.get("pad", (0, 0))
+        ay, ax = g.get("a", (1, 1))
+        by, bx = g.get("b", (0, 0))
+        ho, wo = g["ho"], g["wo"]
+        if ho <= 0 or wo <= 0 or ay * (ho - 1) + by >= oh or ax * (wo - 1) + bx >= ow:
+            raise ValueError(f"group {i}: placement outside the output grid")
+        n_in, n_out, c_off = g.get("n_in", 0), g.get("n_out", 0), g.get("c_off", 0)
+        if n_in < 0 or n_in + n > x.shape[0] or n_out < 0 or n_out + n > y.shape[0]:
+            raise ValueError(f"group {i}: image range outside x / y")
+        if c_off % 8:
+            raise ValueError(f"group {i}: c_off must be a multiple of 8")
+        for name, t in (("bias", bias), ("act_slope", act_slope), ("mask_slope", mask_slope)):
+            if t is not None and (t.dtype != torch.float32 or t.numel() < c_off + cout):
+                raise ValueError(f"group {i}: {name} shorter than c_off + cout")
+        wsp = layouts.split_for(g["w"]) if T == torch.float32 else None
+        garr[i] = _lib.ConvGroup(ptr(g["w"]).value, kh, kw, py, px, ho, wo, ay, by, ax, bx,
+                                 ptr(wsp).value if wsp is not None else None)
+        barr[i] = _lib.ConvBatch(n_in, n_out, c_off)
+        keep += [g["w"], wsp]
+        mac += n * ho * wo * kh * kw * Cin * cout
+    a = ConvArgs()
+    a.x, a.y = ptr(x), ptr(y)
+    a.N, a.H, a.W, a.Cin, a.Cout = n, H, W, Cin, cout
+    a.bias = ptr(bias)
+    a.act_out, a.act_slope = act_out, ptr(act_slope)
+    a.mask_a, a.mask_slope = ptr(mask_a), ptr(mask_slope)
+    a.accumulate = int(bool(accumulate))
+    prof = PROFILE
+    if prof is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    call("mia_conv2d_batched", ctypes.byref(a), int(stride), garr, barr, len(groups), oh, ow, dt(T),
+         stream())
+    if prof is not None:
+        e1.record()
+        prof.append((e0, e1, flops if flops is not None else 2 * mac))
+        _tag(f"conv2d_batched {H}x{W} {Cin}->{cout} s{stride} x{len(groups)} k{groups[0]['kh']}"
+             + (" mask" if mask_a is not None else "") + (" acc" if accumulate else ""))
+    return y
+
+
 def se_fwd(csum, w1, w2, u, s, hw):
     N, C = csum.shape
     Cr = w1.shape[0]

@@ -146,6 +146,19 @@ typedef struct mia_conv_group {
 int mia_conv2d_kpad(int taps, int cin, int dtype);
 int mia_conv2d(const mia_conv_args* args, int stride, const mia_conv_group* groups, int ngroups,
                int out_h, int out_w, int dtype, void* stream);
+/* Up to 16 INDEPENDENT convs of one geometry family in one launch (the e4e GradualStyleBlock
+ * convs of one resolution level across the style heads, psp_encoders GradualStyleBlock.forward,
+ * reached through net.encoder at code/attack/attack_main2.py:597,622): group g is a conv with its
+ * own weights (groups[g]) over images batch[g].n_in … + args->N − 1 of args->x, writing images
+ * batch[g].n_out … of args->y (aux operands such as mask_a likewise), its per-channel operands
+ * (bias, act_slope, mask_slope) read at channel offset batch[g].c_off. x / y / mask_a hold all
+ * groups' images stacked along N. No shuffle_out / sdot / bab / csum. */
+typedef struct mia_conv_batch {
+  int n_in, n_out, c_off;
+} mia_conv_batch;
+int mia_conv2d_batched(const mia_conv_args* args, int stride, const mia_conv_group* groups,
+                       const mia_conv_batch* batch, int ngroups, int out_h, int out_w, int dtype,
+                       void* stream);
 
 /* ---- named entry points (thin wrappers over mia_conv3x3) ------------------------------- */
 /* ModulatedConv2d + NoiseInjection + FusedLeakyReLU bias, forward [ext]

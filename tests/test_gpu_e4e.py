@@ -98,6 +98,60 @@ def test_s2_dgrad_halo_vs_autograd(cuda, dtype, R, cg, cx):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("N,H,S", [(2, 8, 3), (3, 2, 14), (1, 16, 5)])
+def test_conv2d_batched_heads(cuda, dtype, N, H, S):
+    """mia_conv2d_batched (the e4e style-head levels): S independent stride-2 3×3 convs over
+    stacked images with per-group weights, image offsets (slots permuted between input and
+    output) and bias / PReLU slopes at channel offsets; then their input gradients as one batched
+    launch per sub-pixel phase with the slope mask — vs torch fp64 per group."""
+    C = 64
+    ho = (H - 1) // 2 + 1
+    ws = [rnd((C, C, 3, 3), 200 + i, math.sqrt(2 / (9 * C))) for i in range(S)]
+    bs = [rnd((C,), 300 + i, 0.1) for i in range(S)]
+    xs = rnd((S * N, C, H, H), 400)
+    perm = list(reversed(range(S)))  # output slot of group k
+    slope = torch.full((16 * C,), 0.01, device=cuda)
+    groups = []
+    for k in range(S):
+        kp = ops.conv2d_kpad(9, C, dtype)
+        wm = torch.zeros(C, kp, dtype=torch.float64)
+        wm[:, :9 * C] = ws[k].permute(0, 2, 3, 1).reshape(C, 9 * C)
+        groups.append(dict(w=wm.to(dtype).to(cuda), kh=3, kw=3, pad=(1, 1), ho=ho, wo=ho,
+                           n_in=k * N, n_out=perm[k] * N, c_off=k * C))
+    y = torch.full((S * N, ho, ho, C), float("nan"), dtype=dtype, device=cuda)
+    ops.conv2d_batched(nhwc(xs, dtype, cuda), groups, y, (ho, ho), n=N, cout=C, stride=2,
+                       bias=torch.cat(bs).float().to(cuda), act_out=ops.ACT_PRELU, act_slope=slope)
+    gys = rnd((S * N, C, ho, ho), 500)
+    masks = rnd((S * N, C, H, H), 600)
+    gx = torch.full((S * N, H, H, C), float("nan"), dtype=dtype, device=cuda)
+    for ph in range(4):
+        grp = []
+        for k in range(S):
+            pg = e4e._phase_groups([layouts.s2_dgrad_phases(ws[k], dtype)[ph]], H)
+            if pg:
+                grp.append(dict(pg[0], w=pg[0]["w"].to(cuda), n_in=perm[k] * N, n_out=k * N,
+                                c_off=k * C))
+        if grp:
+            ops.conv2d_batched(nhwc(gys, dtype, cuda), grp, gx, (H, H), n=N, cout=C,
+                               mask_a=nhwc(masks, dtype, cuda), mask_slope=slope)
+    torch.cuda.synchronize()
+    tol = {torch.float32: 2e-5, torch.float16: 2e-2}[dtype]
+    for k in range(S):
+        xq = xs[k * N:(k + 1) * N].to(dtype).double()
+        wq = ws[k].to(dtype).double()
+        pre = F.conv2d(xq, wq, bs[k].float().double(), stride=2, padding=1)
+        ref = torch.where(pre > 0, pre, 0.01 * pre)
+        o = perm[k] * N
+        assert rel_err(nchw(y[o:o + N]), ref) < tol
+        xx = torch.zeros_like(xq, requires_grad=True)
+        (gref,) = torch.autograd.grad(F.conv2d(xx, wq, stride=2, padding=1), xx,
+                                      gys[o:o + N].to(dtype).double())
+        mk = masks[k * N:(k + 1) * N].to(dtype).double()
+        gref = torch.where(mk > 0, gref, 0.01 * gref)
+        assert rel_err(nchw(gx[k * N:(k + 1) * N]), gref) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("N,R,ng,cg,cx", [(1, 32, 7, 512, 512), (2, 16, 2, 512, 128),
                                           (2, 16, 3, 64, 64), (1, 16, 4, 256, 192)])
 @pytest.mark.parametrize("mask", [False, True])

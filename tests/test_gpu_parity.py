@@ -47,7 +47,10 @@ def test_objective_and_gradient_match_reference_optimize_vgg(cuda, objg, kind):
     eng.prepare(x0.to(cuda), t.to(cuda))
     L0 = float(eng.loss(x0.to(cuda))[0])
     ref_L0 = float(objg[f"{kind}/losses"][0])
-    assert abs(L0 - ref_L0) <= 5e-6 + 1e-5 * abs(ref_L0), (L0, ref_L0)  # fp32 sums vs '%.5f'
+    # fp32 sums vs '%.5f'; the e4e's SE channel sums are block atomics (fp32 summation order
+    # varies run to run) and its PReLU / LeakyReLU(0.01) branches of activations within rounding
+    # of 0 follow: measured run-to-run spread of the e4e objective ≈ 1e-5 relative
+    assert abs(L0 - ref_L0) <= 5e-6 + 2e-5 * abs(ref_L0), (L0, ref_L0)
     g0 = eng.full_gradient(x0.to(cuda)).cpu().double()
     probes = gen.projections(size)
     proj_rel = _rel([float((p * g0).sum()) for p in probes], objg[f"{kind}/grad0/proj"])

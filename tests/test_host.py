@@ -82,6 +82,7 @@ def test_library_exports_every_header_symbol():
 
 @pytest.mark.parametrize("cname,pyname", [("mia_conv_args", "ConvArgs"),
                                           ("mia_conv_group", "ConvGroup"),
+                                          ("mia_conv_batch", "ConvBatch"),
                                           ("mia_gemm_seg", "GemmSeg"),
                                           ("mia_gemm_group", "GemmGroup")])
 def test_abi_struct_layout_matches_c(tmp_path, cname, pyname):

@@ -17,12 +17,15 @@ Contents (plain PyTorch CPU ops, fp32 or fp64, autograd for the backward):
                       e4e ``models/psp.py``; no version pin exists in the reference). Its published
                       algorithm is restated here. **Parity unpinned**: no reference test or fixture
                       holds generator outputs; property tests only.
-* ``encoder_ref``   — the synthetic linear encoder that stands in for e4e. Parity
-                      unpinned (it is the build's own definition).
+* ``encoder_ref``   — the e4e ``Encoder4Editing(50, 'ir_se')`` restatement (un-vendored omertov
+                      encoder4editing, no version pin: parity unpinned) and the synthetic linear
+                      encoder of SURVEY.md §7 (the build's own definition).
 * ``attack_ref``    — the white-box objective of ``code/attack/interpolation.py:786-818`` and the
                       torchattacks PGD update rule copied in comments at
                       ``code/attack/interpolation.py:62-96``, the Adam pixel mode of
                       ``optimize_vgg`` (``:767,822``) and the torchattacks C&W rule
                       (``:98-193``) composed with the GAN objective (torchattacks is un-vendored
-                      and unpinned). Parity unpinned beyond the VGG part.
+                      and unpinned). The objective and the Adam mode are **pinned** to the
+                      reference's own ``optimize_vgg`` executed in the build container
+                      (``oracle/gen_golden_objective.py`` → ``tests/golden/objective_golden.npz``).
 """

@@ -53,7 +53,7 @@ struct HaloX6 {
   static_assert(LDS <= 160 * 1024, "");
 };
 
-template <int BN_, bool PRO, int EPI>
+template <int BN_, bool PRO, int EPI, bool EARLY>
 __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const ConvK k) {
   typedef HaloX6<BN_> TL;
   constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, NT = TL::NT, BN = TL::BN, BK = TL::BK;
@@ -190,6 +190,22 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
     const char* sb = bring + st * BSTAGE;
     const int dy = t >= 6 ? 2 : (t >= 3 ? 1 : 0), dx = t - 3 * dy;
     if (bwave && s + 1 < nk) issue_b(s + 1, st ^ 1);
+    if constexpr (EARLY) {
+      // H-waves: the next block's halo pieces of this tap before the step's LDS reads, so both
+      // MFMA halves and their fragment reads form one scheduling region
+      if (!bwave && cb + 1 < ncb) {
+#pragma unroll
+        for (int tt = 0; tt < (H_INS + HPS - 1) / HPS; ++tt) {
+          if (t == tt) {
+#pragma unroll
+            for (int q = 0; q < HPS; ++q) {
+              const int j = tt * HPS + q;
+              if (j < H_INS && j < my_pieces) issue_h(cb + 1, j, (cb + 1) & 1);
+            }
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int ch = h * 4 + fq;  // this lane's logical 16-B quad of the K-step (k = 4·ch …)
@@ -213,7 +229,7 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
         for (int j = 0; j < FN; ++j)
           acc[i][j] = EPI != -2 ? mfma_x6(bhm[j], blo[j], ahm[i], al[i], acc[i][j])  // D[ch][px]
                                 : mfma_x6(ahm[i], al[i], bhm[j], blo[j], acc[i][j]);  // D[px][ch]
-      if (h == 0 && !bwave && cb + 1 < ncb) {
+      if (!EARLY && h == 0 && !bwave && cb + 1 < ncb) {
         // H-waves: the next block's halo between the two MFMA halves, HPS pieces per tap 0–3
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -255,15 +271,15 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
   }
 }
 
-template <int BN_, bool PRO, int EPI>
-static int launch_x6_(ConvK& k, hipStream_t st) {
+template <int BN_, bool PRO, int EPI, bool EARLY>
+static int launch_x6_e(ConvK& k, hipStream_t st) {
   typedef HaloX6<BN_> TL;
   k.nbn = (k.a.Cout + TL::BN - 1) / TL::BN;
   k.nblk = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW) * k.nbn;
   size_t lds = TL::LDS;
   lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
   lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
-  auto fn = conv_halo_x6_kernel<BN_, PRO, EPI>;
+  auto fn = conv_halo_x6_kernel<BN_, PRO, EPI, EARLY>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -274,6 +290,13 @@ static int launch_x6_(ConvK& k, hipStream_t st) {
   k.prered = prered_enabled() && EPI >= 0 && (EPI & epi::CSUM);
   hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), lds, st, k);
   return check_launch("conv_halo_x6");
+}
+
+template <int BN_, bool PRO, int EPI>
+static int launch_x6_(ConvK& k, hipStream_t st) {
+  const char* e = getenv("MIA_X6_EARLY");  // A/B: halo DMA at the step start (1) or mid-step (0)
+  if (e && atoi(e) == 1) return launch_x6_e<BN_, PRO, EPI, true>(k, st);
+  return launch_x6_e<BN_, PRO, EPI, false>(k, st);
 }
 
 // Eligible: fp32 with pre-split weights (mia_conv_args.w_split / mia_conv_group.w_split), one

@@ -427,7 +427,7 @@ struct DgX6 {
   static_assert(LDS <= 160 * 1024, "");
 };
 
-template <bool DG, bool PRO>
+template <bool DG, bool PRO, bool EARLY>
 __global__ __launch_bounds__(DgX6::NT, 1) void upconv_x6_kernel(const UpK k) {
   typedef DgX6 TL;
   constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, BN = TL::BN, BK = TL::BK, NT = TL::NT;
@@ -572,6 +572,15 @@ __global__ __launch_bounds__(DgX6::NT, 1) void upconv_x6_kernel(const UpK k) {
       const char* sb = bring + (s & 1) * BSTAGE;
       if (bwave && s + 1 < nk) issue_b(s + 1, (s & 1) ^ 1);
       const int jy = up_jy(st), jx = up_jx(st);
+      if constexpr (EARLY) {  // the next block's halo pieces before the step's LDS reads
+        if (!bwave && st < 4 && cb + 1 < ncb) {
+#pragma unroll
+          for (int q = 0; q < HPS; ++q) {
+            const int j = st * HPS + q;
+            if (j < H_INS && hw + HWAVES * j < HPIECES) issue_h(cb + 1, j, (cb + 1) & 1);
+          }
+        }
+      }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int ch = h * 4 + fq;  // this lane's logical 16-B quad of the K-step
@@ -602,7 +611,7 @@ __global__ __launch_bounds__(DgX6::NT, 1) void upconv_x6_kernel(const UpK k) {
             for (int j = 0; j < FN; ++j)  // D[channel][pixel]
               acc[ph][i][j] = mfma_x6(bhm[j], blo[j], ahm[i], al[i], acc[ph][i][j]);
         }
-        if (h == 0 && !bwave && st < 4 && cb + 1 < ncb) {
+        if (!EARLY && h == 0 && !bwave && st < 4 && cb + 1 < ncb) {
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int q = 0; q < HPS; ++q) {
@@ -664,12 +673,12 @@ __global__ __launch_bounds__(DgX6::NT, 1) void upconv_x6_kernel(const UpK k) {
   }
 }
 
-template <bool DG, bool PRO>
-static int launch_upconv_x6(UpK& k, hipStream_t st) {
+template <bool DG, bool PRO, bool EARLY>
+static int launch_upconv_x6_e(UpK& k, hipStream_t st) {
   typedef DgX6 TL;
   k.nbn = k.Cout / TL::BN;
   k.nblk = k.N * (k.R / TL::PH) * (k.R / TL::PW) * k.nbn;
-  auto fn = upconv_x6_kernel<DG, PRO>;
+  auto fn = upconv_x6_kernel<DG, PRO, EARLY>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -679,6 +688,13 @@ static int launch_upconv_x6(UpK& k, hipStream_t st) {
   }
   hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), TL::LDS, st, k);
   return check_launch("upconv_x6");
+}
+
+template <bool DG, bool PRO>
+static int launch_upconv_x6(UpK& k, hipStream_t st) {
+  const char* e = getenv("MIA_X6_EARLY");  // A/B: halo DMA at the step start (1) or mid-step (0)
+  if (e && atoi(e) == 1) return launch_upconv_x6_e<DG, PRO, true>(k, st);
+  return launch_upconv_x6_e<DG, PRO, false>(k, st);
 }
 
 // the split-once kernel: fp32 with pre-split weights, R % 16 == 0, Cx % 64 == 0 (MIA_S2DG_X6=0

@@ -294,8 +294,10 @@ static int launch_x6_e(ConvK& k, hipStream_t st) {
 
 template <int BN_, bool PRO, int EPI>
 static int launch_x6_(ConvK& k, hipStream_t st) {
-  const char* e = getenv("MIA_X6_EARLY");  // A/B: halo DMA at the step start (1) or mid-step (0)
-  if (e && atoi(e) == 1) return launch_x6_e<BN_, PRO, EPI, true>(k, st);
+  // the next block's halo DMA at the step start (default; measured +2-3 % on the stride-1 layers,
+  // neutral on the up-conv) or between the two MFMA halves (MIA_X6_EARLY=0, A/B)
+  const char* e = getenv("MIA_X6_EARLY");
+  if (!e || atoi(e) != 0) return launch_x6_e<BN_, PRO, EPI, true>(k, st);
   return launch_x6_e<BN_, PRO, EPI, false>(k, st);
 }
 

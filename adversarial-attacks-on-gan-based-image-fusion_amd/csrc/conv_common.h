@@ -33,6 +33,7 @@ struct ConvK {
                                  // measured, the extra barrier costs more than it saves for the
                                  // sdot / q sums of the StyledConv dgrads (MIA_EPI_PRERED=0: off)
   int batched;                   // groups carry image / channel offsets: LDS-staged epilogue only
+  int prio;                      // X6B tile: s_setprio(1) around the MFMA blocks
   ConvGroup g[MIA_MAX_GROUPS];
 };
 

@@ -53,7 +53,7 @@ struct HaloX6 {
   static_assert(LDS <= 160 * 1024, "");
 };
 
-template <int BN_, bool PRO, int EPI, bool EARLY>
+template <int BN_, bool PRO, int EPI, bool EARLY, bool PRIO>
 __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const ConvK k) {
   typedef HaloX6<BN_> TL;
   constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, NT = TL::NT, BN = TL::BN, BK = TL::BK;
@@ -223,12 +223,14 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
         bhm[j] = *(const u32x4*)(sb + row * ROWB + ((ch ^ fsw(row)) << 4));
         blo[j] = *(const u32x2*)(sb + TL::BHM + row * TL::LROWB + ((ch ^ lsw(row)) << 3));
       }
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = EPI != -2 ? mfma_x6(bhm[j], blo[j], ahm[i], al[i], acc[i][j])  // D[ch][px]
                                 : mfma_x6(ahm[i], al[i], bhm[j], blo[j], acc[i][j]);  // D[px][ch]
+      if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
       if (!EARLY && h == 0 && !bwave && cb + 1 < ncb) {
         // H-waves: the next block's halo between the two MFMA halves, HPS pieces per tap 0–3
         __builtin_amdgcn_sched_barrier(0);
@@ -271,7 +273,7 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
   }
 }
 
-template <int BN_, bool PRO, int EPI, bool EARLY>
+template <int BN_, bool PRO, int EPI, bool EARLY, bool PRIO = false>
 static int launch_x6_e(ConvK& k, hipStream_t st) {
   typedef HaloX6<BN_> TL;
   k.nbn = (k.a.Cout + TL::BN - 1) / TL::BN;
@@ -279,7 +281,7 @@ static int launch_x6_e(ConvK& k, hipStream_t st) {
   size_t lds = TL::LDS;
   lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
   lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
-  auto fn = conv_halo_x6_kernel<BN_, PRO, EPI, EARLY>;
+  auto fn = conv_halo_x6_kernel<BN_, PRO, EPI, EARLY, PRIO>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -296,8 +298,14 @@ template <int BN_, bool PRO, int EPI>
 static int launch_x6_(ConvK& k, hipStream_t st) {
   // the next block's halo DMA at the step start (default; measured +2-3 % on the stride-1 layers,
   // neutral on the up-conv) or between the two MFMA halves (MIA_X6_EARLY=0, A/B)
+  // + s_setprio(1) around each MFMA block (default; +1-4 %; MIA_X6_PRIO=0 disables): the wave in
+  // its MFMA phase keeps issue priority over the co-resident wave's LDS reads
   const char* e = getenv("MIA_X6_EARLY");
-  if (!e || atoi(e) != 0) return launch_x6_e<BN_, PRO, EPI, true>(k, st);
+  const char* pe = getenv("MIA_X6_PRIO");
+  const bool prio = !pe || atoi(pe) != 0;
+  if (!e || atoi(e) != 0)
+    return prio ? launch_x6_e<BN_, PRO, EPI, true, true>(k, st)
+                : launch_x6_e<BN_, PRO, EPI, true, false>(k, st);
   return launch_x6_e<BN_, PRO, EPI, false>(k, st);
 }
 

@@ -257,12 +257,14 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
         }
 #pragma unroll
         for (int i = 0; i < FM; ++i) split_quad(af[i], ahm[i], alo[i]);
+        if (k.prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
             acc[i][j] = EPI == -2 ? mfma_x6(ahm[i], alo[i], bhm[j], blo[j], acc[i][j])
                                   : mfma_x6(bhm[j], blo[j], ahm[i], alo[i], acc[i][j]);
+        if (k.prio) __builtin_amdgcn_s_setprio(0);
         continue;
       }
 #pragma unroll
@@ -340,6 +342,10 @@ static int launch_tile(ConvK& k, hipStream_t st) {
     attr_set = true;
   }
   k.prered = prered_enabled() && EPI >= 0 && (EPI & epi::CSUM);
+  // X6B: s_setprio(1) around the MFMA blocks measured 1-2 % slower on this 2-blocks-per-CU tile;
+  // off unless MIA_X6B_PRIO=1 (A/B)
+  const char* pe = getenv("MIA_X6B_PRIO");
+  k.prio = pe && atoi(pe) != 0;
   hipLaunchKernelGGL(fn, dim3(blk), dim3(TL::NT), lds, st, k);
   return check_launch("conv");
 }

@@ -427,7 +427,7 @@ struct DgX6 {
   static_assert(LDS <= 160 * 1024, "");
 };
 
-template <bool DG, bool PRO, bool EARLY>
+template <bool DG, bool PRO, bool EARLY, bool PRIO>
 __global__ __launch_bounds__(DgX6::NT, 1) void upconv_x6_kernel(const UpK k) {
   typedef DgX6 TL;
   constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, BN = TL::BN, BK = TL::BK, NT = TL::NT;
@@ -605,11 +605,13 @@ __global__ __launch_bounds__(DgX6::NT, 1) void upconv_x6_kernel(const UpK k) {
             bhm[j] = *(const u32x4*)(sb + row * ROWB + ((ch ^ fsw(row)) << 4));
             blo[j] = *(const u32x2*)(sb + TL::BHM + row * TL::LROWB + ((ch ^ lsw(row)) << 3));
           }
+          if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int i = 0; i < FM; ++i)
 #pragma unroll
             for (int j = 0; j < FN; ++j)  // D[channel][pixel]
               acc[ph][i][j] = mfma_x6(bhm[j], blo[j], ahm[i], al[i], acc[ph][i][j]);
+          if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
         }
         if (!EARLY && h == 0 && !bwave && st < 4 && cb + 1 < ncb) {
           __builtin_amdgcn_sched_barrier(0);
@@ -673,12 +675,12 @@ __global__ __launch_bounds__(DgX6::NT, 1) void upconv_x6_kernel(const UpK k) {
   }
 }
 
-template <bool DG, bool PRO, bool EARLY>
+template <bool DG, bool PRO, bool EARLY, bool PRIO>
 static int launch_upconv_x6_e(UpK& k, hipStream_t st) {
   typedef DgX6 TL;
   k.nbn = k.Cout / TL::BN;
   k.nblk = k.N * (k.R / TL::PH) * (k.R / TL::PW) * k.nbn;
-  auto fn = upconv_x6_kernel<DG, PRO, EARLY>;
+  auto fn = upconv_x6_kernel<DG, PRO, EARLY, PRIO>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -695,8 +697,14 @@ static int launch_upconv_x6(UpK& k, hipStream_t st) {
   // the next block's halo DMA at the step start (default; measured +2-3 % on the stride-1 layers,
   // neutral on the up-conv) or between the two MFMA halves (MIA_X6_EARLY=0, A/B)
   const char* e = getenv("MIA_X6_EARLY");
-  if (!e || atoi(e) != 0) return launch_upconv_x6_e<DG, PRO, true>(k, st);
-  return launch_upconv_x6_e<DG, PRO, false>(k, st);
+  // s_setprio(1) around the MFMA blocks: neutral here (+1 / −1 % by layer), off unless
+  // MIA_UPX6_PRIO=1 (A/B)
+  const char* pe = getenv("MIA_UPX6_PRIO");
+  const bool prio = pe && atoi(pe) != 0;
+  if (!e || atoi(e) != 0)
+    return prio ? launch_upconv_x6_e<DG, PRO, true, true>(k, st)
+                : launch_upconv_x6_e<DG, PRO, true, false>(k, st);
+  return launch_upconv_x6_e<DG, PRO, false, false>(k, st);
 }
 
 // the split-once kernel: fp32 with pre-split weights, R % 16 == 0, Cx % 64 == 0 (MIA_S2DG_X6=0

@@ -43,6 +43,7 @@ from .weights import (E4E_COARSE, E4E_MIDDLE, E4E_SE_REDUCTION, STYLE_DIM, e4e_s
                       e4e_units, n_latent_for)
 
 BN_EPS = 1e-5
+BATCH_MAX = 16  # groups per mia_conv2d_batched launch
 
 
 def _bn_fold(p, pre):
@@ -179,7 +180,8 @@ class E4EEncoder:
                    if hd["res"][j - 1] == r_in]
             bcat = torch.cat([self.heads[i]["convs"][j]["b"] for i, j in mem]).contiguous()
             self.levels.append((r_in, _s2_out(r_in), mem, bcat))
-        self.slope_cat = torch.full((16 * STYLE_DIM,), 0.01, dtype=f32, device=dev)
+        self.slope_cat = torch.full((max(16, self.n_latent) * STYLE_DIM,), 0.01, dtype=f32,
+                                    device=dev)
         # the heads whose first conv reads the same FPN map (7 on p1, 4 on p2): their first-conv
         # input gradients run as ONE multi-source launch with the packed matrices concatenated
         # along K (mia_conv_s2_dgrad_halo_multi) — one write of the source gradient instead of
@@ -188,8 +190,11 @@ class E4EEncoder:
         for src in ("c3", "p2", "p1"):
             idx = [i for i, hd in enumerate(self.heads) if hd["src"] == src]
             if len(idx) > 1 and all(self.heads[i]["convs"][0]["wdh"] is not None for i in idx):
-                self.src_heads[src] = (idx, torch.cat([self.heads[i]["convs"][0]["wdh"]
-                                                       for i in idx]).contiguous())
+                # ≤ 8 source tensors per launch (11 fine heads at 1024²: two launches)
+                self.src_heads[src] = [
+                    (idx[c:c + 8], torch.cat([self.heads[i]["convs"][0]["wdh"]
+                                              for i in idx[c:c + 8]]).contiguous())
+                    for c in range(0, len(idx), 8)]
         # w = w0 + delta_i: the linear biases of rows i ≥ 1 include style 0's; the backward of
         # style 0 reads the sum of every row (mia_sum_slices)
         b0l = self.heads[0]["lb"]
@@ -308,10 +313,11 @@ class E4EEncoder:
             groups = [dict(_g3(self.heads[i]["convs"][j]["w"], r_out),
                            n_in=self.slot[r_in][i] * N, n_out=self.slot[r_out][i] * N,
                            c_off=k * STYLE_DIM) for k, (i, j) in enumerate(mem)]
-            ops.conv2d_batched(self._level_buf(ws, "a", r_in, N), groups,
-                               self._level_buf(ws, "a", r_out, N), (r_out, r_out), n=N,
-                               cout=STYLE_DIM, stride=2, bias=bcat, act_out=ACT_PRELU,
-                               act_slope=self.slope_cat)
+            for c in range(0, len(groups), BATCH_MAX):  # ≤ 16 groups per launch (18 heads at 1024²)
+                ops.conv2d_batched(self._level_buf(ws, "a", r_in, N), groups[c:c + BATCH_MAX],
+                                   self._level_buf(ws, "a", r_out, N), (r_out, r_out), n=N,
+                                   cout=STYLE_DIM, stride=2, bias=bcat, act_out=ACT_PRELU,
+                                   act_slope=self.slope_cat)
         for i, hd in enumerate(self.heads):
             if hd["res"][-1] != 1:
                 raise ValueError("GradualStyleBlock must end at 1×1 (encoder input R = 256)")
@@ -402,12 +408,14 @@ class E4EEncoder:
                     if pg:
                         groups.append(dict(pg[0], n_in=self.slot[r_out][i] * N,
                                            n_out=self.slot[r_in][i] * N, c_off=k * STYLE_DIM))
-                if groups:
-                    ops.conv2d_batched(gin, groups, gout, (r_in, r_in), n=N, cout=STYLE_DIM,
-                                       mask_a=mask, mask_slope=self.slope_cat)
+                for c in range(0, len(groups), BATCH_MAX):
+                    ops.conv2d_batched(gin, groups[c:c + BATCH_MAX], gout, (r_in, r_in), n=N,
+                                       cout=STYLE_DIM, mask_a=mask, mask_slope=self.slope_cat)
         seen = set()
-        for src, (idx, wcat) in self.src_heads.items():
-            ops.s2_dgrad_halo([self._head_view(ws, "g", i, 0, N) for i in idx], wcat, gfeat[src])
+        for src, chunks in self.src_heads.items():
+            for c, (idx, wcat) in enumerate(chunks):
+                ops.s2_dgrad_halo([self._head_view(ws, "g", i, 0, N) for i in idx], wcat,
+                                  gfeat[src], accumulate=c > 0)
             seen.add(src)
         for i in reversed(range(self.n_latent)):
             hd = self.heads[i]

@@ -35,8 +35,12 @@
 
 namespace mia {
 
-struct HaloUp {
-  static constexpr int PH = 8, PW = 16, WM = 2, WN = 2, FM = 4, FN = 2, NW = 4, NT = 256;
+// BN_ = 64 output channels per block (2 row waves × 2 column waves of 4 × 2 fragments) or 32
+// (the 32-channel up-conv of the 1024² generator: 4 row waves × 1 column wave of 2 × 2 fragments)
+template <int BN_>
+struct HaloUpT {
+  static constexpr int PH = 8, PW = 16, NW = 4, NT = 256;
+  static constexpr int WN = BN_ == 64 ? 2 : 1, WM = NW / WN, FM = PH / WM, FN = 2;
   static constexpr int BN = WN * FN * 16;                       // output channels per block
   static constexpr int HSIDE = PW + 1, HROWS = (PH + 1) * HSIDE;  // 153 halo pixels
   static constexpr int HPIECES = (HROWS + 7) / 8;               // 20 pieces of 8 rows
@@ -48,7 +52,9 @@ struct HaloUp {
   static constexpr int HPS = (H_INS + 3) / 4;                   // issued during steps 0–3
   static constexpr int NSTEP = 5, STAGES = 2;
   static_assert(B_INS * 8 * BWAVES == BROWS && H_INS * HWAVES == HPIECES, "");
+  static_assert(WM * FM == PH && WN * FN * 16 == BN_, "");
 };
+typedef HaloUpT<64> HaloUp;
 
 // K-step st: offset (jy, jx) and the phases of its two weight slots (−1: none)
 __device__ __forceinline__ constexpr int up_jy(int st) { return st == 3 || st == 4 ? 1 : 0; }
@@ -83,9 +89,9 @@ __device__ __forceinline__ const char* up_src(const UpK& k, int i) {
   return (const char*)p;
 }
 
-template <typename T, bool PRO, bool DG>
+template <typename T, bool PRO, bool DG, int BN_ = 64>
 __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
-  typedef HaloUp TL;
+  typedef HaloUpT<BN_> TL;
   typedef typename Vec<T>::type VT;
   constexpr int VEC = Vec<T>::N, BK = ROWB / (int)sizeof(T);  // elements per chunk / per row
   constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, BN = TL::BN, PH = TL::PH, PW = TL::PW;
@@ -342,15 +348,15 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
   }  // 2-byte epilogue
 }
 
-template <typename T, bool PRO, bool DG = false>
+template <typename T, bool PRO, bool DG = false, int BN_ = 64>
 static int launch_upconv_halo(UpK& k, hipStream_t st) {
-  typedef HaloUp TL;
+  typedef HaloUpT<BN_> TL;
   k.nbn = k.Cout / TL::BN;
   k.nblk = k.N * (k.R / TL::PH) * (k.R / TL::PW) * k.nbn;
   size_t lds = 2 * (size_t)TL::HBUF + (size_t)TL::STAGES * TL::BSTAGE;
   if (PRO) lds += (size_t)k.Cin * sizeof(T);
   if (lds > 160 * 1024) return set_error("upconv_halo: LDS budget exceeded");
-  auto fn = upconv_halo_kernel<T, PRO, DG>;
+  auto fn = upconv_halo_kernel<T, PRO, DG, BN_>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -365,7 +371,7 @@ static int launch_upconv_halo(UpK& k, hipStream_t st) {
 bool upconv_halo_eligible(int dtype, int R, int Cin, int Cout) {
   const char* e = getenv("MIA_UPCONV_HALO");  // tuning / A-B switch: 0 = generic phase GEMMs
   if (e && atoi(e) == 0) return false;
-  return R % 16 == 0 && Cin % 64 == 0 && Cout % HaloUp::BN == 0 &&
+  return R % 16 == 0 && Cin % 64 == 0 && Cout % 32 == 0 &&
          (int64_t)(2 * R + 1) * (2 * R + 1) < (1LL << 31);
 }
 
@@ -384,6 +390,12 @@ int launch_upconv_halo(const void* x, const void* w_up, const void* w_up_split, 
   const bool pro = style != nullptr || act_in != MIA_ACT_NONE;
   if (upconv_x6_ok(k, dtype))
     return pro ? launch_upconv_x6<false, true>(k, st) : launch_upconv_x6<false, false>(k, st);
+  if (Cout % 64) {  // the 32-channel tile (1024² generator: 64 → 32 at 512²)
+    MIA_DISPATCH_DTYPE(dtype, T, {
+      return pro ? launch_upconv_halo<T, true, false, 32>(k, st)
+                 : launch_upconv_halo<T, false, false, 32>(k, st);
+    });
+  }
   MIA_DISPATCH_DTYPE(dtype, T, {
     return pro ? launch_upconv_halo<T, true, false>(k, st)
                : launch_upconv_halo<T, false, false>(k, st);

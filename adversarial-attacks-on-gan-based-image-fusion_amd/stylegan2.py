@@ -58,7 +58,7 @@ class SynthesisNet:
             if c["up"] and up_mode == "subpixel":
                 L["wph"] = [m.contiguous().to(dev)
                             for m in layouts.upconv_subpixel_matrices(ws, dtype)]
-                if cin % 64 == 0 and cout % 64 == 0:
+                if cin % 64 == 0 and cout % 32 == 0:  # halo up-conv tiles of 64 / 32 channels
                     L["wup"] = layouts.upconv_halo_matrix(ws, dtype).contiguous().to(dev)
                 L["wd"] = layouts.upconv_dgrad_matrix(ws, dtype).contiguous().to(dev)
             elif c["up"]:

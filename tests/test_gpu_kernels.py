@@ -647,7 +647,7 @@ def test_conv_thin_vgg_input_layer(cuda, monkeypatch, dtype, N, H, W, thin, e4e)
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("N,cin,cout,R", [(2, 64, 64, 16), (1, 128, 192, 32), (2, 256, 128, 16),
-                                          (1, 64, 64, 8)])
+                                          (1, 64, 64, 8), (2, 64, 32, 32), (1, 128, 96, 16)])
 @pytest.mark.parametrize("lrelu_in", [False, True])
 @pytest.mark.parametrize("x6", ["1", "0"])
 def test_upconv_halo_fwd(cuda, monkeypatch, dtype, N, cin, cout, R, lrelu_in, x6):

@@ -309,6 +309,12 @@ static int launch_x6_(ConvK& k, hipStream_t st) {
   return launch_x6_e<BN_, PRO, EPI, false>(k, st);
 }
 
+// MIA_X6_64AUX=1: the 64-column tile also for launches with per-pixel aux operands (A/B)
+static bool x6_64_aux() {
+  const char* e = getenv("MIA_X6_64AUX");
+  return e && atoi(e) != 0;
+}
+
 // Eligible: fp32 with pre-split weights (mia_conv_args.w_split / mia_conv_group.w_split), one
 // group, stride 1, 3×3 pad 1, identity placement, 16-divisible maps, Cin % 32 == 0, Cout ≥ 64.
 bool conv_halo_x6_eligible(const ConvK& k, int dtype) {
@@ -328,7 +334,8 @@ bool conv_halo_x6_eligible(const ConvK& k, int dtype) {
          // 64 channels: the 64-column tile, where the epilogue reads no per-pixel aux tensor
          // (with tap / mask / accumulate operands it measured 6–9 % slower than the generic
          // tile: one block per CU leaves that epilogue exposed; without them 2–11 % faster)
-         (a.Cout > 64 || (a.Cout == 64 && !a.tap_a && !a.mask_a && !a.accumulate));
+         (a.Cout > 64 || (a.Cout == 64 && ((!a.tap_a && !a.mask_a && !a.accumulate) ||
+                                            x6_64_aux())));
 }
 
 int launch_conv_halo_x6(ConvK& k, hipStream_t st) {

@@ -80,10 +80,26 @@ def test_patch_attack_e4e_first_step_branch_forced(cuda):
     net = networks.build_net(S, seed=0, device=cuda, encoder="e4e")
     img = seeded(6, (N, 3, S, S)) * 0.9
     patch, mask = _square(N, S, 64, 100, 30)
-    _, _, p, _ = gfa_amd.patch_attack(img.to(cuda), patch.to(cuda), mask.to(cuda), net, 1)
+    # the branches of the gradient pass's own forward (the 3rd encoder forward: prepare encodes
+    # t and x0 first; the final rec pass re-encodes the same composite, but the fp32 forward is
+    # not bit-deterministic — the SE channel sums are block atomics — so a few near-zero
+    # activations may take the other branch there)
+    enc = net.encoder.impl
+    seen = []
+    fwd = enc.forward_nhwc
+
+    def capture(xin, ws, tag="e"):
+        lat = fwd(xin, ws, tag)
+        seen.append(e4e_masks(enc))
+        return lat
+    enc.forward_nhwc = capture
+    try:
+        _, _, p, _ = gfa_amd.patch_attack(img.to(cuda), patch.to(cuda), mask.to(cuda), net, 1)
+    finally:
+        del enc.forward_nhwc
+    assert len(seen) == 4, len(seen)
+    masks = seen[2]
     gp, vp, ep = to64(_params(net))
-    # the encoder's last forward is at the composite (the final rec pass re-encodes it)
-    masks = e4e_masks(net.encoder.impl)
     _, p_ref, _ = attack_ref.patch_attack(gp, vp, ep, img.double(), patch.double(),
                                           mask.double(), img.double(), S, 1, dtype=torch.float64,
                                           grad_ctx=lambda: encoder_ref.forced_masks(masks))

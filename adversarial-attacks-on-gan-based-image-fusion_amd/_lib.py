@@ -150,6 +150,8 @@ SIGNATURES = {
                                              c_int, c_int, P]),
     "mia_se_fwd": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
     "mia_se_apply": (c_int, [P, P, P, c_int, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "mia_chan_sum_parts": (c_int, [c_int, c_int]),
+    "mia_chan_sum": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_chan_dot": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_se_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
     "mia_se_grad_scale": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P]),

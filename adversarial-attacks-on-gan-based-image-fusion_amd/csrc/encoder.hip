@@ -158,6 +158,68 @@ __global__ __launch_bounds__(256) void chan_dot_kernel(const T* __restrict__ a,
   }
 }
 
+// ---- deterministic per-(image, channel) sums: Σ_p a·b (DOT) or Σ_p a over the pixels ------------
+// chunk q of image n writes its partial to part[(n·nch + q)·C + c] (a fixed-order reduction inside
+// the block), then chan_fin adds the nch partials in order: bit-reproducible run to run, unlike
+// atomics across blocks (the SE average pool feeds PReLU / ReLU branches downstream).
+template <typename T, bool DOT>
+__global__ __launch_bounds__(256) void chan_part_kernel(const T* __restrict__ a,
+                                                        const T* __restrict__ b,
+                                                        float* __restrict__ part, int HW, int C,
+                                                        int pix_per_chunk) {
+  __shared__ float red[256 * 8];
+  const int n = blockIdx.y, tid = threadIdx.x;
+  const int cv = C / 8;
+  const int lanes_per_pix = cv < 256 ? cv : 256;
+  const int pr = 256 / lanes_per_pix;
+  const int vc = tid % lanes_per_pix, pl = tid / lanes_per_pix;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  const int p0 = blockIdx.x * pix_per_chunk, p1 = min(HW, p0 + pix_per_chunk);
+  if (pl < pr) {
+    for (int pix = p0 + pl; pix < p1; pix += pr) {
+      for (int c8 = vc; c8 < cv; c8 += lanes_per_pix) {
+        float va[8], vb[8];
+        const size_t off = ((size_t)n * HW + pix) * C + c8 * 8;
+        load8<T>(a + off, va);
+        if constexpr (DOT) {
+          load8<T>(b + off, vb);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] += va[e] * vb[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[e] += va[e];
+        }
+      }
+    }
+  }
+  // (C > 2048 is rejected: every channel chunk c8 < cv maps to one lane, lanes_per_pix = cv)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[tid * 8 + e] = acc[e];
+  __syncthreads();
+  if (tid < lanes_per_pix) {
+    float* dst = part + ((size_t)n * gridDim.x + blockIdx.x) * C + tid * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float s = 0.f;
+      for (int q = 0; q < pr; ++q) s += red[(q * lanes_per_pix + tid) * 8 + e];
+      dst[e] = s;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void chan_fin_kernel(const float* __restrict__ part,
+                                                       float* out, int N, int C, int nch,
+                                                       int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i - (i / C) * C;
+  float s = accumulate ? out[i] : 0.f;
+  for (int q = 0; q < nch; ++q) s += part[((size_t)n * nch + q) * C + c];
+  out[i] = s;
+}
+
 // ---- g_r = gamma·(g_out·s + gavg) ----------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void se_grad_scale_kernel(const T* __restrict__ go,
@@ -399,6 +461,38 @@ extern "C" int mia_chan_dot(const void* a, const void* b, float* gs, int N, int 
   MIA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(chan_dot_kernel<T>, dim3(nch, N), dim3(256), 0,
                                                   st, (const T*)a, (const T*)b, gs, HW, C, ppc));
   return check_launch("chan_dot");
+}
+
+static int chan_chunks(int N, int HW) { return std::max(1, std::min(HW / 16, 4096 / N + 1)); }
+
+extern "C" int mia_chan_sum_parts(int N, int HW) {
+  const int chunks = chan_chunks(N, HW);
+  const int ppc = (HW + chunks - 1) / chunks;
+  return (HW + ppc - 1) / ppc;
+}
+
+extern "C" int mia_chan_sum(const void* a, const void* b, float* part, float* out, int N, int HW,
+                            int C, int accumulate, int dtype, void* stream) {
+  MIA_CHECK_ARG(a && part && out && N > 0 && HW > 0, "bad args");
+  ENC_CHECK_C(C);
+  MIA_CHECK_ARG(C <= 2048, "C ≤ 2048");
+  hipStream_t st = (hipStream_t)stream;
+  const int chunks = chan_chunks(N, HW);
+  const int ppc = (HW + chunks - 1) / chunks;
+  const int nch = (HW + ppc - 1) / ppc;
+  MIA_DISPATCH_DTYPE(dtype, T, {
+    if (b)
+      hipLaunchKernelGGL((chan_part_kernel<T, true>), dim3(nch, N), dim3(256), 0, st,
+                         (const T*)a, (const T*)b, part, HW, C, ppc);
+    else
+      hipLaunchKernelGGL((chan_part_kernel<T, false>), dim3(nch, N), dim3(256), 0, st,
+                         (const T*)a, (const T*)nullptr, part, HW, C, ppc);
+  });
+  const int rc = check_launch("chan_part");
+  if (rc) return rc;
+  hipLaunchKernelGGL(chan_fin_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, part, out, N, C,
+                     nch, accumulate);
+  return check_launch("chan_fin");
 }
 
 extern "C" int mia_se_grad_scale(const void* g_out, const float* s, const float* gavg,

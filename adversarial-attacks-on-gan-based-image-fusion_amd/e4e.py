@@ -201,6 +201,15 @@ class E4EEncoder:
         self.lin_bias = [b0l] + [(h["lb"] + b0l).contiguous() for h in self.heads[1:]]
         self.flops_fwd_per_image = self._count_flops()
 
+    def _chan_part(self, ws, N, hw, c):
+        """fp32 scratch of ops.chan_sum (one buffer, sized for the largest user)."""
+        need = N * ops.chan_sum_parts(N, hw) * c
+        buf = ws.cache.get("e.chan_part")
+        if buf is None or buf.numel() < need:
+            buf = torch.empty(need, dtype=torch.float32, device=self.device)
+            ws.cache["e.chan_part"] = buf
+        return buf
+
     def _level_buf(self, ws, kind, r, N):
         """Stacked head activations ('a') or their gradients ('g') at resolution r."""
         return self._buf(ws, f"h{kind}{r}", (len(self.slot[r]) * N, r, r, STYLE_DIM))
@@ -267,9 +276,12 @@ class E4EEncoder:
             ops.conv2d(xb, [_g3(U["w1"], h)], a1, (h, h), cout=d, act_out=ACT_PRELU,
                        act_slope=U["slope"])
             r = self._buf(ws, f"r_{i}", (N, ho, ho, d))
-            cs = ops.zero_(self._buf(ws, f"cs_{i}", (N, d), f32))
-            ops.conv2d(a1, [_g3(U["w2"], ho)], r, (ho, ho), cout=d, stride=s, bias=U["b2"],
-                       csum=cs)
+            cs = self._buf(ws, f"cs_{i}", (N, d), f32)
+            ops.conv2d(a1, [_g3(U["w2"], ho)], r, (ho, ho), cout=d, stride=s, bias=U["b2"])
+            # the SE average pool's sum: a deterministic reduction (not the conv epilogue's block
+            # atomics), so the forward — and the PReLU / ReLU branches after it — reproduce bit
+            # for bit run to run
+            ops.chan_sum(r, None, self._chan_part(ws, N, ho * ho, d), cs)
             u = self._buf(ws, f"u_{i}", (N, U["cr"]), f32)
             sv = self._buf(ws, f"s_{i}", (N, d), f32)
             ops.se_fwd(cs, U["se_w1"], U["se_w2"], u, sv, ho * ho)
@@ -446,7 +458,8 @@ class E4EEncoder:
             u = U[i]
             d, s, cin = u["depth"], u["stride"], u["cin"]
             h = u["_a1"].shape[1]
-            gs = ops.chan_dot(Gc, u["_r"], self._buf(ws, "gs", (N, d), f32))
+            gs = ops.chan_sum(Gc, u["_r"], self._chan_part(ws, N, u["_hw"], d),
+                              self._buf(ws, "gs", (N, d), f32))
             gavg = ops.se_bwd(gs, u["_s"], u["_u"], u["se_w1"], u["se_w2"],
                               self._buf(ws, "gavg", (N, d), f32), u["_hw"])
             g_r = ops.se_grad_scale(Gc, u["_s"], gavg, self._buf(ws, f"g_r{d}", Gc.shape))

@@ -836,6 +836,25 @@ def chan_dot(a, b, gs, accumulate=False):
     return gs
 
 
+def chan_sum_parts(N, HW):
+    """Chunks per image of mia_chan_sum (host-side helper of the library, no device work)."""
+    return _lib.load().mia_chan_sum_parts(int(N), int(HW))
+
+
+def chan_sum(a, b, part, out, accumulate=False):
+    """mia_chan_sum: out (N, C) fp32 (+)= Σ_pixels a·b (b given) or Σ_pixels a, deterministic;
+    part: fp32 scratch of N · chan_sum_parts(N, H·W) · C floats."""
+    N, H, W, C = a.shape
+    if b is not None:
+        _need(b, a.shape, a.dtype, "b")
+    _need(out, (N, C), torch.float32, "out")
+    if part.dtype != torch.float32 or part.numel() < N * chan_sum_parts(N, H * W) * C:
+        raise ValueError("chan_sum: part scratch too small")
+    call("mia_chan_sum", ptr(a), ptr(b), ptr(part), ptr(out), N, H * W, C,
+         int(bool(accumulate)), dt(a), stream())
+    return out
+
+
 def se_bwd(gs, s, u, w1, w2, gavg, hw):
     N, C = s.shape
     Cr = w1.shape[0]

@@ -410,6 +410,14 @@ int mia_se_apply(const void* r, const float* s, const void* sc, int ss, void* ou
                  void* stream);
 int mia_chan_dot(const void* a, const void* b, float* gs, int N, int HW, int C, int accumulate,
                  int dtype, void* stream);
+/* Deterministic per-(image, channel) sums over the pixels of (N, HW, C) NHWC tensors:
+ * out[n][c] (+)= Σ_p a·b (b given: the SE gate gradient Σ ∂out·r, as mia_chan_dot) or Σ_p a
+ * (b NULL: the SE average pool's sum, psp_encoders SEModule AdaptiveAvgPool2d, reached through
+ * net.encoder at code/attack/attack_main2.py:597,622). Fixed-order reduction through `part`
+ * (fp32 scratch of N · mia_chan_sum_parts(N, HW) · C floats): bit-reproducible run to run. */
+int mia_chan_sum_parts(int N, int HW);
+int mia_chan_sum(const void* a, const void* b, float* part, float* out, int N, int HW, int C,
+                 int accumulate, int dtype, void* stream);
 int mia_se_bwd(const float* gs, const float* s, const float* u, const float* w1, const float* w2,
                float* gavg, int N, int C, int Cr, float inv_hw, void* stream);
 int mia_se_grad_scale(const void* g_out, const float* s, const float* gavg, const float* gamma,

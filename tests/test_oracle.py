@@ -105,9 +105,13 @@ def test_synthesis_gradcheck_tiny():
     for k in list(p):
         if k.endswith(".conv.weight") and p[k].shape[1] == 512:
             pass
-    lat = torch.randn(1, n_latent_for(8), 512, dtype=torch.float64, requires_grad=True)
+    # seeded: an unseeded draw (global RNG state depends on the tests before it) can put a
+    # leaky-ReLU kink inside the ±h central difference and fail at the 1e-5 bar
+    gen = torch.Generator().manual_seed(3)
+    lat = torch.randn(1, n_latent_for(8), 512, dtype=torch.float64, generator=gen)
+    lat.requires_grad_(True)
     # gradcheck is expensive at 512 channels; check a directional derivative instead
-    v = torch.randn_like(lat)
+    v = torch.randn(lat.shape, dtype=torch.float64, generator=gen)
     f = lambda z: stylegan2_ref.synthesis(p, z, 8).sum()  # noqa: E731
     (g,) = torch.autograd.grad(f(lat), lat)
     h = 1e-6

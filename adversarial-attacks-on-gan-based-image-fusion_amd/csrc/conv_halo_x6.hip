@@ -29,6 +29,14 @@
 
 namespace mia {
 
+#ifdef MIA_STAMPS
+// Diagnostic build only (csrc/Makefile `stamps`, tools/probe/x6_stamps.py): wave 0 of every block
+// adds its phase cycles here; nothing in the kernel reads them back and no output depends on them.
+// [variant = (BN == 128) + 2·PRO][blocks, cycles, prologue, in-loop splits, epilogue, 100-MHz
+// ticks, K-steps, -]
+__device__ unsigned long long g_x6_stamps[4][8];
+#endif
+
 // BN_ = 128: 4 row waves × 2 column waves of 4 × 4 fragments; BN_ = 64 (the 64-channel layers):
 // 8 row waves of 2 × 4 fragments.
 template <int BN_>
@@ -86,6 +94,11 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
   const bool bwave = wid < TL::BWAVES;
   const int hw = wid - TL::BWAVES;
   const int my_pieces = bwave ? 0 : (HPIECES - hw + HWAVES - 1) / HWAVES;
+#ifdef MIA_STAMPS
+  const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long st_r0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long st_pro = 0, st_cv = 0;
+#endif
 
   // per-lane DMA sources (byte pointers; nullptr → the zero page)
   constexpr int NSRC = H_INS > B_HM_INS + B_L_INS ? H_INS : B_HM_INS + B_L_INS;
@@ -176,6 +189,9 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
   __syncthreads();
   convert(0, 0);
   __syncthreads();
+#ifdef MIA_STAMPS
+  st_pro = __builtin_amdgcn_s_memtime();
+#endif
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -253,12 +269,21 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (t == 8 && cb + 1 < ncb) {  // every wave is past the last read of lbuf: split block cb+1
+#ifdef MIA_STAMPS
+      const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+#endif
       convert(cb + 1, (cb + 1) & 1);
       __syncthreads();
+#ifdef MIA_STAMPS
+      st_cv += __builtin_amdgcn_s_memtime() - c0;
+#endif
     }
     st ^= 1;
     if (++t == 9) { t = 0; ++cb; }
   }
+#ifdef MIA_STAMPS
+  const unsigned long long st_loop = __builtin_amdgcn_s_memtime();
+#endif
   if constexpr (EPI >= 0) {
     halo_epilogue_f<float, TL, EPI>(k, acc, n, y0, x0, n0, wm, wn, lane, -1, -1, nullptr,
                                     k.prered ? (float*)smem : nullptr, TL::WM, TL::BN);
@@ -271,6 +296,20 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
       return (img_row + (r >> 4)) * W + x0 + (r & 15);
     });
   }
+#ifdef MIA_STAMPS
+  if (wid == 0 && lane == 0) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* g = g_x6_stamps[(BN_ == 128 ? 1 : 0) + (PRO ? 2 : 0)];
+    atomicAdd(g + 0, 1ull);
+    atomicAdd(g + 1, t1 - st_t0);
+    atomicAdd(g + 2, st_pro - st_t0);
+    atomicAdd(g + 3, st_cv);
+    atomicAdd(g + 4, t1 - st_loop);
+    atomicAdd(g + 5, r1 - st_r0);
+    atomicAdd(g + 6, (unsigned long long)nk);
+  }
+#endif
 }
 
 template <int BN_, bool PRO, int EPI, bool EARLY, bool PRIO = false>
@@ -309,6 +348,43 @@ static int launch_x6_(ConvK& k, hipStream_t st) {
   return launch_x6_e<BN_, PRO, EPI, false>(k, st);
 }
 
+// The register epilogue specialised for the feature masks of the attack's fp32 launches (every aux
+// load of a row chunk hoisted, compile-time features; halo_epilogue.h): the runtime-generic one
+// issues its per-row loads one dependent round trip at a time, ≈ 10 % of a block's cycles
+// (tools/probe/x6_stamps.py). Any other mask runs the generic epilogue.
+template <int BN_, bool PRO>
+static int launch_x6_spec(ConvK& k, hipStream_t st) {
+  using namespace epi;
+  const int f = epi_mask(k);
+  if constexpr (PRO) {  // modulated input: the StyledConv forward
+    if (f == (OSC | NOISE | BIAS | LRELU))
+      return launch_x6_<BN_, PRO, OSC | NOISE | BIAS | LRELU>(k, st);
+  } else if constexpr (BN_ == 64) {  // the 64-column tile: launches without per-pixel aux operands
+    switch (f) {
+      case 0: return launch_x6_<BN_, PRO, 0>(k, st);
+      case BIAS: return launch_x6_<BN_, PRO, BIAS>(k, st);            // e4e conv2 (SE body)
+      case BIAS | RELU: return launch_x6_<BN_, PRO, BIAS | RELU>(k, st);  // VGG forward
+      case PRELU: return launch_x6_<BN_, PRO, PRELU>(k, st);          // e4e conv1
+      default: break;
+    }
+  } else {
+    switch (f) {
+      case 0: return launch_x6_<BN_, PRO, 0>(k, st);
+      case BIAS: return launch_x6_<BN_, PRO, BIAS>(k, st);
+      case BIAS | RELU: return launch_x6_<BN_, PRO, BIAS | RELU>(k, st);
+      case PRELU: return launch_x6_<BN_, PRO, PRELU>(k, st);
+      case MASK: return launch_x6_<BN_, PRO, MASK>(k, st);            // VGG input gradient
+      case TAP: return launch_x6_<BN_, PRO, TAP>(k, st);              // VGG gradient at a tap
+      case ACC: return launch_x6_<BN_, PRO, ACC>(k, st);              // e4e residual gradient
+      case MASK | MSL: return launch_x6_<BN_, PRO, MASK | MSL>(k, st);  // e4e PReLU gradient
+      case OSC | SDOT: return launch_x6_<BN_, PRO, OSC | SDOT>(k, st);  // StyledConv dgrad
+      case OSC | SDOT | BAB: return launch_x6_<BN_, PRO, OSC | SDOT | BAB>(k, st);
+      default: break;
+    }
+  }
+  return launch_x6_<BN_, PRO, -1>(k, st);
+}
+
 // MIA_X6_64AUX=1: the 64-column tile also for launches with per-pixel aux operands (A/B)
 static bool x6_64_aux() {
   const char* e = getenv("MIA_X6_64AUX");
@@ -338,15 +414,43 @@ bool conv_halo_x6_eligible(const ConvK& k, int dtype) {
                                             x6_64_aux())));
 }
 
+#ifdef MIA_STAMPS
+extern "C" int mia_debug_x6_stamps(unsigned long long* host, int reset) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_x6_stamps), sizeof(g_x6_stamps)) != hipSuccess)
+    return 1;
+  if (reset) {
+    static const unsigned long long zero[4][8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_x6_stamps), zero, sizeof(zero)) != hipSuccess) return 1;
+  }
+  return 0;
+}
+#endif
+
 int launch_conv_halo_x6(ConvK& k, hipStream_t st) {
   const bool pro = k.a.in_scale != nullptr || k.a.act_in != MIA_ACT_NONE;
-  const char* e = getenv("MIA_HALO_EPI");  // A/B: 0 = LDS-staged shared epilogue
-  const bool lds_epi = e && atoi(e) == 0;
+#ifdef MIA_STAMPS
+  {  // each distinct (Cout tile, prologue, epilogue feature mask) once
+    static int seen[64];
+    static int nseen = 0;
+    const int key = (epi_mask(k) << 2) | (pro ? 2 : 0) | (k.a.Cout == 64 ? 1 : 0);
+    bool found = false;
+    for (int i = 0; i < nseen; ++i) found |= seen[i] == key;
+    if (!found && nseen < 64) {
+      seen[nseen++] = key;
+      fprintf(stderr, "x6 launch: Cout %d pro %d epi_mask %d (%dx%d Cin %d)\n", k.a.Cout, pro,
+              epi_mask(k), k.a.H, k.a.W, k.a.Cin);
+    }
+  }
+#endif
+  const char* e = getenv("MIA_HALO_EPI");  // A/B: 0 = LDS-staged shared epilogue, 2 = runtime
+  const int sel = e ? atoi(e) : 1;          // register epilogue; default 1 = specialised
   if (k.a.Cout == 64) {
-    if (lds_epi) return pro ? launch_x6_<64, true, -2>(k, st) : launch_x6_<64, false, -2>(k, st);
+    if (sel == 0) return pro ? launch_x6_<64, true, -2>(k, st) : launch_x6_<64, false, -2>(k, st);
+    if (sel == 1) return pro ? launch_x6_spec<64, true>(k, st) : launch_x6_spec<64, false>(k, st);
     return pro ? launch_x6_<64, true, -1>(k, st) : launch_x6_<64, false, -1>(k, st);
   }
-  if (lds_epi) return pro ? launch_x6_<128, true, -2>(k, st) : launch_x6_<128, false, -2>(k, st);
+  if (sel == 0) return pro ? launch_x6_<128, true, -2>(k, st) : launch_x6_<128, false, -2>(k, st);
+  if (sel == 1) return pro ? launch_x6_spec<128, true>(k, st) : launch_x6_spec<128, false>(k, st);
   return pro ? launch_x6_<128, true, -1>(k, st) : launch_x6_<128, false, -1>(k, st);
 }
 

@@ -21,9 +21,15 @@
 // Measured dead end: each wave owning 16 channels × all 256 pixels with its weights loaded from
 // L2 straight into VGPRs (no weight ring, no per-K-step barrier, 9 VALU per 96 MFMAs with
 // padded [hi|mid] / [lo|hi] planes read as single ds_read_b128 tuples) ran 4–13 % SLOWER than
-// this kernel: the per-K-step barrier is not the limiter. At ≈ 200 TFLOP/s these layers run
-// ≈ 0.75 of the six-product rate at the ≈ 1.6 GHz the chip holds under this MFMA load
-// (2500 × 1.6 / 2.4 / 6 ≈ 278 TFLOP/s).
+// this kernel. Phase stamps (csrc/Makefile `stamps`, tools/probe/x6_stamps.py) over the bench
+// attack: the chip holds 2.2–2.3 GHz in this kernel; per block 3 % prologue, 3–6 % in-loop splits,
+// 2–5 % epilogue, 89 % main loop, and the main loop runs at 66 % of its MFMA-only bound (16 cycles
+// per MFMA, two waves per SIMD). A weight-streaming wave spends a third of the loop at the
+// step-end wait + barrier, a halo wave 2–3 %: the halo waves are the long pole of each step.
+// Measured neutral or slower for the loop (not kept): both halves' fragment reads up front, a
+// fragment-level read/MFMA pipeline with (lo, hi) windows loaded in place (no register copies),
+// every wave streaming a share of the weights and of the halo, a 4-stage weight ring (64-channel
+// tile), and a persistent form.
 #include "conv_common.h"
 #include "halo_epilogue.h"
 
@@ -33,8 +39,8 @@ namespace mia {
 // Diagnostic build only (csrc/Makefile `stamps`, tools/probe/x6_stamps.py): wave 0 of every block
 // adds its phase cycles here; nothing in the kernel reads them back and no output depends on them.
 // [variant = (BN == 128) + 2·PRO][blocks, cycles, prologue, in-loop splits, epilogue, 100-MHz
-// ticks, K-steps, -]
-__device__ unsigned long long g_x6_stamps[4][8];
+// ticks, K-steps, wave 0 (weights) / wave 4 (halo) cycles in the end-of-step wait + barrier, -…]
+__device__ unsigned long long g_x6_stamps[4][16];
 #endif
 
 // BN_ = 128: 4 row waves × 2 column waves of 4 × 4 fragments; BN_ = 64 (the 64-channel layers):
@@ -97,7 +103,7 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
 #ifdef MIA_STAMPS
   const unsigned long long st_t0 = __builtin_amdgcn_s_memtime();
   const unsigned long long st_r0 = __builtin_amdgcn_s_memrealtime();
-  unsigned long long st_pro = 0, st_cv = 0;
+  unsigned long long st_pro = 0, st_cv = 0, st_wb = 0;
 #endif
 
   // per-lane DMA sources (byte pointers; nullptr → the zero page)
@@ -264,10 +270,16 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
       }
     }
     // B-wave: step s+1's weights must have landed. H-wave: the next block's halo by the last tap.
+#ifdef MIA_STAMPS
+    const unsigned long long w0 = __builtin_amdgcn_s_memtime();
+#endif
     if (bwave || t == 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS reads of the step are done
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+#ifdef MIA_STAMPS
+    st_wb += __builtin_amdgcn_s_memtime() - w0;
+#endif
     if (t == 8 && cb + 1 < ncb) {  // every wave is past the last read of lbuf: split block cb+1
 #ifdef MIA_STAMPS
       const unsigned long long c0 = __builtin_amdgcn_s_memtime();
@@ -308,7 +320,9 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
     atomicAdd(g + 4, t1 - st_loop);
     atomicAdd(g + 5, r1 - st_r0);
     atomicAdd(g + 6, (unsigned long long)nk);
+    atomicAdd(g + 7, st_wb);
   }
+  if (wid == 4 && lane == 0) atomicAdd(&g_x6_stamps[(BN_ == 128 ? 1 : 0) + (PRO ? 2 : 0)][8], st_wb);
 #endif
 }
 
@@ -423,7 +437,7 @@ extern "C" int mia_debug_x6_stamps(unsigned long long* host, int reset) {
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_x6_stamps), sizeof(g_x6_stamps)) != hipSuccess)
     return 1;
   if (reset) {
-    static const unsigned long long zero[4][8] = {};
+    static const unsigned long long zero[4][16] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_x6_stamps), zero, sizeof(zero)) != hipSuccess) return 1;
   }
   return 0;

@@ -51,7 +51,7 @@ def main():
     assert os.path.basename(_lib.LIB_PATH) == "libmiattack_stamps.so"
     fn = lib.mia_debug_x6_stamps
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]
-    buf = (ctypes.c_ulonglong * 32)()
+    buf = (ctypes.c_ulonglong * 64)()
     eng.run(x0, tgt, a.pgd_steps, 8 / 255, 2 / 255)
     torch.cuda.synchronize()
     assert fn(buf, 1) == 0
@@ -63,7 +63,7 @@ def main():
     assert fn(buf, 0) == 0
     print(f"attack {e0.elapsed_time(e1):.1f} ms")
     for v in range(4):
-        r = [buf[v * 8 + i] for i in range(8)]
+        r = [buf[v * 16 + i] for i in range(16)]
         nb = r[0]
         if not nb:
             continue
@@ -73,7 +73,8 @@ def main():
         print(f"{NAMES[v]:11s} blocks {nb:9d}  cycles/block {tot / nb:9.0f}  "
               f"prologue {pro / tot:6.1%}  splits {cv / tot:6.1%}  epilogue {epi / tot:6.1%}  "
               f"loop {loop / tot:6.1%}  loop vs MFMA-only {ideal / loop:6.1%}  "
-              f"clock {tot / rt * 0.1:5.2f} GHz")
+              f"clock {tot / rt * 0.1:5.2f} GHz  step-end wait+barrier: weights wave "
+              f"{r[7] / loop:6.1%} halo wave {r[8] / loop:6.1%} of the loop")
 
 
 if __name__ == "__main__":

@@ -67,8 +67,9 @@ struct HaloX6 {
   static_assert(LDS <= 160 * 1024, "");
 };
 
-template <int BN_, bool PRO, int EPI, bool EARLY, bool PRIO>
+template <int BN_, bool PRO, int EPI, bool EARLY, bool PRIO, bool UNR>
 __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const ConvK k) {
+  static_assert(!UNR || (EARLY && PRIO && EPI != -2), "UNR: the EARLY + PRIO schedule, D[ch][px]");
   typedef HaloX6<BN_> TL;
   constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, NT = TL::NT, BN = TL::BN, BK = TL::BK;
   constexpr int HSIDE = TL::HSIDE, HROWS = TL::HROWS, HPIECES = TL::HPIECES, HBUF = TL::HBUF;
@@ -206,6 +207,87 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int frow = lane & 15, fq = lane >> 4;
+  if constexpr (UNR) {
+    // The taps unrolled: every fragment address is a lane-constant LDS offset chosen at compile
+    // time — for the A fragments one per (row shift q = i + dy, column shift dx), computed once
+    // here (the swizzle is not linear in the row, so per step it cost ≈ 8 VALU per fragment); the
+    // second MFMA half reads channel chunk ^ 4 (byte offset ^ 64, lo ^ 32). Same reads, same
+    // MFMAs in the same order as the rolled loop below.
+    int oh[FM + 2][3], ol[FM + 2][3];
+#pragma unroll
+    for (int q = 0; q < FM + 2; ++q)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int hr = (wm * FM + q) * HSIDE + frow + c;
+        int vh = hr * ROWB + ((fq ^ fsw(hr)) << 4), vl = hr * TL::LROWB + ((fq ^ lsw(hr)) << 3);
+        asm volatile("" : "+v"(vh), "+v"(vl));  // kept in registers, not recomputed per step
+        oh[q][c] = vh;
+        ol[q][c] = vl;
+      }
+    int st = 0;
+    for (int cb = 0; cb < ncb; ++cb) {
+      const char* ha = hbuf + (cb & 1) * HBUF;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int s = cb * 9 + t;
+        const int dy = t / 3, dx = t % 3;
+        const char* sb = bring + st * BSTAGE;
+        if (bwave && s + 1 < nk) issue_b(s + 1, st ^ 1);
+        if (!bwave && cb + 1 < ncb && t < (H_INS + HPS - 1) / HPS) {
+#pragma unroll
+          for (int q = 0; q < HPS; ++q) {
+            const int j = t * HPS + q;
+            if (j < H_INS && j < my_pieces) issue_h(cb + 1, j, (cb + 1) & 1);
+          }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ch = h * 4 + fq;
+          u32x4 ahm[FM], bhm[FN];
+          u32x2 al[FM], blo[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i) {
+            ahm[i] = *(const u32x4*)(ha + (oh[i + dy][dx] ^ (h * 64)));
+            al[i] = *(const u32x2*)(lbuf + (ol[i + dy][dx] ^ (h * 32)));
+          }
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int row = wn * FN * 16 + 16 * j + frow;
+            bhm[j] = *(const u32x4*)(sb + row * ROWB + ((ch ^ fsw(row)) << 4));
+            blo[j] = *(const u32x2*)(sb + TL::BHM + row * TL::LROWB + ((ch ^ lsw(row)) << 3));
+          }
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = mfma_x6(bhm[j], blo[j], ahm[i], al[i], acc[i][j]);  // D[ch][px]
+          __builtin_amdgcn_s_setprio(0);
+        }
+#ifdef MIA_STAMPS
+        const unsigned long long w0 = __builtin_amdgcn_s_memtime();
+#endif
+        if (bwave || t == 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+#ifdef MIA_STAMPS
+        st_wb += __builtin_amdgcn_s_memtime() - w0;
+#endif
+        if (t == 8 && cb + 1 < ncb) {
+#ifdef MIA_STAMPS
+          const unsigned long long c0 = __builtin_amdgcn_s_memtime();
+#endif
+          convert(cb + 1, (cb + 1) & 1);
+          __syncthreads();
+#ifdef MIA_STAMPS
+          st_cv += __builtin_amdgcn_s_memtime() - c0;
+#endif
+        }
+        st ^= 1;
+      }
+    }
+  } else {
   int st = 0, cb = 0, t = 0;
   for (int s = 0; s < nk; ++s) {
     const char* ha = hbuf + (cb & 1) * HBUF;
@@ -293,6 +375,7 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
     st ^= 1;
     if (++t == 9) { t = 0; ++cb; }
   }
+  }  // !UNR
 #ifdef MIA_STAMPS
   const unsigned long long st_loop = __builtin_amdgcn_s_memtime();
 #endif
@@ -326,7 +409,7 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
 #endif
 }
 
-template <int BN_, bool PRO, int EPI, bool EARLY, bool PRIO = false>
+template <int BN_, bool PRO, int EPI, bool EARLY, bool PRIO = false, bool UNR = false>
 static int launch_x6_e(ConvK& k, hipStream_t st) {
   typedef HaloX6<BN_> TL;
   k.nbn = (k.a.Cout + TL::BN - 1) / TL::BN;
@@ -334,7 +417,7 @@ static int launch_x6_e(ConvK& k, hipStream_t st) {
   size_t lds = TL::LDS;
   lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
   lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
-  auto fn = conv_halo_x6_kernel<BN_, PRO, EPI, EARLY, PRIO>;
+  auto fn = conv_halo_x6_kernel<BN_, PRO, EPI, EARLY, PRIO, UNR>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -356,6 +439,12 @@ static int launch_x6_(ConvK& k, hipStream_t st) {
   const char* e = getenv("MIA_X6_EARLY");
   const char* pe = getenv("MIA_X6_PRIO");
   const bool prio = !pe || atoi(pe) != 0;
+  if constexpr (EPI >= 0 && BN_ == 64) {  // + the taps unrolled with lane-constant fragment
+    const char* u = getenv("MIA_X6_UNR");  // offsets (A/B: MIA_X6_UNR=0). The 128-channel tile
+                                           // spills with the offset tables (256 VGPRs).
+    if ((!u || atoi(u) != 0) && (!e || atoi(e) != 0) && prio)
+      return launch_x6_e<BN_, PRO, EPI, true, true, true>(k, st);
+  }
   if (!e || atoi(e) != 0)
     return prio ? launch_x6_e<BN_, PRO, EPI, true, true>(k, st)
                 : launch_x6_e<BN_, PRO, EPI, true, false>(k, st);

@@ -226,10 +226,14 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
       }
     int st = 0;
     for (int cb = 0; cb < ncb; ++cb) {
-      const char* ha = hbuf + (cb & 1) * HBUF;
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int s = cb * 9 + t;
+        // opaque per tap: keeps (table ^ half) and (buffer + table) from being hoisted out of the
+        // unrolled taps as 54 more live registers
+        int hoff = (cb & 1) * HBUF, x1 = 64, x2 = 32;
+        asm volatile("" : "+s"(hoff), "+s"(x1), "+s"(x2));
+        const char* ha = hbuf + hoff;
         const int dy = t / 3, dx = t % 3;
         const char* sb = bring + st * BSTAGE;
         if (bwave && s + 1 < nk) issue_b(s + 1, st ^ 1);
@@ -247,8 +251,8 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
           u32x2 al[FM], blo[FN];
 #pragma unroll
           for (int i = 0; i < FM; ++i) {
-            ahm[i] = *(const u32x4*)(ha + (oh[i + dy][dx] ^ (h * 64)));
-            al[i] = *(const u32x2*)(lbuf + (ol[i + dy][dx] ^ (h * 32)));
+            ahm[i] = *(const u32x4*)(ha + (h ? oh[i + dy][dx] ^ x1 : oh[i + dy][dx]));
+            al[i] = *(const u32x2*)(lbuf + (h ? ol[i + dy][dx] ^ x2 : ol[i + dy][dx]));
           }
 #pragma unroll
           for (int j = 0; j < FN; ++j) {
@@ -439,7 +443,7 @@ static int launch_x6_(ConvK& k, hipStream_t st) {
   const char* e = getenv("MIA_X6_EARLY");
   const char* pe = getenv("MIA_X6_PRIO");
   const bool prio = !pe || atoi(pe) != 0;
-  if constexpr (EPI >= 0 && BN_ == 64) {  // + the taps unrolled with lane-constant fragment
+  if constexpr (EPI >= 0) {  // + the taps unrolled with lane-constant fragment
     const char* u = getenv("MIA_X6_UNR");  // offsets (A/B: MIA_X6_UNR=0). The 128-channel tile
                                            // spills with the offset tables (256 VGPRs).
     if ((!u || atoi(u) != 0) && (!e || atoi(e) != 0) && prio)

@@ -443,9 +443,8 @@ static int launch_x6_(ConvK& k, hipStream_t st) {
   const char* e = getenv("MIA_X6_EARLY");
   const char* pe = getenv("MIA_X6_PRIO");
   const bool prio = !pe || atoi(pe) != 0;
-  if constexpr (EPI >= 0) {  // + the taps unrolled with lane-constant fragment
-    const char* u = getenv("MIA_X6_UNR");  // offsets (A/B: MIA_X6_UNR=0). The 128-channel tile
-                                           // spills with the offset tables (256 VGPRs).
+  if constexpr (EPI >= 0) {  // + the taps unrolled with lane-constant fragment offsets
+    const char* u = getenv("MIA_X6_UNR");  // (A/B: MIA_X6_UNR=0)
     if ((!u || atoi(u) != 0) && (!e || atoi(e) != 0) && prio)
       return launch_x6_e<BN_, PRO, EPI, true, true, true>(k, st);
   }

@@ -23,9 +23,11 @@
 // padded [hi|mid] / [lo|hi] planes read as single ds_read_b128 tuples) ran 4–13 % SLOWER than
 // this kernel. Phase stamps (csrc/Makefile `stamps`, tools/probe/x6_stamps.py) over the bench
 // attack: the chip holds 2.2–2.3 GHz in this kernel; per block 3 % prologue, 3–6 % in-loop splits,
-// 2–5 % epilogue, 89 % main loop, and the main loop runs at 66 % of its MFMA-only bound (16 cycles
-// per MFMA, two waves per SIMD). A weight-streaming wave spends a third of the loop at the
-// step-end wait + barrier, a halo wave 2–3 %: the halo waves are the long pole of each step.
+// 2–5 % epilogue, 88 % main loop, and the main loop runs at 72 % of its MFMA-only bound (16 cycles
+// per MFMA, two waves per SIMD; 66 % before the taps were unrolled over offset tables): the loop is
+// largely issue-bound. Wave 0 of a block spends a third of the loop at the step-end wait +
+// barrier, wave 4 2–3 %, whichever DMA role either streams (the older wave wins the issue
+// arbitration; the younger one is the long pole of each step).
 // Measured neutral or slower for the loop (not kept): both halves' fragment reads up front, a
 // fragment-level read/MFMA pipeline with (lo, hi) windows loaded in place (no register copies),
 // every wave streaming a share of the weights and of the halo, a 4-stage weight ring (64-channel

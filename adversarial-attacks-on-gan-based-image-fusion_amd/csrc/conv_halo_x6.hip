@@ -116,15 +116,18 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
   for (int j = 0; j < NSRC; ++j) {
     src[j] = nullptr;
     if (bwave) {
+      // register epilogues: weight rows past Cout read row Cout − 1 instead of the zero page (their
+      // accumulator rows are never stored or summed), so the per-step DMA address needs no select
       if (j < B_HM_INS) {
         const int row = (wid * B_HM_INS + j) * 8 + (lane >> 3);
-        if (n0 + row < Cout)
-          src[j] = (const char*)(Whm + (size_t)(n0 + row) * Kpad + ((lane & 7) ^ fsw(row)) * 4);
+        const int c = EPI >= 0 ? min(n0 + row, Cout - 1) : n0 + row;
+        if (c < Cout)
+          src[j] = (const char*)(Whm + (size_t)c * Kpad + ((lane & 7) ^ fsw(row)) * 4);
       } else if (j < B_HM_INS + B_L_INS) {
         const int row = (wid * B_L_INS + j - B_HM_INS) * 16 + (lane >> 2);
-        if (n0 + row < Cout)
-          src[j] = (const char*)(Wl + (size_t)(n0 + row) * Kpad +
-                                 ((lane & 3) ^ (lsw(row) >> 1)) * 8);
+        const int c = EPI >= 0 ? min(n0 + row, Cout - 1) : n0 + row;
+        if (c < Cout)
+          src[j] = (const char*)(Wl + (size_t)c * Kpad + ((lane & 3) ^ (lsw(row) >> 1)) * 8);
       }
     } else if (j < H_INS) {
       const int hr = (hw + HWAVES * j) * 8 + (lane >> 3);
@@ -142,13 +145,15 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
     char* dst = bring + st * BSTAGE;
 #pragma unroll
     for (int j = 0; j < B_HM_INS; ++j) {
-      const char* a = src[j] ? src[j] + (size_t)koff * 4 : zero;
+      const char* a = EPI >= 0 ? src[j] + (size_t)koff * 4 : src[j] ? src[j] + (size_t)koff * 4 : zero;
       __builtin_amdgcn_global_load_lds((gptr_t)a, (lptr_t)(dst + (wid * B_HM_INS + j) * 1024), 16,
                                        0, 0);
     }
 #pragma unroll
     for (int j = 0; j < B_L_INS; ++j) {
-      const char* a = src[B_HM_INS + j] ? src[B_HM_INS + j] + (size_t)koff * 2 : zero;
+      const char* a = EPI >= 0                ? src[B_HM_INS + j] + (size_t)koff * 2
+                      : src[B_HM_INS + j] ? src[B_HM_INS + j] + (size_t)koff * 2
+                                          : zero;
       __builtin_amdgcn_global_load_lds((gptr_t)a,
                                        (lptr_t)(dst + TL::BHM + (wid * B_L_INS + j) * 1024), 16, 0,
                                        0);

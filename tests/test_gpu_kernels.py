@@ -930,3 +930,72 @@ def test_fp32_arithmetic_is_fp32_accurate(cuda, monkeypatch, path):
     print(f"{path}: max-abs err {mx:.3e}, norm-relative {nrm:.3e} (native fp32 MFMA "
           f"{native[path][0]:.2e}, {native[path][1]:.2e})")
     assert mx <= 2 * native[path][0] and nrm <= 2 * native[path][1]
+
+
+@pytest.mark.parametrize("C,H,W", [(64, 32, 48), (128, 32, 16), (256, 16, 16)])
+@pytest.mark.parametrize("mode", ["plain", "bias_relu", "prelu", "mask_slope", "acc", "mask",
+                                  "tap_mask", "bias"])
+def test_x6_halo_variants_bitwise(cuda, monkeypatch, C, H, W, mode):
+    """fp32 split-once halo kernel (conv_halo_x6.hip): the default launch (specialised register
+    epilogue, taps unrolled over lane-constant fragment offsets, weight rows past Cout clamped)
+    computes the same products in the same order as the rolled loop with the runtime-feature
+    epilogue (MIA_X6_UNR=0, MIA_HALO_EPI=2): outputs bit-identical, for every epilogue feature
+    set of the attack's fp32 launches, on the 64- and 128-channel tiles; and both against fp64."""
+    g = torch.Generator().manual_seed(C + H * 3 + W + len(mode))
+    N = 2
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
+    kp = ops.conv2d_kpad(9, C, torch.float32)
+    wm = torch.zeros(C, kp)
+    wm[:, :9 * C] = w.permute(0, 2, 3, 1).reshape(C, 9 * C)
+    grp = [dict(w=wm.to(cuda), kh=3, kw=3, pad=(1, 1), ho=H, wo=W)]
+    conv = F.conv2d(x.double(), w.double(), padding=1)
+    y0 = torch.randn(N, C, H, W, generator=g)
+    slope = torch.rand(C, generator=g) * 0.5 + 0.05
+    sl = slope.double().view(1, C, 1, 1)
+    b = torch.randn(C, generator=g) * 0.1
+    m = torch.randn(N, C, H, W, generator=g)
+    a = torch.randn(N, C, H, W, generator=g).relu()
+    t = torch.randn(N, C, H, W, generator=g)
+    kw, ref = {}, conv
+    if mode == "bias_relu":
+        ref = F.relu(conv + b.double().view(1, C, 1, 1))
+        kw = dict(bias=b.to(cuda), act_out=ops.ACT_RELU)
+    elif mode == "bias":
+        ref = conv + b.double().view(1, C, 1, 1)
+        kw = dict(bias=b.to(cuda))
+    elif mode == "prelu":
+        ref = torch.where(conv > 0, conv, sl * conv)
+        kw = dict(act_out=ops.ACT_PRELU, act_slope=slope.to(cuda))
+    elif mode == "mask_slope":
+        ref = torch.where(m.double() > 0, conv, sl * conv)
+        kw = dict(mask_a=nhwc(m, torch.float32).to(cuda), mask_slope=slope.to(cuda))
+    elif mode == "mask":
+        ref = conv * (m.double() > 0)
+        kw = dict(mask_a=nhwc(m, torch.float32).to(cuda))
+    elif mode == "acc":
+        ref = conv + y0.double()
+        kw = dict(accumulate=True)
+
+    def run():
+        y = nhwc(y0, torch.float32).to(cuda)
+        xc = nhwc(x, torch.float32).to(cuda)
+        if mode == "tap_mask":
+            ops.conv3x3(xc, layouts.fwd_matrix(w, torch.float32).to(cuda), y, cout=C,
+                        tap_a=nhwc(a, torch.float32).to(cuda),
+                        tap_t=nhwc(t, torch.float32).to(cuda), tap_coef=0.37,
+                        mask_a=nhwc(a, torch.float32).to(cuda))
+        else:
+            ops.conv2d(xc, grp, y, (H, W), cout=C, **kw)
+        torch.cuda.synchronize()
+        return y
+
+    if mode == "tap_mask":
+        ref = (conv + 0.37 * (a.double() - t.double())) * (a.double() > 0)
+    monkeypatch.setenv("MIA_X6_64AUX", "1")  # the 64-column tile for the tap launch too
+    y_def = run()
+    monkeypatch.setenv("MIA_X6_UNR", "0")
+    monkeypatch.setenv("MIA_HALO_EPI", "2")
+    y_gen = run()
+    assert torch.equal(y_def, y_gen)
+    assert rel_err(nchw(y_def), ref) < 2 * TOL[torch.float32]

@@ -48,14 +48,20 @@ def attack_distributed(net, imgs, eps, steps, *, target, group=None, random_star
       of the all-gather (every rank must still enter the collective).
     * The random-start noise is drawn ONCE for the full batch from ``seed`` (the same host draw as
       a single-GPU ``attack(..., random_start=True, seed=seed)``) and sliced per shard, so the
-      output does not depend on the world size."""
+      output does not depend on the world size.
+    * fp16 loss-scale overflows are decided job-wide (``pgd.rescale_consensus``, one int32 MAX
+      all-reduce per attack run): every shard re-runs at the same λ, and a fatal overflow raises
+      FloatingPointError on EVERY rank (an empty-shard rank included) before the all-gather, so
+      no rank is left blocked in the collective."""
     from . import pgd
+    group = group if group is not None else dist.group.WORLD
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     n = imgs.shape[0]
     lo, hi = shard_bounds(n, world, rank)
     gather_dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else net.decoder.device
     if hi == lo:
+        pgd.idle_rank_consensus(group)
         local = torch.zeros((0,) + tuple(imgs.shape[1:]), dtype=torch.float32, device=gather_dev)
         return gather_shards(local, n, group).to(imgs.device)
     tgt = target if target.shape[0] == 1 else target[lo:hi]
@@ -63,5 +69,5 @@ def attack_distributed(net, imgs, eps, steps, *, target, group=None, random_star
     if random_start:
         noise = pgd.make_start_noise(tuple(imgs.shape), seed)[lo:hi]
     local = pgd.attack(net, imgs[lo:hi], eps, steps, target=tgt, random_start=random_start,
-                       seed=seed, start_noise=noise, **kw)
+                       seed=seed, start_noise=noise, group=group, **kw)
     return gather_shards(local.to(gather_dev, torch.float32), n, group).to(imgs.device)

@@ -61,6 +61,12 @@ def patch_white_box(inputs, mask, adv_patch):
     dev = inputs.device
     f32 = torch.float32
     one = tuple(inputs.shape[1:])
+    for nm, t in (("mask", mask), ("adv_patch", adv_patch)):
+        # the (1,3,S,S) mask / patch adversarial_patch.main saves; a batch-shaped (N,3,S,S)
+        # placement (the reference would broadcast it to N·N images) is not supported
+        if t.numel() != inputs[0].numel() or tuple(t.shape[-3:]) != one:
+            raise ValueError(f"{nm} must have shape (3,S,S) or (1,3,S,S) with (3,S,S) = {one}; "
+                             f"got {tuple(t.shape)} (batch-shaped masks are not supported)")
     m = mask.detach().to(dev, f32).reshape(one).contiguous()
     p = adv_patch.detach().to(dev, f32).reshape(one).contiguous()
     x = inputs.detach().to(f32).contiguous()

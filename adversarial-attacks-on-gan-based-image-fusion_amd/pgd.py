@@ -37,6 +37,31 @@ PATCH_WEIGHTS = dict(lat_t=0.0, lat_o=-1.0, img_rec_t=0.0, vgg_rec_t=0.0, img_o=
 # the engine divides λ by RESCALE and re-runs the attack, at most MAX_RESCALES times.
 DEFAULT_LOSS_SCALE = {torch.float32: 1.0, torch.float16: 2.0 ** 8, torch.bfloat16: 1.0}
 RESCALE, MAX_RESCALES = 16.0, 4
+RUN_OK, RUN_RESCALE, RUN_FATAL = 0, 1, 2  # per-run status, MAX-reduced over the ranks
+
+
+def rescale_consensus(status, group=None):
+    """The job-wide status of one attack run: the MAX of every rank's (OK < RESCALE < FATAL).
+    Without a process group (single process) the local status."""
+    if group is None:
+        return status
+    import torch.distributed as dist
+    dev = (torch.device("cpu") if dist.get_backend(group) == "gloo"
+           else torch.device("cuda", torch.cuda.current_device()))
+    t = torch.tensor([int(status)], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
+def idle_rank_consensus(group):
+    """A rank with an empty shard takes part in the attack's status rounds (one all-reduce per
+    run of the ranks that attack) until they finish or fail together."""
+    while True:
+        st = rescale_consensus(RUN_OK, group)
+        if st == RUN_OK:
+            return
+        if st == RUN_FATAL:
+            raise FloatingPointError("non-finite gradient on another rank")
 
 
 def _f32(v):
@@ -190,7 +215,19 @@ class AttackEngine:
         max_count times: g = ∇_adv L, patch −= g (the full-image gradient, step 1), adv =
         clamp((1−m)·img + m·patch, min(img), max(img)). `patch` (img's shape, fp32) is updated in
         place, as the reference's. Returns (adv, rec) with rec = G(E(adv')) of the last
-        iteration's input (the reference's adv_img_rec)."""
+        iteration's input (the reference's adv_img_rec).
+
+        A loss-scale overflow (fp16) lowers λ and re-runs the whole loop from the caller's
+        patch, like PGD / Adam / C&W (the raw-gradient step would otherwise have written NaN /
+        Inf into the patch)."""
+        patch0 = patch.clone()
+
+        def once():
+            patch.copy_(patch0)
+            return self._run_patch(img, t, patch, mask, max_count)
+        return self._with_rescale(once)
+
+    def _run_patch(self, img, t, patch, mask, max_count):
         ws = self.ws
         f32 = torch.float32
         self.prepare(img, t)
@@ -208,8 +245,6 @@ class AttackEngine:
             ops.grad_assemble(adv, self.x0, g_xv, g_enc, g, self.pf, ENC_POOL_RES, self.c_img_o,
                               1.0 / (self.loss_scale * img.shape[0]), nonfinite=self.nonfinite)
             ops.patch_update(patch, g, img, mask, adv, lo, hi)
-        if self.overflowed():
-            raise FloatingPointError("non-finite patch gradient (run fp32)")
         lat, _ = self._encode(last if max_count > 0 else adv, "in.x")
         return adv.clone(), self.G.forward(lat, ws).clone()
 
@@ -223,20 +258,31 @@ class AttackEngine:
         """Images whose gradient had a non-finite element since prepare() (one host sync)."""
         return self.nonfinite.nonzero().flatten().tolist()
 
-    def _with_rescale(self, run_once):
+    def _with_rescale(self, run_once, group=None):
         """Run an attack; if any image's gradient overflowed, lower λ and run it again (fp16).
         A non-finite gradient at λ that cannot be lowered (fp32 / bf16, or after MAX_RESCALES)
-        raises: sign(NaN) = 0 would otherwise leave those pixels silently unattacked."""
+        raises: sign(NaN) = 0 would otherwise leave those pixels silently unattacked.
+
+        ``group`` (attack_distributed): the decision is taken by every rank together — each
+        rank's status (OK / RESCALE / FATAL) is MAX-all-reduced after every run, so all shards
+        re-run at the same λ (the result does not depend on the world size) and a fatal overflow
+        raises on every rank instead of leaving the others blocked in the final all-gather."""
         self.rescales = 0
         while True:
             out = run_once()
             bad = self.overflowed()
-            if not bad:
+            status = (RUN_OK if not bad else RUN_RESCALE
+                      if self.dtype == torch.float16 and self.rescales < MAX_RESCALES
+                      else RUN_FATAL)
+            status = rescale_consensus(status, group)
+            if status == RUN_OK:
                 return out
-            if self.dtype != torch.float16 or self.rescales >= MAX_RESCALES:
+            if status == RUN_FATAL:
                 raise FloatingPointError(
-                    f"non-finite gradient for images {bad[:8]} (dtype {self.dtype}, loss scale "
-                    f"{self.loss_scale:g}): check the weights / inputs, or run fp32")
+                    f"non-finite gradient for images {bad[:8]}"
+                    + ("" if bad else " on another rank")
+                    + f" (dtype {self.dtype}, loss scale {self.loss_scale:g}): check the weights "
+                    "/ inputs, or run fp32")
             self.set_loss_scale(self.loss_scale / RESCALE)
             self.rescales += 1
 
@@ -273,11 +319,11 @@ class AttackEngine:
                           nonfinite=self.nonfinite)
         return g
 
-    def run_adam(self, x0, t, steps, lr=0.01, betas=(0.9, 0.999), eps=1e-8):
+    def run_adam(self, x0, t, steps, lr=0.01, betas=(0.9, 0.999), eps=1e-8, group=None):
         """``optimize_vgg`` literal mode (interpolation.py:743-843): Adam(lr) on the pixels,
         descending L, no ε-ball or clamp. The gradient carries the loss scale λ, so Adam's eps is
         scaled by λ too (m̂/(√v̂ + λ·eps) on λ·g ≡ m̂/(√v̂ + eps) on g)."""
-        return self._with_rescale(lambda: self._run_adam(x0, t, steps, lr, betas, eps))
+        return self._with_rescale(lambda: self._run_adam(x0, t, steps, lr, betas, eps), group)
 
     def _run_adam(self, x0, t, steps, lr, betas, eps):
         self.prepare(x0, t)
@@ -292,12 +338,12 @@ class AttackEngine:
             ops.adam_step(x, g, m, v, lr, betas[0], betas[1], eps * self.loss_scale, it)
         return x.clone()
 
-    def run_cw(self, x0, t, steps, c=1e-4, lr=0.01, betas=(0.9, 0.999), eps=1e-8):
+    def run_cw(self, x0, t, steps, c=1e-4, lr=0.01, betas=(0.9, 0.999), eps=1e-8, group=None):
         """torchattacks C&W L2 (interpolation.py:98-193) composed with the GAN objective, in
         [-1,1] space: adv = tanh(w); cost = Σ‖(adv − x0)/2‖² + c·Σ L_n(adv); Adam(lr) on w;
         best-L2 tracking with success = L_n(adv) < L_n(x0); early stop every steps//10 when the
         cost rises (one host sync there). See oracle.attack_ref.cw_attack."""
-        return self._with_rescale(lambda: self._run_cw(x0, t, steps, c, lr, betas, eps))
+        return self._with_rescale(lambda: self._run_cw(x0, t, steps, c, lr, betas, eps), group)
 
     def _run_cw(self, x0, t, steps, c, lr, betas, eps):
         self.prepare(x0, t)
@@ -338,10 +384,10 @@ class AttackEngine:
                 prev = cost
         return best.clone()
 
-    def run(self, x0, t, steps, eps, alpha, random_start=False, start_noise=None):
+    def run(self, x0, t, steps, eps, alpha, random_start=False, start_noise=None, group=None):
         """PGD-steps from x0 toward the objective; returns the adversarial images (new tensor)."""
         return self._with_rescale(
-            lambda: self._run_pgd(x0, t, steps, eps, alpha, random_start, start_noise))
+            lambda: self._run_pgd(x0, t, steps, eps, alpha, random_start, start_noise), group)
 
     def _run_pgd(self, x0, t, steps, eps, alpha, random_start, start_noise):
         e, a = 2.0 * eps, 2.0 * alpha
@@ -378,7 +424,7 @@ def make_start_noise(shape, seed):
 
 def attack(net, imgs, eps, steps, *, target=None, vgg=None, alpha=0.01, random_start=False,
            seed=0, start_noise=None, norm="linf", loss="gan_vgg", loss_scale=None, lr=0.01,
-           cw_c=1e-4, return_info=False):
+           cw_c=1e-4, return_info=False, group=None):
     """Craft adversarial images against the GAN fusion pipeline.
 
     net     pSp-like bundle: net.encoder, net.decoder (.size), net.latent_avg, net.opts
@@ -397,6 +443,8 @@ def attack(net, imgs, eps, steps, *, target=None, vgg=None, alpha=0.01, random_s
                       no ε-ball (eps is ignored and may be None);
             'l2_cw' — torchattacks C&W L2 (interpolation.py:98-193) with f = the objective,
                       c = cw_c, Adam(lr) in tanh space (eps ignored; see AttackEngine.run_cw).
+    group   process group of a data-parallel job (``dist.attack_distributed``): the fp16
+            loss-scale re-run decision is all-reduced over it so every shard runs at one λ.
     Returns the adversarial images on the input's device (fp32), and a dict if return_info.
     """
     if norm not in NORMS:
@@ -437,11 +485,12 @@ def attack(net, imgs, eps, steps, *, target=None, vgg=None, alpha=0.01, random_s
             raise ValueError("start_noise must have the shape of imgs")
         noise = start_noise.to(dev, torch.float32).contiguous()
     if norm == "linf":
-        adv = eng.run(x0, t, int(steps), float(eps), float(alpha), random_start, noise)
+        adv = eng.run(x0, t, int(steps), float(eps), float(alpha), random_start, noise,
+                      group=group)
     elif norm == "adam":
-        adv = eng.run_adam(x0, t, int(steps), lr=float(lr))
+        adv = eng.run_adam(x0, t, int(steps), lr=float(lr), group=group)
     else:
-        adv = eng.run_cw(x0, t, int(steps), c=float(cw_c), lr=float(lr))
+        adv = eng.run_cw(x0, t, int(steps), c=float(cw_c), lr=float(lr), group=group)
     adv = adv.to(imgs.device)
     if return_info:
         info = dict(loss=eng.loss(adv.to(dev)), steps=int(steps), eps=eps, alpha=alpha, norm=norm,

@@ -46,9 +46,17 @@ class Refs:
 
 
 def objective(gp, vp, ep, x, refs, size, weights=LOSS_WEIGHTS, per_image=False):
+    """The per-image objective (summed unless ``per_image``). With only the latent terms weighted
+    (the patch attack's loss, adversarial_patch.py:125) the generator and VGG terms are 0·(finite)
+    = +0 exactly in L and in ∇L, so they are not evaluated."""
     pf = max(1, size // 256)
     xp = F.avg_pool2d(x, pf) if pf > 1 else x
     lat = encoder_ref.apply(ep, xp, size)
+    w = weights
+    if all(w[k] == 0 for k in ("img_rec_t", "vgg_rec_t", "img_o", "vgg_img")):
+        L = (w["lat_t"] * _mse_per_image(refs.lat_t, lat)
+             + w["lat_o"] * _mse_per_image(refs.lat_o, lat))
+        return L if per_image else L.sum()
     rec = stylegan2_ref.synthesis(gp, lat, size)
     recp = F.avg_pool2d(rec, pf) if pf > 1 else rec
     taps_rec = vgg_ref.vgg_forward(vp, recp)
@@ -59,7 +67,6 @@ def objective(gp, vp, ep, x, refs, size, weights=LOSS_WEIGHTS, per_image=False):
     l_vgg_rec_t = sum(_mse_per_image(a, b) for a, b in zip(taps_rec, refs.taps_t))
     l_img_o = _mse_per_image(refs.x0, x)
     l_vgg_img = sum(_mse_per_image(a, b) for a, b in zip(taps_x, refs.taps_o))
-    w = weights
     L = (w["lat_t"] * l_lat_t + w["lat_o"] * l_lat_o + w["img_rec_t"] * l_img_rec_t
          + w["vgg_rec_t"] * l_vgg_rec_t + w["img_o"] * l_img_o + w["vgg_img"] * l_vgg_img)
     return L if per_image else L.sum()
@@ -195,15 +202,16 @@ def patch_attack(gp, vp, ep, img, patch, mask, t, size, max_count, dtype=torch.f
     lo, hi = torch.min(img), torch.max(img)
     n = img.shape[0]
     rec = None
-    for _ in range(max_count):
+    for it in range(max_count):
         x = adv.detach().requires_grad_(True)
         with (grad_ctx() if grad_ctx is not None else contextlib.nullcontext()):
             L = objective(gp, vp, ep, x, refs, size, weights=PATCH_WEIGHTS, per_image=True)
             (g,) = torch.autograd.grad(L.sum() / n, x)
         with torch.no_grad():
-            pf = max(1, size // 256)
-            xp = F.avg_pool2d(adv, pf) if pf > 1 else adv
-            rec = stylegan2_ref.synthesis(gp, encoder_ref.apply(ep, xp, size), size)
+            if it == max_count - 1:  # adv_img_rec: the last iteration's reconstruction
+                pf = max(1, size // 256)
+                xp = F.avg_pool2d(adv, pf) if pf > 1 else adv
+                rec = stylegan2_ref.synthesis(gp, encoder_ref.apply(ep, xp, size), size)
             patch = patch - g
             adv = torch.clamp((1 - mask) * img + mask * patch, lo, hi)
     return adv.detach(), patch.detach(), rec

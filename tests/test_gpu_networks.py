@@ -331,3 +331,24 @@ def test_cfg1_fusion_pair_fgsm(cuda):
     assert d.max().item() <= 16 / 255 + 1e-6 and ((d - 16 / 255).abs() < 1e-6).float().mean() > 0.5
     lat = networks.get_latents(net, adv)
     assert tuple(lat.shape) == (1, 14, 512)
+
+
+def test_partial_fusion_matches_reference(cuda):
+    """partial_adv_fusion_arithmetic on the church drawer vs the reference's own
+    partial_adv_fusion_arithmetic + interpolation (interpolation.py:921-977, 658-669) run with the
+    oracle generator in fp64 (tests/golden/fusion_golden.npz): the M + 1 fused images within 1e-4
+    of the image range (the fp32 synthesis bound of test_style_fusion_simple_api)."""
+    import os
+    import golden_inputs as gi
+    from conftest import GOLDEN
+    from gfa_amd import StyleFusionSimple, partial_adv_fusion_arithmetic
+    fg = np.load(os.path.join(GOLDEN, "fusion_golden.npz"))
+    drawer = StyleFusionSimple("church", None, None, cuda, n_mean_latent=64)
+    W, Wa = gi.fusion_latents()
+    sweep = partial_adv_fusion_arithmetic(drawer, None, None, W.to(cuda), Wa.to(cuda)).cpu()
+    ref = torch.from_numpy(fg["fused/slice"])
+    assert tuple(sweep.shape) == (W.shape[0] + 1, 3, gi.SIZE, gi.SIZE)
+    assert rel_err(sweep[gi.SLICE], ref) < 1e-4
+    probes = gi.projections(gi.SIZE, W.shape[0] + 1)
+    got = torch.tensor([float((q * sweep.double()).sum()) for q in probes])
+    assert rel_err(got, torch.from_numpy(fg["fused/proj"])) < 1e-4

@@ -20,7 +20,7 @@ import torch
 from conftest import GOLDEN
 from gpu_helpers import capture_vgg, engine, forced_all, free, grad_stats, seeded, to64
 from oracle import attack_ref
-from oracle import gen_golden_objective as gen
+import golden_inputs as gen
 
 pytestmark = pytest.mark.gpu
 

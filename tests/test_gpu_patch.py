@@ -107,3 +107,50 @@ def test_patch_attack_e4e_first_step_branch_forced(cuda):
     rel = ((dp - dp_ref).norm() / dp_ref.norm()).item()
     print(f"e4e patch step vs oracle: rel {rel:.2e}")
     assert rel < 1e-4
+
+
+# ---- against the reference's own code (tests/golden/patch_golden.npz, oracle/gen_golden_patch.py)
+
+def test_patch_white_box_matches_reference_output(cuda):
+    """gfa_amd.patch_white_box on the fixture's inputs (3 images at 64², a soft-edged mask) is
+    bit-identical to the reference's own patch_white_box (attack_main2.py:413-433) output."""
+    import os
+    from conftest import GOLDEN
+    pg = np.load(os.path.join(GOLDEN, "patch_golden.npz"))
+    x, m, p = (torch.from_numpy(pg[f"wb/{k}"]) for k in ("inputs", "mask", "patch"))
+    got = gfa_amd.patch_white_box(x.to(cuda), m.to(cuda), p.to(cuda)).cpu()
+    assert torch.equal(got, torch.from_numpy(pg["wb/out"]))
+
+
+def test_patch_attack_matches_reference_attack(cuda):
+    """gfa_amd.patch_attack (fp32, e4e, 256², 2 images, 3 iterations) vs the reference's own
+    adversarial_patch.attack run in fp64 with the oracle networks: the patch's change inside the
+    mask (Δpatch ≈ 3e-3) within 2e-3 in norm (unforced e4e branches: activations within fp32
+    rounding of 0 may take the other PReLU branch), the adversarial image within 1e-5 and the
+    reconstruction within 1e-3 max-abs, all projections within 1e-3."""
+    import os
+    import golden_inputs as gi
+    from conftest import GOLDEN
+    pg = np.load(os.path.join(GOLDEN, "patch_golden.npz"))
+    P = gi.PATCH
+    net = networks.build_net(gi.SIZE, seed=gi.SEEDS["gen"], device=cuda, encoder="e4e",
+                             vgg_seed=gi.SEEDS["vgg"])
+    img, patch, mask, tgt = gi.patch_inputs()
+    adv, m, p, rec = gfa_amd.patch_attack(img.to(cuda), patch.to(cuda), mask.to(cuda), net,
+                                          P["max_count"], target_img=tgt.to(cuda))
+    ys, xs = slice(P["y0"], P["y0"] + P["side"]), slice(P["x0"], P["x0"] + P["side"])
+    p, adv, rec = p.cpu().double(), adv.cpu().double(), rec.cpu().double()
+    dp = p[:, :, ys, xs] - patch.double()[:, :, ys, xs]
+    dp_ref = torch.from_numpy(pg["patch/region"]).double() - patch.double()[:, :, ys, xs]
+    rel = ((dp - dp_ref).norm() / dp_ref.norm()).item()
+    print(f"patch change vs reference attack: rel {rel:.2e} (|Δ| {dp_ref.abs().max():.2e})")
+    assert dp_ref.abs().max() > 1e-3 and rel < 2e-3
+    assert (adv[:, :, ys, xs] - torch.from_numpy(pg["adv/region"]).double()).abs().max() < 1e-5
+    assert (adv[gi.SLICE] - torch.from_numpy(pg["adv/slice"])).abs().max() < 1e-5
+    assert (rec[gi.SLICE] - torch.from_numpy(pg["rec/slice"])).abs().max() < 1e-3
+    probes = gi.projections(gi.SIZE, P["n"])
+    for nm, t in (("adv", adv), ("rec", rec)):
+        got = torch.tensor([float((q * t).sum()) for q in probes])
+        ref = torch.from_numpy(pg[f"{nm}/proj"])
+        assert ((got - ref).abs().max() / ref.abs().max()).item() < 1e-3, nm
+    assert torch.equal(m.cpu(), mask)

@@ -366,3 +366,30 @@ def test_split_f32_is_exact():
     h, m, l = parts
     assert torch.equal(h + m + l, w.double())
     assert (h.abs() >= m.abs()).all() and (m.abs() >= l.abs()).all()
+
+
+def test_make_grid_geometry_matches_reference_files():
+    """records.make_grid lays tiles out as the reference's own saved grids
+    (/root/reference/images/*.jpg, recorded by oracle/gen_golden_grids.py as size + per-column /
+    per-row mean brightness): 5 tiles of 1024² at padding 2 → 5132 × 1028, the 6-image partial
+    fusion sweep → 6158 × 1028, single images unpadded; every padding column / row of make_grid is
+    a black stripe in the reference's file and every tile column / row is not."""
+    import numpy as np
+    from gfa_amd import records
+    d = np.load(os.path.join(os.path.dirname(__file__), "golden", "reference_grids.npz"))
+    files = sorted({k.rsplit("/", 1)[0] for k in d.files})
+    assert len(files) >= 10
+    for f in files:
+        w, h = (int(v) for v in d[f"{f}/size"])
+        n = 1 if (w, h) == (1024, 1024) else (w - 2) // 1026
+        assert n in (1, 5, 6), (f, w, h)
+        # a small stand-in tile of the same layout: make_grid's geometry scales with the tile
+        grid = records.make_grid(torch.ones(n, 3, 1024, 1024), padding=2)
+        assert tuple(grid.shape) == (3, h, w), (f, tuple(grid.shape))
+        if n == 1:
+            continue
+        col_is_pad = (grid[0].sum(0) == 0).numpy()
+        row_is_pad = (grid[0].sum(1) == 0).numpy()
+        col, row = d[f"{f}/col"], d[f"{f}/row"]
+        assert col[col_is_pad].max() < 12 and col[~col_is_pad].min() > 20, f
+        assert row[row_is_pad].max() < 12 and row[~row_is_pad].min() > 20, f

@@ -207,7 +207,7 @@ def test_oracle_adam_mode_matches_reference_optimize_vgg(objg):
     optimize_vgg run (linear stand-in encoder, 3 Adam iterations at 256²): every iteration's
     inversion_loss (the reference's '%.5f' text), gradient (slices + random projections of the
     whole tensor) and the final image."""
-    from oracle import gen_golden_objective as gen
+    import golden_inputs as gen
     torch.set_num_threads(os.cpu_count() or 1)
     n, lr, size = int(objg["n_iters"]), float(objg["lr"]), int(objg["size"])
     gp, vp, ep = gen.networks("linear")
@@ -228,7 +228,7 @@ def test_oracle_adam_mode_matches_reference_optimize_vgg(objg):
 def test_oracle_e4e_objective_matches_reference_optimize_vgg(objg):
     """With the e4e restatement in the encoder slot: the objective and its full gradient at x0
     (iteration 0 of the reference's optimize_vgg) from attack_ref.loss_grad (fp64)."""
-    from oracle import gen_golden_objective as gen
+    import golden_inputs as gen
     torch.set_num_threads(os.cpu_count() or 1)
     size = int(objg["size"])
     gp, vp, ep = gen.networks("e4e")
@@ -271,3 +271,68 @@ def test_forced_branches_reproduce_the_free_forward():
     img = stylegan2_ref.synthesis(gp, lat, 32)
     with stylegan2_ref.forced_masks({}):  # no entry: the free branch
         assert torch.equal(img, stylegan2_ref.synthesis(gp, lat, 32))
+
+
+# ---- the patch attack / patch_white_box / partial fusion pinned to the reference's own code ------
+# tests/golden/{patch,fusion}_golden.npz: oracle/gen_golden_patch.py ran adversarial_patch.attack
+# (adversarial_patch.py:94-160), patch_white_box (attack_main2.py:413-433) and
+# partial_adv_fusion_arithmetic + interpolation (interpolation.py:921-977, 658-669) unchanged with
+# the oracle networks (fp64).
+
+def test_oracle_patch_attack_matches_reference_attack():
+    """attack_ref.patch_attack (fp64, e4e, 256², 2 images, 3 iterations) reproduces the
+    reference's own adversarial_patch.attack: its 'Loss:%.5f' lines, the patch, the adversarial
+    image (patch region in full, slices, projections) and the reconstruction."""
+    import golden_inputs as gi
+    torch.set_num_threads(os.cpu_count() or 1)
+    pg = np.load(os.path.join(GOLDEN, "patch_golden.npz"))
+    P = gi.PATCH
+    gp, vp, ep = gi.networks("e4e")
+    img, patch, mask, tgt = (t.double() for t in gi.patch_inputs())
+    refs = attack_ref.Refs(gp, vp, ep, img, tgt, gi.SIZE)
+    L = attack_ref.objective(gp, vp, ep, ((1 - mask) * img + mask * patch), refs, gi.SIZE,
+                             weights=attack_ref.PATCH_WEIGHTS, per_image=True).mean()
+    assert abs(float(L) - float(pg["losses"][0])) <= 5.1e-6
+    adv, p, rec = attack_ref.patch_attack(gp, vp, ep, img, patch, mask, tgt, gi.SIZE,
+                                          P["max_count"], dtype=torch.float64)
+    ys, xs = slice(P["y0"], P["y0"] + P["side"]), slice(P["x0"], P["x0"] + P["side"])
+    probes = gi.projections(gi.SIZE, P["n"])
+    for nm, t in (("patch", p), ("adv", adv), ("rec", rec)):
+        assert _rel(t[gi.SLICE].numpy(), pg[f"{nm}/slice"]) < 1e-9, nm
+        assert _rel(t[:, :, ys, xs].float().numpy(), pg[f"{nm}/region"]) < 1e-6, nm
+        assert _rel([float((q * t).sum()) for q in probes], pg[f"{nm}/proj"]) < 1e-9, nm
+
+
+def test_patch_white_box_formula_matches_reference():
+    """The torch fp32 composite the device kernel is tested bit-exact against
+    (test_gpu_patch.py) equals the reference's own patch_white_box output."""
+    pg = np.load(os.path.join(GOLDEN, "patch_golden.npz"))
+    x, m, p = (torch.from_numpy(pg[f"wb/{k}"]) for k in ("inputs", "mask", "patch"))
+    want = torch.cat([torch.clamp((1 - m) * x[i] + m * p, x[i].min(), x[i].max())
+                      for i in range(x.shape[0])])
+    assert torch.equal(want, torch.from_numpy(pg["wb/out"]))
+
+
+def test_oracle_partial_fusion_matches_reference():
+    """The partial-fusion sweep restated on the oracle generator (mean of the W latents with one
+    adversarial latent swapped in at a time, then all) reproduces the reference's own
+    partial_adv_fusion_arithmetic output."""
+    import golden_inputs as gi
+    from gfa_amd.weights import make_generator_weights
+    from oracle import stylegan2_ref
+    torch.set_num_threads(os.cpu_count() or 1)
+    fg = np.load(os.path.join(GOLDEN, "fusion_golden.npz"))
+    gp = {k: v.double() for k, v in make_generator_weights(gi.SIZE, seed=0).items()}
+    W, Wa = (t.double() for t in gi.fusion_latents())
+    M = W.shape[0]
+    out = []
+    for j in range(M + 1):
+        lat = Wa.clone() if j == M else W.clone()
+        if j < M:
+            lat[j] = Wa[j]
+        w = lat.mean(0, keepdim=True).unsqueeze(1).repeat(1, 14, 1)
+        out.append(stylegan2_ref.synthesis(gp, w, gi.SIZE))
+    fused = torch.cat(out)
+    assert _rel(fused[gi.SLICE].numpy(), fg["fused/slice"]) < 1e-12
+    probes = gi.projections(gi.SIZE, M + 1)
+    assert _rel([float((q * fused).sum()) for q in probes], fg["fused/proj"]) < 1e-12

@@ -71,6 +71,11 @@ class GemmGroup(ctypes.Structure):
 SIGNATURES = {
     "mia_version": (c_int, []),
     "mia_last_error_string": (ctypes.c_char_p, []),
+    "mia_conv_workspace_size": (c_int64, [c_int, c_int, c_int, c_int, c_int]),
+    "mia_reduction_workspace_size": (c_int64, [c_int, c_int, c_int]),
+    "mia_reserve_reduction_scratch": (c_int, [c_int64, P]),
+    "mia_reduction_scratch_bytes": (c_int64, [P]),
+    "mia_release_reduction_scratch": (c_int, [P]),
     "mia_conv_kpad": (c_int, [c_int, c_int]),
     "mia_conv3x3": (c_int, [ctypes.POINTER(ConvArgs), c_int, P]),
     "mia_modconv_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P,

@@ -34,8 +34,32 @@ struct ConvK {
                                  // sdot / q sums of the StyledConv dgrads (MIA_EPI_PRERED=0: off)
   int batched;                   // groups carry image / channel offsets: LDS-staged epilogue only
   int prio;                      // X6B tile: s_setprio(1) around the MFMA blocks
+  // deterministic sums (mia_common.h RedQ): partial slots of sdot (q 0), bab_q (1), csum (2)
+  float* red_part;
+  int red_nslots, red_count;     // slots per output; outputs per quantity (N·Cout)
+  int red_px;                    // LDS-staged epilogue: one slot per output pixel (small images)
   ConvGroup g[MIA_MAX_GROUPS];
 };
+
+// the partial of quantity q (0 sdot, 1 bab_q, 2 csum) of contributor `slot` to output i = n·Cout+c
+__device__ __forceinline__ void red_put(const ConvK& k, int q, int slot, int i, float v) {
+  red_store(k.red_part, k.red_nslots, k.red_count, q, slot, i, v);
+}
+
+// Slots of the register epilogues (halo_epilogue / halo_epilogue_f): a contributor is one wave's
+// FM rows × 16 columns of the (Hg × Wg) output grid, or — with the LDS pre-reduction across the
+// nwm wave rows — the block's FM·nwm rows × 16 columns.
+__host__ __device__ __forceinline__ int halo_red_h(int FM, int nwm, bool lds_red) {
+  return lds_red && nwm > 1 ? FM * nwm : FM;
+}
+__device__ __forceinline__ int halo_red_slot(int y_first, int x0, int h, int Wg) {
+  return (y_first / h) * (Wg >> 4) + (x0 >> 4);
+}
+inline int halo_red_slots(int Hg, int Wg, int FM, int nwm, bool lds_red) {
+  return (Hg / halo_red_h(FM, nwm, lds_red)) * (Wg / 16);
+}
+// open the launch's reductions (nslots contributors per output) / add them up after it
+int conv_red_begin(ConvK& k, RedQ& r, int nslots, hipStream_t st, bool zero = false);
 
 typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
@@ -301,7 +325,8 @@ struct Tile {
 template <typename T, typename TL, typename RowM>
 __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G,
                                               f32x4 (&acc)[TL::FM][TL::FN], char* smem, int n0,
-                                              bool single, int n_single, RowM rowm) {
+                                              bool single, int n_single, RowM rowm,
+                                              int slot = 0) {
   constexpr int WN = TL::WN, FM = TL::FM, FN = TL::FN, NT = TL::NT, NW = TL::NW;
   constexpr int BM = TL::BM, BN = TL::BN, ES = TL::ES, EROWS = TL::EROWS;
   const mia_conv_args& p = k.a;
@@ -396,7 +421,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
           for (int e = 0; e < 8; ++e) {
             const float c = v[e] * apply_act(xv[e], p.act_aux);
             if (single) part[e] += c;
-            else atomicAdd(&p.sdot[(size_t)n * Cout + col + e], c);
+            else red_put(k, 0, pix, n * Cout + col + e, c);  // one slot per output pixel
           }
         }
         if (Y) {
@@ -452,7 +477,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
               const float gp = v[e] * gr;
               const float c = gp * (xv[e] * lrelu_s2_inv_grad(xv[e]) - nz - bbias8[e]);
               if (single) partq[e] += c;
-              else atomicAdd(&p.bab_q[(size_t)n * Cout + col + e], c);
+              else red_put(k, 1, pix, n * Cout + col + e, c);
               v[e] = gp * dm8[e];
             }
           }
@@ -460,7 +485,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               if (single) pcs[e] += v[e];
-              else atomicAdd(&p.csum[(size_t)n * Cout + col + e], v[e]);
+              else red_put(k, 2, pix, n * Cout + col + e, v[e]);
             }
           }
           store8<T>(Y + off, v);
@@ -485,7 +510,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
       float s = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) s += red[w * BN + tid];
-      atomicAdd(&p.bab_q[(size_t)n_single * Cout + n0 + tid], s);
+      red_put(k, 1, slot, n_single * Cout + n0 + tid, s);  // the block's slot
     }
     __syncthreads();
   }
@@ -503,13 +528,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
       float s = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) s += red[w * BN + tid];
-      atomicAdd(&p.csum[(size_t)n_single * Cout + n0 + tid], s);
+      red_put(k, 2, slot, n_single * Cout + n0 + tid, s);
     }
     __syncthreads();
   }
   if (p.sdot && single) {
     // reduce the per-thread partial sums of equal channel chunks: lanes cc, cc+CPR, … of a wave
-    // by shuffles, then the waves through LDS, one atomic per channel per block
+    // by shuffles, then the waves through LDS, one partial per channel per block (its slot)
 #pragma unroll
     for (int e = 0; e < 8; ++e)
       for (int o = CPR; o < 64; o <<= 1) part[e] += __shfl_xor(part[e], o, 64);
@@ -523,7 +548,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
       float s = 0.f;
 #pragma unroll
       for (int w = 0; w < NW; ++w) s += red[w * BN + tid];
-      atomicAdd(&p.sdot[(size_t)n_single * Cout + n0 + tid], s);
+      red_put(k, 0, slot, n_single * Cout + n0 + tid, s);
     }
   }
 }

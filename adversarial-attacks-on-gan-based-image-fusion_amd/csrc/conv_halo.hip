@@ -283,7 +283,7 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
     const int img_row = n * H + y0;
     conv_epilogue<T, TL>(k, G, acc, smem, n0, true, n, [=](int r) {
       return (img_row + (r >> 4)) * W + x0 + (r & 15);
-    });
+    }, (y0 / TL::PH) * (W / TL::PW) + x0 / TL::PW);  // the patch's reduction slot
   }
 #ifdef MIA_HALO_TIMING
   HT_STAMP(t_end);
@@ -336,8 +336,16 @@ static int launch_halo_tile_(ConvK& k, hipStream_t st) {
   k.stagger_cycles = es ? (unsigned)atoi(es) : 0u;
   if (k.nblk < 4 * k.stagger_blocks) k.stagger_cycles = 0;  // short launches: not worth a tail
   k.prered = prered_enabled() && EPI >= 0 && (EPI & epi::CSUM);
+  const int H = k.a.H, W = k.a.W;
+  const int nslots = EPI >= 0    ? halo_red_slots(H, W, TL::FM, TL::WM, k.prered)
+                     : EPI == -1 ? halo_red_slots(H, W, TL::FM, TL::WM, false)
+                                 : (H / TL::PH) * (W / TL::PW);
+  RedQ r;
+  int rc = conv_red_begin(k, r, nslots, st);
+  if (rc != MIA_OK) return rc;
   hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), lds, st, k);
-  return check_launch("conv_halo");
+  rc = check_launch("conv_halo");
+  return rc != MIA_OK ? rc : red_finish(r, st);
 }
 
 template <typename T, typename TL, bool PRO, bool SPEC>

@@ -400,7 +400,7 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
     const int img_row = n * H + y0;
     conv_epilogue<float, TL>(k, G, acc, smem, n0, true, n, [=](int r) {
       return (img_row + (r >> 4)) * W + x0 + (r & 15);
-    });
+    }, (y0 / TL::PH) * (W / TL::PW) + x0 / TL::PW);  // the patch's reduction slot
   }
 #ifdef MIA_STAMPS
   if (wid == 0 && lane == 0) {
@@ -437,8 +437,16 @@ static int launch_x6_e(ConvK& k, hipStream_t st) {
     attr_set = true;
   }
   k.prered = prered_enabled() && EPI >= 0 && (EPI & epi::CSUM);
+  const int H = k.a.H, W = k.a.W;
+  const int nslots = EPI >= 0    ? halo_red_slots(H, W, TL::FM, TL::WM, k.prered)
+                     : EPI == -1 ? halo_red_slots(H, W, TL::FM, TL::WM, false)
+                                 : (H / TL::PH) * (W / TL::PW);
+  RedQ r;
+  int rc = conv_red_begin(k, r, nslots, st);
+  if (rc != MIA_OK) return rc;
   hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), lds, st, k);
-  return check_launch("conv_halo_x6");
+  rc = check_launch("conv_halo_x6");
+  return rc != MIA_OK ? rc : red_finish(r, st);
 }
 
 template <int BN_, bool PRO, int EPI>

@@ -309,12 +309,14 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
   } else {
     const int last = min(m0 + BM, G.m) - 1;
     const int n_first_img = m0 / HWo;
-    const bool single = n_first_img == last / HWo;
+    // sums: one partial per channel per tile (slot = the tile's index within its image) when
+    // the images are whole tiles, else one per output pixel (k.red_px: small images)
+    const bool single = n_first_img == last / HWo && !k.red_px;
     const int gm = G.m;
     conv_epilogue<T, TL>(k, G, acc, smem, n0, single, n_first_img, [=](int r) {
       const int m = m0 + r;
       return m < gm ? m : -1;
-    });
+    }, (m0 - n_first_img * HWo) / BM);
   }
 }
 
@@ -346,8 +348,22 @@ static int launch_tile(ConvK& k, hipStream_t st) {
   // off unless MIA_X6B_PRIO=1 (A/B)
   const char* pe = getenv("MIA_X6B_PRIO");
   k.prio = pe && atoi(pe) != 0;
+  // deterministic sums: contributor slots per (image, channel) (sums need one group, identity
+  // placement: run_conv)
+  const int HWo = k.g[0].ho * k.g[0].wo;
+  int nslots;
+  if constexpr (EPI >= 0) {  // register epilogue on the virtual (HWo/16 × 16) grid
+    nslots = halo_red_slots(HWo / 16, 16, TL::FM, TL::WM, k.prered);
+  } else {
+    k.red_px = HWo % TL::BM != 0;
+    nslots = k.red_px ? HWo : HWo / TL::BM;
+  }
+  RedQ r;
+  int rc = conv_red_begin(k, r, nslots, st);
+  if (rc != MIA_OK) return rc;
   hipLaunchKernelGGL(fn, dim3(blk), dim3(TL::NT), lds, st, k);
-  return check_launch("conv");
+  rc = check_launch("conv");
+  return rc != MIA_OK ? rc : red_finish(r, st);
 }
 
 typedef Tile<2, 2, 4, 2, 2> Tile128x64;
@@ -461,6 +477,17 @@ static int launch_conv(ConvK& k, hipStream_t st) {
   return small ? launch_bn<T, false, true>(k, st) : launch_bn<T, false, false>(k, st);
 }
 
+int conv_red_begin(ConvK& k, RedQ& r, int nslots, hipStream_t st, bool zero) {
+  const mia_conv_args& a = k.a;
+  const int count = a.N * a.Cout;
+  const int rc = red_begin(r, a.sdot, a.bab_demod ? a.bab_q : nullptr, a.csum, nslots, count, st,
+                           zero);
+  k.red_part = r.part;
+  k.red_nslots = nslots;
+  k.red_count = count;
+  return rc;
+}
+
 static int bk_for(int dtype) { return dtype == MIA_F32 ? 32 : 64; }
 
 static int kpad_for(int k, int dtype) {
@@ -485,7 +512,9 @@ static int run_conv(ConvK& k, int dtype, hipStream_t st) {
                 "bab_demod needs aux_x (stored activations, act_aux NONE), bab_q and y");
   MIA_CHECK_ARG(!a.tap_a || a.tap_t, "tap_a needs tap_t");
   MIA_CHECK_ARG(a.act_out != MIA_ACT_PRELU || a.act_slope, "MIA_ACT_PRELU needs act_slope");
-  MIA_CHECK_ARG(!a.csum || (a.y && !a.shuffle_out), "csum needs y (un-shuffled)");
+  MIA_CHECK_ARG(!a.csum || (a.y && !a.shuffle_out && k.ng == 1 &&
+                             k.g[0].ho * k.g[0].wo == k.HT * k.WT),
+                "csum needs y (un-shuffled), one group with an identity output placement");
   MIA_CHECK_ARG(!a.shuffle_out || !(a.tap_a || a.mask_a || a.sdot),
                 "aux inputs need un-shuffled output");
   MIA_CHECK_ARG((int64_t)a.N * a.H * a.W * a.Cin < (1LL << 31), "input too large for 32-bit offsets");

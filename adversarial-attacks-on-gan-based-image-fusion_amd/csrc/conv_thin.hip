@@ -222,9 +222,10 @@ struct Thin32Tile {
   static constexpr int FM = 1, FN = 2;
 };
 
-// the reductions of image n: the 16 pixel lanes by shuffles, then one atomic per channel
+// the reductions of image n: the 16 pixel lanes by shuffles, then one partial per channel into the
+// wave's slot for image n (its index among the waves whose runs meet image n)
 template <int EPI>
-__device__ __forceinline__ void thin32_flush(const mia_conv_args& p, EpiSums<2>& sums, int n,
+__device__ __forceinline__ void thin32_flush(const ConvK& k, EpiSums<2>& sums, int n, int slot,
                                              int frow, int fq) {
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -239,9 +240,9 @@ __device__ __forceinline__ void thin32_flush(const mia_conv_args& p, EpiSums<2>&
       }
       const int c = 16 * j + 4 * fq + e;
       if (frow == 0) {
-        if constexpr ((EPI & epi::SDOT) != 0) atomicAdd(&p.sdot[(size_t)n * 32 + c], a);
-        if constexpr ((EPI & epi::BAB) != 0) atomicAdd(&p.bab_q[(size_t)n * 32 + c], b);
-        if constexpr ((EPI & epi::CSUM) != 0) atomicAdd(&p.csum[(size_t)n * 32 + c], cs);
+        if constexpr ((EPI & epi::SDOT) != 0) red_put(k, 0, slot, n * 32 + c, a);
+        if constexpr ((EPI & epi::BAB) != 0) red_put(k, 1, slot, n * 32 + c, b);
+        if constexpr ((EPI & epi::CSUM) != 0) red_put(k, 2, slot, n * 32 + c, cs);
       }
       sums.part[j][e] = sums.partq[j][e] = sums.pcs[j][e] = 0.f;
     }
@@ -300,7 +301,7 @@ __global__ __launch_bounds__(256) void conv_thin32_kernel(const ConvK k) {
     if (g + 1 < g1) gather(g + 1, a_nxt);
     if (n != cur_n) {
       if constexpr (RED) {
-        if (cur_n >= 0) thin32_flush<EPI>(p, sums, cur_n, frow, fq);
+        if (cur_n >= 0) thin32_flush<EPI>(k, sums, cur_n, wave - (int)(cur_n * gpi / per), frow, fq);
       }
       cur_n = n;
       if constexpr (PRO) {
@@ -323,7 +324,7 @@ __global__ __launch_bounds__(256) void conv_thin32_kernel(const ConvK k) {
     for (int t = 0; t < 9; ++t) a_cur[t] = a_nxt[t];
   }
   if constexpr (RED) {
-    if (cur_n >= 0) thin32_flush<EPI>(p, sums, cur_n, frow, fq);
+    if (cur_n >= 0) thin32_flush<EPI>(k, sums, cur_n, wave - (int)(cur_n * gpi / per), frow, fq);
   }
 }
 
@@ -603,9 +604,18 @@ bool conv_thin32_eligible(const ConvK& k, int dtype) {
 }
 
 template <typename T, bool PRO, int F>
-static int launch_thin32_(const ConvK& k, int grid, hipStream_t st) {
+static int launch_thin32_(ConvK& k, int grid, hipStream_t st) {
+  // the waves walk contiguous runs of `per` 16-pixel groups: the waves meeting image n are
+  // wave (n·gpi)/per … , at most gpi/per + 2 of them (slots without a contributor stay 0)
+  const int64_t gpi = (int64_t)k.a.H * (k.a.W / 16);
+  const int64_t nwaves = (int64_t)grid * 4;
+  const int64_t per = ((int64_t)k.a.N * gpi + nwaves - 1) / nwaves;
+  RedQ r;
+  int rc = conv_red_begin(k, r, (int)(gpi / per + 2), st, true);
+  if (rc != MIA_OK) return rc;
   hipLaunchKernelGGL((conv_thin32_kernel<T, PRO, F>), dim3(grid), dim3(256), 0, st, k);
-  return check_launch("conv_thin32");
+  rc = check_launch("conv_thin32");
+  return rc != MIA_OK ? rc : red_finish(r, st);
 }
 
 int launch_conv_thin32(ConvK& k, int dtype, hipStream_t st) {

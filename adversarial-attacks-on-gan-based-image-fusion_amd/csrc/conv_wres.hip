@@ -221,8 +221,13 @@ static int launch_wres_(ConvK& k, int grid, size_t lds, hipStream_t st) {
       return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     attr_set = true;
   }
+  RedQ r;
+  int rc = conv_red_begin(k, r,
+                          halo_red_slots(k.a.H, k.a.W, WresTile::FM, WresTile::NW, k.prered), st);
+  if (rc != MIA_OK) return rc;
   hipLaunchKernelGGL(fn, dim3(grid), dim3(WresTile::NT), lds, st, k);
-  return check_launch("conv_wres");
+  rc = check_launch("conv_wres");
+  return rc != MIA_OK ? rc : red_finish(r, st);
 }
 
 // the epilogue feature masks with a specialisation (the runtime-feature epilogue would spill next

@@ -118,10 +118,11 @@ __global__ __launch_bounds__(256) void se_apply_kernel(const T* __restrict__ r,
   }
 }
 
-// ---- gs[n][c] += Σ_p a·b: block (chunk, n); lanes own 8-channel vectors, LDS reduction ----------
+// ---- gs[n][c] += Σ_p a·b: block (chunk, n); lanes own 8-channel vectors, LDS reduction; the
+// block's partial goes to its slot (chunk) of the library's reduction scratch (red_finish) -------
 template <typename T>
 __global__ __launch_bounds__(256) void chan_dot_kernel(const T* __restrict__ a,
-                                                       const T* __restrict__ b, float* gs, int HW,
+                                                       const T* __restrict__ b, float* part, int HW,
                                                        int C, int pix_per_chunk) {
   __shared__ float red[256 * 8];
   const int n = blockIdx.y, tid = threadIdx.x;
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(256) void chan_dot_kernel(const T* __restrict__ a,
     for (int e = 0; e < 8; ++e) {
       float s = 0.f;
       for (int q = 0; q < pr; ++q) s += red[(q * lanes_per_pix + tid) * 8 + e];
-      atomicAdd(&gs[(size_t)n * C + tid * 8 + e], s);
+      red_store(part, gridDim.x, gridDim.y * C, 0, blockIdx.x, n * C + tid * 8 + e, s);
     }
   }
 }
@@ -447,6 +448,13 @@ extern "C" int mia_se_apply(const void* r, const float* s, const void* sc, int s
   return check_launch("se_apply");
 }
 
+// pixel chunks per image: a function of HW only, so an image's sums are the same fp32 additions
+// whatever the batch (batch-1 and batch-N runs agree bit for bit)
+static int chan_chunks(int N, int HW) {
+  (void)N;
+  return std::max(1, std::min(HW / 16, 32));
+}
+
 extern "C" int mia_chan_dot(const void* a, const void* b, float* gs, int N, int HW, int C,
                             int accumulate, int dtype, void* stream) {
   MIA_CHECK_ARG(a && b && gs && N > 0 && HW > 0, "bad args");
@@ -455,15 +463,18 @@ extern "C" int mia_chan_dot(const void* a, const void* b, float* gs, int N, int 
   hipStream_t st = (hipStream_t)stream;
   if (!accumulate && hipMemsetAsync(gs, 0, (size_t)N * C * sizeof(float), st) != hipSuccess)
     return set_error("chan_dot: memset failed");
-  const int chunks = std::max(1, std::min(HW / 16, 4096 / N + 1));
+  const int chunks = chan_chunks(N, HW);
   const int ppc = (HW + chunks - 1) / chunks;
   const int nch = (HW + ppc - 1) / ppc;
+  RedQ r;
+  int rc = red_begin(r, gs, nullptr, nullptr, nch, N * C, st);
+  if (rc != MIA_OK) return rc;
   MIA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(chan_dot_kernel<T>, dim3(nch, N), dim3(256), 0,
-                                                  st, (const T*)a, (const T*)b, gs, HW, C, ppc));
-  return check_launch("chan_dot");
+                                                  st, (const T*)a, (const T*)b, r.part, HW, C,
+                                                  ppc));
+  rc = check_launch("chan_dot");
+  return rc != MIA_OK ? rc : red_finish(r, st);
 }
-
-static int chan_chunks(int N, int HW) { return std::max(1, std::min(HW / 16, 4096 / N + 1)); }
 
 extern "C" int mia_chan_sum_parts(int N, int HW) {
   const int chunks = chan_chunks(N, HW);

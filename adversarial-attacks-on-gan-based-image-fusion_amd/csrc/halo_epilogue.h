@@ -19,8 +19,8 @@ __device__ __forceinline__ void ld4f(const float* p, float (&v)[4]) {
 // channels × patch pixels), so for every fragment a lane holds 4 consecutive output channels of
 // one pixel: each per-element operation of conv_epilogue (same order, same semantics) runs in
 // registers with 8-/16-byte aux loads and stores and no LDS staging. The sdot / q reductions sum
-// a lane's pixels, then the 16 pixel lanes of a channel group by shuffles, then one atomic per
-// channel per wave.
+// a lane's pixels, then the 16 pixel lanes of a channel group by shuffles, then one partial per
+// channel per wave into the launch's reduction slots (red_put; added up in order after it).
 template <typename T, typename TL>
 __device__ __forceinline__ void halo_epilogue(const ConvK& k, const f32x4 (&acc)[TL::FM][TL::FN],
                                               int n, int y0, int x0, int n0, int wm, int wn,
@@ -162,6 +162,8 @@ __device__ __forceinline__ void halo_epilogue(const ConvK& k, const f32x4 (&acc)
     }
   }
   if (p.sdot || bab || p.csum) {
+    // this wave's FM rows × 16 columns are one contributor slot (halo_red_slot)
+    const int slot = halo_red_slot(y0 + wm * FM, x0, FM, W);
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int c = cl + 16 * j;
@@ -175,9 +177,10 @@ __device__ __forceinline__ void halo_epilogue(const ConvK& k, const f32x4 (&acc)
           cs += __shfl_xor(cs, o, 64);
         }
         if (px == 0 && c < Cout) {
-          if (p.sdot) atomicAdd(&p.sdot[(size_t)n * Cout + c + e], a);
-          if (bab) atomicAdd(&p.bab_q[(size_t)n * Cout + c + e], b);
-          if (p.csum) atomicAdd(&p.csum[(size_t)n * Cout + c + e], cs);
+          const int i = n * Cout + c + e;
+          if (p.sdot) red_put(k, 0, slot, i, a);
+          if (bab) red_put(k, 1, slot, i, b);
+          if (p.csum) red_put(k, 2, slot, i, cs);
         }
       }
     }
@@ -215,7 +218,7 @@ struct EpiChunk {  // rows per aux-load chunk (bounds the live registers for tal
 };
 
 // Per-lane partial sums of the reductions (sdot, q, csum), kept across calls by a caller that
-// flushes them itself (conv_thin.hip: one flush per image run instead of atomics per call).
+// flushes them itself (conv_thin.hip: one flush per image run instead of one per call).
 template <int FN>
 struct EpiSums {
   float part[FN][4], partq[FN][4], pcs[FN][4];
@@ -402,6 +405,9 @@ __device__ __forceinline__ void halo_epilogue_f(
         }
       return;
     }
+    const bool lds_red = red != nullptr && nwm > 1;
+    const int rh = halo_red_h(FM, nwm, lds_red);  // contributor rows: the wave's or the block's
+    const int slot = halo_red_slot(lds_red ? y0 : y0 + wm * FM, x0, rh, W);
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int c = cl + 16 * j;
@@ -414,7 +420,7 @@ __device__ __forceinline__ void halo_epilogue_f(
           if constexpr (BAB) b += __shfl_xor(b, o, 64);
           if constexpr (CSUM) cs += __shfl_xor(cs, o, 64);
         }
-        if (red != nullptr && nwm > 1) {  // (quantity, wave row, block channel) in LDS
+        if (lds_red) {  // (quantity, wave row, block channel) in LDS
           if (px == 0) {
             const int lc = c - n0 + e;
             int qi = 0;
@@ -423,15 +429,16 @@ __device__ __forceinline__ void halo_epilogue_f(
             if constexpr (CSUM) red[(qi++ * nwm + wm) * cw + lc] = cs;
           }
         } else if (px == 0 && c < Cout) {
-          if constexpr (SDOT) atomicAdd(&p.sdot[(size_t)n * Cout + c + e], a);
-          if constexpr (BAB) atomicAdd(&p.bab_q[(size_t)n * Cout + c + e], b);
-          if constexpr (CSUM) atomicAdd(&p.csum[(size_t)n * Cout + c + e], cs);
+          const int i = n * Cout + c + e;
+          if constexpr (SDOT) red_put(k, 0, slot, i, a);
+          if constexpr (BAB) red_put(k, 1, slot, i, b);
+          if constexpr (CSUM) red_put(k, 2, slot, i, cs);
         }
       }
     }
-    if (red != nullptr && nwm > 1) {
-      // the waves of one channel range meet here; the first wave row sums them and issues one
-      // atomic per channel (nwm× fewer atomics)
+    if (lds_red) {
+      // the waves of one channel range meet here; the first wave row sums them (in wave order)
+      // and stores one partial per channel for the block (nwm× fewer partials)
       __syncthreads();
       if (wm == 0 && px == 0) {
 #pragma unroll
@@ -442,14 +449,13 @@ __device__ __forceinline__ void halo_epilogue_f(
             if (c >= Cout) continue;
             const int lc = c - n0 + e;
             int qi = 0;
-            float* dst[3] = {SDOT ? p.sdot : nullptr, BAB ? p.bab_q : nullptr,
-                             CSUM ? p.csum : nullptr};
+            const bool has[3] = {SDOT, BAB, CSUM};
 #pragma unroll
             for (int qq = 0; qq < 3; ++qq) {
-              if (dst[qq] == nullptr) continue;
+              if (!has[qq]) continue;
               float t = 0.f;
               for (int w = 0; w < nwm; ++w) t += red[(qi * nwm + w) * cw + lc];
-              atomicAdd(&dst[qq][(size_t)n * Cout + c + e], t);
+              red_put(k, qq, slot, n * Cout + c + e, t);
               ++qi;
             }
           }

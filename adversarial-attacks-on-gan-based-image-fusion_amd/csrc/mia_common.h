@@ -48,6 +48,33 @@ __device__ __forceinline__ float wave_sum(float v) {
 int set_error(const std::string& msg);
 int check_launch(const char* what);
 
+// ---- deterministic reductions (reduce.hip) ---------------------------------------------------
+// Per-(image, channel) sums that many blocks contribute to (the StyledConv style gradient sdot,
+// the backward front's q, the channel sums, per-image losses) never use float atomics: every
+// contributor stores its partial into its own SLOT of a partial buffer, and red_finish adds the
+// slots of each output IN SLOT ORDER after the launch. The result is bit-identical run to run,
+// and an image's sums do not depend on which other images share the launch. Partial layout:
+// part[(q·nslots + slot)·count + i] for quantity q (up to 3 per launch), output i < count.
+struct RedQ {
+  float* dst[3];     // outputs (+= the ordered slot sum); nullptr = quantity absent
+  float* part;       // partial buffer (library scratch of this stream, red_scratch)
+  int nslots, count; // slots per output, outputs per quantity
+};
+// library-owned device scratch of at least `bytes` for `st` (grown on demand, kept per stream;
+// growth synchronises the stream before releasing the old buffer)
+float* red_scratch(hipStream_t st, size_t bytes);
+// partial buffer for the quantities of dst[] (nslots × count each); zero = clear it first (for
+// launches in which some slots may have no contributor). Returns MIA_OK or an error code.
+int red_begin(RedQ& r, float* d0, float* d1, float* d2, int nslots, int count, hipStream_t st,
+              bool zero = false);
+// dst_q[i] += Σ_{slot = 0 … nslots−1} part[q][slot][i], in slot order
+int red_finish(const RedQ& r, hipStream_t st);
+
+__device__ __forceinline__ void red_store(float* part, int nslots, int count, int q, int slot,
+                                          int i, float v) {
+  part[((size_t)q * nslots + slot) * count + i] = v;
+}
+
 }  // namespace mia
 
 #define MIA_DISPATCH_DTYPE(dtype, T, ...)                                   \

@@ -40,8 +40,8 @@ template <typename T>
 __global__ void bias_act_bwd_kernel(const T* __restrict__ g_a, const T* __restrict__ pre,
                                     const float* __restrict__ noise, float nw,
                                     const float* __restrict__ bias, const float* __restrict__ demod,
-                                    T* __restrict__ gy, float* __restrict__ q, int H, int W, int C,
-                                    int unshuffle, int from_act, int pix_per_block) {
+                                    T* __restrict__ gy, float* __restrict__ qpart, int H, int W,
+                                    int C, int unshuffle, int from_act, int pix_per_block) {
   typedef typename Vec<T>::type VT;
   constexpr int V = Vec<T>::N;
   __shared__ float red[TPB * 8];
@@ -97,8 +97,10 @@ __global__ void bias_act_bwd_kernel(const T* __restrict__ g_a, const T* __restri
     for (int s = 1; s < ppp; ++s)
 #pragma unroll
       for (int e = 0; e < V; ++e) qa[e] += red[(s * tpp + chunk) * V + e];
+    // the block's partial into its slot (blockIdx.x); red_finish adds the slots in order
 #pragma unroll
-    for (int e = 0; e < V; ++e) atomicAdd(&q[(size_t)n * C + c0 + e], qa[e]);
+    for (int e = 0; e < V; ++e)
+      red_store(qpart, gridDim.x, gridDim.y * C, 0, blockIdx.x, n * C + c0 + e, qa[e]);
   }
 }
 
@@ -404,8 +406,9 @@ struct TorgbFront {
 template <typename T, bool FRONT>
 __global__ void torgb_bwd_kernel(const float* __restrict__ grgb, const T* __restrict__ pre,
                                  const float* __restrict__ s, const float* __restrict__ wr,
-                                 T* __restrict__ g_a, float* __restrict__ gs, int H, int W, int Cin,
-                                 int accumulate, int pix_per_block, int act_in, TorgbFront fr) {
+                                 T* __restrict__ g_a, float* __restrict__ part_out, int H, int W,
+                                 int Cin, int accumulate, int pix_per_block, int act_in,
+                                 TorgbFront fr) {
   typedef typename Vec<T>::type VT;
   constexpr int V = Vec<T>::N;
   extern __shared__ float sh[];  // wr [3][Cin], s [Cin], partials [TPB/tpp][Cin] (× 2 if FRONT)
@@ -478,8 +481,9 @@ __global__ void torgb_bwd_kernel(const float* __restrict__ grgb, const T* __rest
       sum += part[sb * Cin + c];
       if (FRONT) sq += partq[sb * Cin + c];
     }
-    atomicAdd(&gs[(size_t)n * Cin + c], sum);
-    if (FRONT) atomicAdd(&fr.q[(size_t)n * Cin + c], sq);
+    // the block's partials into its slot (blockIdx.x): gs (quantity 0) and q (1)
+    red_store(part_out, gridDim.x, gridDim.y * Cin, 0, blockIdx.x, n * Cin + c, sum);
+    if (FRONT) red_store(part_out, gridDim.x, gridDim.y * Cin, 1, blockIdx.x, n * Cin + c, sq);
   }
 }
 
@@ -648,7 +652,7 @@ __global__ void image_to_nhwc_kernel(const float* __restrict__ x, T* __restrict_
 // MSE pieces (K10).
 template <typename T>
 __global__ void mse_sum_kernel(const T* __restrict__ a, const T* __restrict__ b,
-                               float* __restrict__ loss, int64_t len, float coef) {
+                               float* __restrict__ part, int64_t len, float coef) {
   const int n = blockIdx.y;
   const T* pa = a + (size_t)n * len;
   const T* pb = b + (size_t)n * len;
@@ -664,7 +668,7 @@ __global__ void mse_sum_kernel(const T* __restrict__ a, const T* __restrict__ b,
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int w = 0; w < TPB / 64; ++w) s += red[w];
-    atomicAdd(&loss[n], coef * s);
+    red_store(part, gridDim.x, gridDim.y, 0, blockIdx.x, n, coef * s);  // the block's slot
   }
 }
 
@@ -948,10 +952,15 @@ extern "C" int mia_bias_act_bwd(const void* g_a, const void* pre, const float* n
   const int ppp = TPB / (C / V);
   const int ppb = ppp * 16;
   dim3 grid((HW + ppb - 1) / ppb, N);
+  RedQ r;
+  int rc = red_begin(r, q, nullptr, nullptr, grid.x, N * C, (hipStream_t)stream);
+  if (rc != MIA_OK) return rc;
   MIA_DISPATCH_DTYPE(dtype, T,
-      MIA_LAUNCH(bias_act_bwd_kernel<T>, grid, dim3(TPB), 0, (const T*)g_a, (const T*)pre, noise,
-                 noise_w, bias, demod, (T*)gy, q, H, W, C, unshuffle, from_act, ppb));
-  return MIA_OK;
+      hipLaunchKernelGGL(bias_act_bwd_kernel<T>, grid, dim3(TPB), 0, (hipStream_t)stream,
+                         (const T*)g_a, (const T*)pre, noise, noise_w, bias, demod, (T*)gy, r.part,
+                         H, W, C, unshuffle, from_act, ppb));
+  rc = check_launch("bias_act_bwd_kernel");
+  return rc != MIA_OK ? rc : red_finish(r, (hipStream_t)stream);
 }
 
 extern "C" int mia_upconv_blur_fwd(const void* t, void* pre, const float* demod,
@@ -1055,10 +1064,15 @@ extern "C" int mia_torgb_bwd(const float* g_rgb, const void* pre, const float* s
   const size_t sh = (4 * Cin + (size_t)ppp * Cin) * sizeof(float);
   MIA_CHECK_ARG(sh <= 64 * 1024, "LDS budget");
   const TorgbFront fr{};
+  RedQ r;
+  int rc = red_begin(r, gs, nullptr, nullptr, grid.x, N * Cin, (hipStream_t)stream);
+  if (rc != MIA_OK) return rc;
   MIA_DISPATCH_DTYPE(dtype, T,
-      MIA_LAUNCH((torgb_bwd_kernel<T, false>), grid, dim3(TPB), sh, g_rgb, (const T*)pre, style,
-                 wr, (T*)g_a, gs, H, W, Cin, accumulate, ppb, act_in, fr));
-  return MIA_OK;
+      hipLaunchKernelGGL((torgb_bwd_kernel<T, false>), grid, dim3(TPB), sh, (hipStream_t)stream,
+                         g_rgb, (const T*)pre, style, wr, (T*)g_a, r.part, H, W, Cin, accumulate,
+                         ppb, act_in, fr));
+  rc = check_launch("torgb_bwd_kernel");
+  return rc != MIA_OK ? rc : red_finish(r, (hipStream_t)stream);
 }
 
 extern "C" int mia_torgb_bwd_front(const float* g_rgb, const void* act, const float* style,
@@ -1074,10 +1088,15 @@ extern "C" int mia_torgb_bwd_front(const float* g_rgb, const void* act, const fl
   const size_t sh = (4 * Cin + 2 * (size_t)ppp * Cin) * sizeof(float);
   MIA_CHECK_ARG(sh <= 64 * 1024, "LDS budget");
   const TorgbFront fr{demod, noise, noise_w, bias, q};
+  RedQ r;
+  int rc = red_begin(r, gs, q, nullptr, grid.x, N * Cin, (hipStream_t)stream);
+  if (rc != MIA_OK) return rc;
   MIA_DISPATCH_DTYPE(dtype, T,
-      MIA_LAUNCH((torgb_bwd_kernel<T, true>), grid, dim3(TPB), sh, g_rgb, (const T*)act, style,
-                 wr, (T*)gy, gs, H, W, Cin, 0, ppb, MIA_ACT_NONE, fr));
-  return MIA_OK;
+      hipLaunchKernelGGL((torgb_bwd_kernel<T, true>), grid, dim3(TPB), sh, (hipStream_t)stream,
+                         g_rgb, (const T*)act, style, wr, (T*)gy, r.part, H, W, Cin, 0, ppb,
+                         MIA_ACT_NONE, fr));
+  rc = check_launch("torgb_bwd_kernel");
+  return rc != MIA_OK ? rc : red_finish(r, (hipStream_t)stream);
 }
 
 static inline int pool_out(int H, int ceil_mode) { return ceil_mode ? (H + 1) / 2 : H / 2; }
@@ -1147,9 +1166,14 @@ extern "C" int mia_mse_sum(const void* a, const void* b, float* loss, int n, int
                            float coef, int dtype, void* stream) {
   MIA_CHECK_ARG(a && b && loss && n > 0 && len > 0, "bad args");
   dim3 grid(blocks_for(len, TPB, 1024), n);
+  RedQ r;
+  int rc = red_begin(r, loss, nullptr, nullptr, grid.x, n, (hipStream_t)stream);
+  if (rc != MIA_OK) return rc;
   MIA_DISPATCH_DTYPE(dtype, T,
-      MIA_LAUNCH(mse_sum_kernel<T>, grid, dim3(TPB), 0, (const T*)a, (const T*)b, loss, len, coef));
-  return MIA_OK;
+      hipLaunchKernelGGL(mse_sum_kernel<T>, grid, dim3(TPB), 0, (hipStream_t)stream, (const T*)a,
+                         (const T*)b, r.part, len, coef));
+  rc = check_launch("mse_sum_kernel");
+  return rc != MIA_OK ? rc : red_finish(r, (hipStream_t)stream);
 }
 
 extern "C" int mia_mse_grad_f32(const float* a, const float* b, float* g, int64_t len, float coef,

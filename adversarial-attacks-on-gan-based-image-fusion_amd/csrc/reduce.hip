@@ -1,0 +1,127 @@
+// Deterministic reductions (mia_common.h, RedQ): library-owned partial buffers per stream and the
+// ordered finish. Replaces float atomics across blocks wherever several blocks add into one
+// per-(image, channel) sum: with atomics the summation order — and so the fp32 result — changed
+// run to run (SURVEY.md §5 asks for bit-identical reruns; the reference runs with
+// cudnn.deterministic, code/attack/interpolation.py:195-200).
+#include <algorithm>
+#include <mutex>
+#include <unordered_map>
+
+#include "mia_common.h"
+
+namespace mia {
+
+namespace {
+struct Scratch {
+  float* p = nullptr;
+  size_t bytes = 0;
+};
+std::mutex g_mu;
+std::unordered_map<hipStream_t, Scratch> g_scratch;
+}  // namespace
+
+float* red_scratch(hipStream_t st, size_t bytes) {
+  std::lock_guard<std::mutex> lock(g_mu);
+  Scratch& s = g_scratch[st];
+  if (s.bytes >= bytes) return s.p;
+  if (s.p) {  // kernels queued on this stream may still read / write the old buffer
+    if (hipStreamSynchronize(st) != hipSuccess || hipFree(s.p) != hipSuccess) return nullptr;
+    s.p = nullptr;
+    s.bytes = 0;
+  }
+  // grow geometrically: the partial footprint of a step varies per layer
+  size_t want = bytes < (1u << 20) ? (1u << 20) : bytes;
+  want = want + want / 4;
+  void* p = nullptr;
+  if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+  s.p = (float*)p;
+  s.bytes = want;
+  return s.p;
+}
+
+int red_begin(RedQ& r, float* d0, float* d1, float* d2, int nslots, int count, hipStream_t st,
+              bool zero) {
+  r.dst[0] = d0;
+  r.dst[1] = d1;
+  r.dst[2] = d2;
+  r.nslots = nslots;
+  r.count = count;
+  r.part = nullptr;
+  if (!d0 && !d1 && !d2) return MIA_OK;
+  if (nslots < 1 || count < 1) return set_error("red_begin: empty reduction");
+  const size_t bytes = (size_t)3 * nslots * count * sizeof(float);
+  r.part = red_scratch(st, bytes);
+  if (!r.part) return set_error("red_begin: scratch allocation failed");
+  if (zero && hipMemsetAsync(r.part, 0, bytes, st) != hipSuccess)
+    return set_error("red_begin: memset failed");
+  return MIA_OK;
+}
+
+__global__ __launch_bounds__(256) void red_finish_kernel(const float* __restrict__ part,
+                                                         float* d0, float* d1, float* d2,
+                                                         int nslots, int count) {
+  const int q = blockIdx.y;
+  float* dst = q == 0 ? d0 : (q == 1 ? d1 : d2);
+  if (!dst) return;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= count) return;
+  const float* src = part + (size_t)q * nslots * count + i;
+  float s = 0.f;
+  for (int k = 0; k < nslots; ++k) s += src[(size_t)k * count];
+  dst[i] += s;
+}
+
+int red_finish(const RedQ& r, hipStream_t st) {
+  if (!r.part) return MIA_OK;
+  hipLaunchKernelGGL(red_finish_kernel, dim3((r.count + 255) / 256, 3), dim3(256), 0, st, r.part,
+                     r.dst[0], r.dst[1], r.dst[2], r.nslots, r.count);
+  return check_launch("red_finish");
+}
+
+}  // namespace mia
+
+using namespace mia;
+
+// Slots per output: a register-epilogue contributor covers ≥ 16 pixels (one 16-column row
+// segment), the thin32 kernel's at most H·W/16 + 2 waves meet one image; only the LDS-staged
+// epilogue on images that are not whole tiles (H·W not a multiple of the tile rows) falls back to
+// one slot per pixel. The scratch always holds 3 quantities' slots (sdot, bab_q, csum).
+extern "C" int64_t mia_conv_workspace_size(int N, int H_out, int W_out, int Cout, int has_sums) {
+  if (!has_sums || N <= 0 || H_out <= 0 || W_out <= 0 || Cout <= 0) return 0;
+  const int64_t hw = (int64_t)H_out * W_out;
+  const int64_t slots = hw % 256 == 0 ? hw / 16 + 2 : hw + 2;
+  return (int64_t)3 * slots * N * Cout * (int64_t)sizeof(float);
+}
+
+// pointwise reductions: one slot per block of ≥ 16 pixels (bias_act / torgb: 16 pixel passes of
+// ≥ 1 pixel; chan_dot: ≤ 32 chunks; mse_sum: ≤ 1024 blocks of 256 elements)
+extern "C" int64_t mia_reduction_workspace_size(int N, int HW, int C) {
+  if (N <= 0 || HW <= 0 || C <= 0) return 0;
+  const int64_t slots = std::max<int64_t>(1024, HW);
+  return (int64_t)3 * slots * N * C * (int64_t)sizeof(float);
+}
+
+extern "C" int mia_reserve_reduction_scratch(int64_t bytes, void* stream) {
+  MIA_CHECK_ARG(bytes >= 0, "bytes must be >= 0");
+  if (bytes == 0) return MIA_OK;
+  return red_scratch((hipStream_t)stream, (size_t)bytes) ? MIA_OK
+                                                         : set_error("scratch allocation failed");
+}
+
+extern "C" int64_t mia_reduction_scratch_bytes(void* stream) {
+  std::lock_guard<std::mutex> lock(g_mu);
+  auto it = g_scratch.find((hipStream_t)stream);
+  return it == g_scratch.end() ? 0 : (int64_t)it->second.bytes;
+}
+
+extern "C" int mia_release_reduction_scratch(void* stream) {
+  std::lock_guard<std::mutex> lock(g_mu);
+  auto it = g_scratch.find((hipStream_t)stream);
+  if (it == g_scratch.end()) return MIA_OK;
+  if (it->second.p) {
+    if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess || hipFree(it->second.p) != hipSuccess)
+      return set_error("scratch release failed");
+  }
+  g_scratch.erase(it);
+  return MIA_OK;
+}

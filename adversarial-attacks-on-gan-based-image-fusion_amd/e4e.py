@@ -278,9 +278,9 @@ class E4EEncoder:
             r = self._buf(ws, f"r_{i}", (N, ho, ho, d))
             cs = self._buf(ws, f"cs_{i}", (N, d), f32)
             ops.conv2d(a1, [_g3(U["w2"], ho)], r, (ho, ho), cout=d, stride=s, bias=U["b2"])
-            # the SE average pool's sum: a deterministic reduction (not the conv epilogue's block
-            # atomics), so the forward — and the PReLU / ReLU branches after it — reproduce bit
-            # for bit run to run
+            # the SE average pool's sum: an ordered two-pass reduction with per-image pixel
+            # chunks (mia_chan_sum), so the forward — and the PReLU / ReLU branches after it —
+            # reproduce bit for bit run to run and batch to batch
             ops.chan_sum(r, None, self._chan_part(ws, N, ho * ho, d), cs)
             u = self._buf(ws, f"u_{i}", (N, U["cr"]), f32)
             sv = self._buf(ws, f"s_{i}", (N, d), f32)

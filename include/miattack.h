@@ -15,6 +15,14 @@
  *   - `stream` is a hipStream_t; every call is asynchronous on it, stateless and re-entrant.
  *   - Every call returns 0 on success or a negative MIA_E* code; mia_last_error_string() (per
  *     thread) gives detail. No C++ exception crosses the ABI.
+ *   - Deterministic reductions: no float atomics. Every per-(image, channel) / per-image sum that
+ *     several blocks contribute to (sdot, bab_q, csum, the torgb / bias_act style and q sums,
+ *     mia_mse_sum's loss, mia_chan_dot) is written as per-block partials into a device scratch
+ *     the library keeps PER STREAM, then added in a fixed order by a finish kernel on the same
+ *     stream: results are bit-identical run to run, and an image's sums do not depend on the
+ *     other images of the call. The scratch grows on first use (a synchronising hipMalloc; the
+ *     old buffer is freed after a stream synchronise); mia_reserve_reduction_scratch pre-sizes
+ *     it from the *_workspace_size queries below so that no step allocates.
  */
 #ifndef MIATTACK_H
 #define MIATTACK_H
@@ -40,6 +48,23 @@ extern "C" {
 
 int mia_version(void);
 const char* mia_last_error_string(void);
+
+/* ---- reduction scratch (see Conventions) ----------------------------------------------------
+ * Upper bounds of the scratch bytes one call needs:
+ *   mia_conv_workspace_size — mia_conv3x3 / mia_conv2d / mia_upconv_dgrad* with sdot / bab_q /
+ *     csum for N images of an H_out × W_out output with Cout channels (0 without sums);
+ *   mia_reduction_workspace_size — the pixel-chunked pointwise reductions (bias_act_bwd,
+ *     torgb_bwd[_front], chan_dot: N images of HW pixels × C channels; mse_sum: C = 1).
+ * Replaces: nothing in the reference (cuDNN / the rosinality ops allocate their own workspace);
+ * the SURVEY.md §8(b) contract's workspace queries. */
+int64_t mia_conv_workspace_size(int N, int H_out, int W_out, int Cout, int has_sums);
+int64_t mia_reduction_workspace_size(int N, int HW, int C);
+/* ensure the stream's scratch holds at least `bytes` (synchronises `stream` if it grows) */
+int mia_reserve_reduction_scratch(int64_t bytes, void* stream);
+/* bytes the stream's scratch holds now (0 if none) */
+int64_t mia_reduction_scratch_bytes(void* stream);
+/* free the stream's scratch (synchronises `stream`) */
+int mia_release_reduction_scratch(void* stream);
 /* K-padding the conv weights need for `dtype` (weights are [Cout][Kpad], K = 9*Cin). */
 int mia_conv_kpad(int cin, int dtype);
 

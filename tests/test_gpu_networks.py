@@ -71,6 +71,10 @@ def test_vgg_taps_and_grad_vs_reference_golden(cuda, golden, dtype, tol):
         # ReLU masks of near-zero pre-activations flip between summation orders, so the input
         # gradient is compared in norm (plus a loose max) rather than element-wise
         nrm = ((got - ref).norm() / ref.norm()).item()
+        stable = ref.abs() > 1e-3 * ref.abs().max()
+        st_mx = ((got - ref).abs()[stable].max() / ref.abs().max()).item()
+        print(f"VGG golden grad {dtype} {tag}: norm {nrm:.2e} max {rel_err(got, ref):.2e} "
+              f"max on |g| > 1e-3·max {st_mx:.2e}")
         assert nrm < 30 * tol and rel_err(got, ref) < 100 * tol, (tag, "grad", nrm)
         assert gx[..., 3:].abs().max().item() == 0.0
 
@@ -197,8 +201,8 @@ def test_cw_mode_matches_oracle(cuda, c):
     """norm='l2_cw' (torchattacks C&W composed with the objective) vs the oracle restatement:
     tanh space, Adam on w, best-L2 selection with success = objective below the clean image's.
     At c = 1e-4 the success test is a near-tie: it needs the fp32 path to be run-to-run
-    deterministic (one sdot atomic per (image, channel) at 32², conv_mfma.hip keeps the 128-row
-    tiles in fp32), else a whole image may select a different iterate."""
+    deterministic (every per-(image, channel) sum is an ordered reduction, mia_common.h RedQ),
+    else a whole image may select a different iterate."""
     size, N, steps, lr = 32, 2, 4, 0.01
     eng, x0, t, (gp, vp, ep) = _engine(size, torch.float32, N, cuda, seed=6)
     adv = eng.run_cw(x0.to(cuda), t.to(cuda), steps, c=c, lr=lr).cpu()

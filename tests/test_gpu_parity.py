@@ -42,33 +42,55 @@ def test_objective_and_gradient_match_reference_optimize_vgg(cuda, objg, kind):
     e4e, whose full iteration-0 gradient the fixture holds — the gradient at the first Adam
     iterate x1 = x0 − lr·g0/(|g0| + 1e-8) (Adam's first step, exact)."""
     size, lr = int(objg["size"]), float(objg["lr"])
-    eng, _ = engine(size, torch.float32, cuda, encoder=kind)
+    eng, params = engine(size, torch.float32, cuda, encoder=kind)
     x0, t = gen.seeded_pair(size)
     eng.prepare(x0.to(cuda), t.to(cuda))
     L0 = float(eng.loss(x0.to(cuda))[0])
     ref_L0 = float(objg[f"{kind}/losses"][0])
-    # fp32 sums vs '%.5f'; the e4e's SE channel sums are block atomics (fp32 summation order
-    # varies run to run) and its PReLU / LeakyReLU(0.01) branches of activations within rounding
-    # of 0 follow: measured run-to-run spread of the e4e objective ≈ 1e-5 relative
-    assert abs(L0 - ref_L0) <= 5e-6 + 2e-5 * abs(ref_L0), (L0, ref_L0)
-    g0 = eng.full_gradient(x0.to(cuda)).cpu().double()
+    # fp32 sums vs the reference's '%.5f' text (±5e-6) + 1e-5 relative: the fp32 arithmetic and,
+    # for e4e, its unforced PReLU / LeakyReLU branches within rounding of 0 (measured e4e
+    # 9.1e-5 = 8.0e-6 relative; the device run is bit-reproducible, ordered reductions)
+    print(f"{kind}: L0 {L0:.8f} vs reference {ref_L0:.5f} (Δ {abs(L0 - ref_L0):.2e})")
+    assert abs(L0 - ref_L0) <= 5e-6 + 1e-5 * abs(ref_L0), (L0, ref_L0)
+    with capture_vgg(eng.V) as cap:
+        g0 = eng.full_gradient(x0.to(cuda)).cpu().double()
     probes = gen.projections(size)
     proj_rel = _rel([float((p * g0).sum()) for p in probes], objg[f"{kind}/grad0/proj"])
+    print(f"{kind}: gradient projections rel {proj_rel:.2e}")
     if kind == "linear":
-        assert _rel(g0[gen.SLICE], objg["linear/grad0/slice"]) < 1e-3
         assert proj_rel < 1e-3
-    else:
-        # the e4e's LeakyReLU(0.01) / PReLU branches of activations within rounding of 0 may go
-        # the other way in fp32 (the fixture cannot be mask-forced): norm / sign criteria here,
-        # exactness mask-for-mask in test_e4e_attack_gradient_mask_for_mask
-        assert proj_rel < 3e-2
+        assert _rel(g0[gen.SLICE], objg["linear/grad0/slice"]) < 1e-3
     if kind == "e4e":
+        # The fixture cannot be mask-forced: an e4e PReLU / LeakyReLU(0.01) branch of an
+        # activation within fp32 rounding of 0 may go the other way on the device, and its effect
+        # spreads over the image through the encoder's 1²…4² maps. The fp64 oracle forced onto
+        # the device's branches separates the two effects: it equals the fixture except on the
+        # pixels those branch ties touch, and the device equals it to fp32 arithmetic everywhere.
         ref = torch.from_numpy(objg["e4e/grad0/full"]).double()
-        nrm, mx, agree = grad_stats(g0, ref)
-        assert nrm < 3e-2 and agree > 0.995, (nrm, mx, agree)  # unforced masks: see module doc
+        p64 = to64(params)
+        refs = attack_ref.Refs(*p64, x0.double(), t.double(), size)
+        gf = _forced_oracle_grad(eng, cap, p64, refs, x0, size)[1]
+        nrm, mx, agree = grad_stats(g0, gf)
+        scale = ref.abs().max()
+        stable = ref.abs() > 1e-4 * scale
+        tie = ((gf - ref).abs() / scale)  # the branch ties' effect (fp64 both sides)
+        dev = ((g0 - ref).abs() / scale)
+        agree_ref = (torch.sign(g0[stable]) == torch.sign(ref[stable])).double().mean().item()
+        print(f"e4e grad0: vs branch-forced oracle norm {nrm:.2e} max {mx:.2e}; vs the reference "
+              f"run: max-rel {dev[stable].max():.2e} (the fp64 oracle on the device's branches: "
+              f"{tie[stable].max():.2e}), {(tie <= 1e-6).double().mean().item():.3f} of pixels "
+              f"untouched by ties; stable-pixel sign agreement {agree_ref:.6f}")
+        assert nrm < 1e-4 and mx < 1e-4, (nrm, mx)
+        # the device deviates from the reference's own run by the branch ties and fp32
+        # arithmetic only: never more than the fp64 oracle on the same branches + 1e-4
+        assert (dev <= tie + 1e-4).all(), (dev - tie).max().item()
+        assert agree_ref >= 0.9998, agree_ref  # measured 0.99986
         x1 = (x0.double() - lr * ref / (ref.abs() + 1e-8)).float()
         g1 = eng.full_gradient(x1.to(cuda)).cpu().double()
-        assert _rel([float((p * g1).sum()) for p in probes], objg["e4e/grad1/proj"]) < 3e-2
+        p1 = _rel([float((p * g1).sum()) for p in probes], objg["e4e/grad1/proj"])
+        print(f"e4e grad1 projections rel {p1:.2e}")
+        # the ±1 projections sum every pixel, the tie-touched ones included (measured 1.1e-3)
+        assert proj_rel < 3e-3 and p1 < 3e-3, (proj_rel, p1)
     del eng
     free()
 

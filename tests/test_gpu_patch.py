@@ -81,9 +81,7 @@ def test_patch_attack_e4e_first_step_branch_forced(cuda):
     img = seeded(6, (N, 3, S, S)) * 0.9
     patch, mask = _square(N, S, 64, 100, 30)
     # the branches of the gradient pass's own forward (the 3rd encoder forward: prepare encodes
-    # t and x0 first; the final rec pass re-encodes the same composite, but the fp32 forward is
-    # not bit-deterministic — the SE channel sums are block atomics — so a few near-zero
-    # activations may take the other branch there)
+    # t and x0 first; the final rec pass re-encodes the same composite)
     enc = net.encoder.impl
     seen = []
     fwd = enc.forward_nhwc

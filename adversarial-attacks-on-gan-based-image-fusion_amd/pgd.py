@@ -338,14 +338,17 @@ class AttackEngine:
             ops.adam_step(x, g, m, v, lr, betas[0], betas[1], eps * self.loss_scale, it)
         return x.clone()
 
-    def run_cw(self, x0, t, steps, c=1e-4, lr=0.01, betas=(0.9, 0.999), eps=1e-8, group=None):
+    def run_cw(self, x0, t, steps, c=1e-4, lr=0.01, betas=(0.9, 0.999), eps=1e-8, group=None,
+               early_stop=True):
         """torchattacks C&W L2 (interpolation.py:98-193) composed with the GAN objective, in
         [-1,1] space: adv = tanh(w); cost = Σ‖(adv − x0)/2‖² + c·Σ L_n(adv); Adam(lr) on w;
         best-L2 tracking with success = L_n(adv) < L_n(x0); early stop every steps//10 when the
-        cost rises (one host sync there). See oracle.attack_ref.cw_attack."""
-        return self._with_rescale(lambda: self._run_cw(x0, t, steps, c, lr, betas, eps), group)
+        cost rises (one host sync there). See oracle.attack_ref.cw_attack. ``early_stop=False``
+        runs every iteration (a fixed-work timing; not the reference's semantics)."""
+        return self._with_rescale(
+            lambda: self._run_cw(x0, t, steps, c, lr, betas, eps, early_stop), group)
 
-    def _run_cw(self, x0, t, steps, c, lr, betas, eps):
+    def _run_cw(self, x0, t, steps, c, lr, betas, eps, early_stop=True):
         self.prepare(x0, t)
         ws = self.ws
         N = x0.shape[0]
@@ -377,7 +380,7 @@ class AttackEngine:
             ops.zero_(sq)
             ops.mse_sum(adv, x0, sq)
             ops.cw_select(adv, best, sq, best_l2, f, f0, 0.25)
-            if step % every == 0:
+            if early_stop and step % every == 0:
                 cost = 0.25 * float(sq.cpu().double().sum()) + c * float(f.cpu().double().sum())
                 if cost > prev:
                     break

@@ -60,7 +60,7 @@ def arith_key(dtype):
     return "fp32native" if dtype == "fp32" and _lib.F32_ARITH == "native" else dtype
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
@@ -81,22 +81,25 @@ def parse():
                     help="linf = PGD L∞ (the headline); l2_cw = C&W-L2 with the VGG perceptual "
                          "objective (BASELINE config #5 at --size 1024 --dtype fp16), c = 1e-4, "
                          "lr = 0.01, --pgd-steps iterations with the reference's early stop")
+    ap.add_argument("--cw-fixed", action="store_true",
+                    help="l2_cw: run all --pgd-steps iterations (no early stop) — a labelled "
+                         "fixed-work timing beside the reference-semantics line")
     ap.add_argument("--encoder", default="e4e", choices=["e4e", "linear"],
                     help="e4e = Encoder4Editing(50,'ir_se'), the reference's net.encoder "
                          "(code/utils/model_utils.py:24; default); linear = the SURVEY.md §7 "
                          "stand-in (rounds before the e4e encoder existed)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def encoder_weights(kind, size):
     return make_e4e_weights(size, seed=1) if kind == "e4e" else make_encoder_weights(size, seed=1)
 
 
-def cpu_baseline(size, pgd_steps, encoder):
+def cpu_baseline(size, pgd_steps, encoder, batch8=True):
     """The oracle (CPU restatement, fp32, all host cores) on a bounded sample of the same
-    workload: ONE complete PGD-`pgd_steps` attack of one 256² image (target precompute + every
-    iteration), wall-clocked end to end — BASELINE.md's procedure at B=1. B=min(N,8)=8 would
-    take 8× as long (≈ 3–4 min on the box's 16 cores) and is left out of the default run."""
+    workload, wall-clocked end to end (target precompute + every iteration; SURVEY.md §8(d): B=1
+    and B=min(N,8)): ONE complete PGD-`pgd_steps` attack of one 256² image, and — `batch8` — one
+    of a batch of 8 (≈ 1–2 min on the box's 16 cores)."""
     from oracle import attack_ref, vgg_ref
     # the box's CPU share (OMP_NUM_THREADS is set to it there); affinity shows the whole machine
     cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
@@ -106,17 +109,28 @@ def cpu_baseline(size, pgd_steps, encoder):
     ep = encoder_weights(encoder, size)
     vp = vgg_ref.load_positional(make_vgg_weights(1234))
     g = torch.Generator().manual_seed(123)
-    x0 = torch.rand(1, 3, size, size, generator=g) * 2 - 1
-    t = torch.rand(1, 3, size, size, generator=g) * 2 - 1
-    attack_ref.pgd(gp, vp, ep, x0, t, size, 8 / 255, 2 / 255, 1)  # warm-up (allocator, threads)
+    x0 = torch.rand(8, 3, size, size, generator=g) * 2 - 1
+    t = torch.rand(8, 3, size, size, generator=g) * 2 - 1
+    eps, alpha = 8 / 255, 2 / 255
+    attack_ref.pgd(gp, vp, ep, x0[:1], t[:1], size, eps, alpha, 1)  # warm-up (allocator, threads)
     t0 = time.perf_counter()
-    adv = attack_ref.pgd(gp, vp, ep, x0, t, size, 8 / 255, 2 / 255, pgd_steps)
+    adv = attack_ref.pgd(gp, vp, ep, x0[:1], t[:1], size, eps, alpha, pgd_steps)
     dt = time.perf_counter() - t0
-    assert adv.shape == x0.shape
-    return {"value": 1.0 / dt, "unit": "attacked images/s", "cores": cores, "kind": "port",
-            "sample": f"oracle fp32 CPU: one complete PGD-{pgd_steps} attack of 1 image @{size}² "
-                      f"({encoder} encoder), wall clock {dt:.1f} s incl. the target precompute; "
-                      f"torch.set_num_threads({cores})"}
+    assert adv.shape == x0[:1].shape
+    out = {"value": 1.0 / dt, "unit": "attacked images/s", "cores": cores, "kind": "port",
+           "sample": f"oracle fp32 CPU: one complete PGD-{pgd_steps} attack of 1 image @{size}² "
+                     f"({encoder} encoder), wall clock {dt:.1f} s incl. the target precompute; "
+                     f"torch.set_num_threads({cores})"}
+    if batch8:
+        t0 = time.perf_counter()
+        adv = attack_ref.pgd(gp, vp, ep, x0, t, size, eps, alpha, pgd_steps)
+        dt8 = time.perf_counter() - t0
+        assert adv.shape == x0.shape
+        out["batch8"] = {"value": 8.0 / dt8, "unit": "attacked images/s", "cores": cores,
+                         "sample": f"the same, one complete PGD-{pgd_steps} attack of a batch of "
+                                   f"8 images (B = min(N, 8), SURVEY.md §8(d)), wall clock "
+                                   f"{dt8:.1f} s"}
+    return out
 
 
 def pmc_profile(dtype, batch, size, pgd_steps, encoder="linear"):
@@ -150,52 +164,72 @@ def union_ms(iv):
     return tot + ce - cs
 
 
-def run_leg(args, dtype, steps, warmup, dev, world, rank, roofline):
-    """Build the networks at `dtype`, run `warmup` untimed and `steps` timed complete attacks
-    (barrier + synchronize on both sides, max over ranks). Returns the measurements."""
+EPS, ALPHA = 8 / 255, 2 / 255  # α = 2/255 (recorded in config)
+
+
+def build_engine(args, dtype, dev):
+    """The bench's networks at `dtype` (seeded random init)."""
     T = DT[dtype]
-    S, B = args.size, args.batch
+    S = args.size
     gp = make_generator_weights(S, seed=0)
     ep = encoder_weights(args.encoder, S)
     vs = make_vgg_weights(1234)
     enc = (E4EEncoder(ep, S, dtype=T, device=dev) if args.encoder == "e4e"
            else SyntheticEncoder(ep, S, device=dev))
-    eng = pgd.AttackEngine(enc,
-                           SynthesisNet(gp, S, dtype=T, device=dev),
-                           VGGNet(vs, dtype=T, device=dev))
+    return pgd.AttackEngine(enc, SynthesisNet(gp, S, dtype=T, device=dev),
+                            VGGNet(vs, dtype=T, device=dev))
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def run_leg(args, dtype, steps, warmup, dev, world, rank, roofline, make_engine=build_engine):
+    """Build the networks at `dtype`, run `warmup` untimed and `steps` timed complete attacks
+    (barrier + synchronize on both sides, max over ranks), each ending in the all-gather of the
+    shards when world > 1. Returns the measurements. `make_engine` (tests: a CPU stub under
+    gloo) builds the engine."""
+    S, B = args.size, args.batch
+    eng = make_engine(args, dtype, dev)
     g = torch.Generator().manual_seed(1000 + rank)
     x0 = (torch.rand(B, 3, S, S, generator=g) * 2 - 1).to(dev)
     tgt = (torch.rand(B, 3, S, S, generator=g) * 2 - 1).to(dev)
-    eps, alpha = 8 / 255, 2 / 255
+    eps, alpha = EPS, ALPHA
     n_total = B * world
     cw_runs = []
+    gathered = []
 
     def one_step():
         if args.norm == "l2_cw":
-            adv = eng.run_cw(x0, tgt, args.pgd_steps, c=1e-4, lr=0.01)
+            adv = eng.run_cw(x0, tgt, args.pgd_steps, c=1e-4, lr=0.01,
+                             early_stop=not args.cw_fixed)
             cw_runs.append(eng.cw_steps_run)
         else:
             adv = eng.run(x0, tgt, args.pgd_steps, eps, alpha)
         if world > 1:
-            gather_shards(adv, n_total)
+            gathered[:] = [gather_shards(adv, n_total)]
         return adv
 
-    torch.cuda.reset_peak_memory_stats(dev)
+    cuda = dev.type == "cuda"
+    if cuda:
+        torch.cuda.reset_peak_memory_stats(dev)
     for _ in range(warmup):
         one_step()
-    torch.cuda.synchronize()
+    _sync(dev)
     prof = []
-    if roofline:
+    if roofline and cuda:
         ops.PROFILE = prof
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
-    t_ref = torch.cuda.Event(enable_timing=True)  # origin of the conv launches' event intervals
-    t_ref.record()
+    _sync(dev)
+    if cuda:
+        t_ref = torch.cuda.Event(enable_timing=True)  # origin of the conv launches' intervals
+        t_ref.record()
     t0 = time.perf_counter()
     for _ in range(steps):
         adv = one_step()
-    torch.cuda.synchronize()
+    _sync(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -212,18 +246,23 @@ def run_leg(args, dtype, steps, warmup, dev, world, rank, roofline):
     r = {"elapsed": elapsed, "n_total": n_total, "timed_cw": timed_cw,
          "iters": sum(timed_cw) / len(timed_cw) if timed_cw else args.pgd_steps,
          "flops_img_step": pgd.algorithmic_flops_per_image_step(eng.G, eng.V, eng.E),
-         "peak_hbm_gb": torch.cuda.max_memory_allocated(dev) / 1e9, "output_ok": ok}
+         "peak_hbm_gb": torch.cuda.max_memory_allocated(dev) / 1e9 if cuda else 0.0,
+         "output_ok": ok}
+    if gathered:  # the all-gathered job output: n_total images, this rank's shard in place
+        ga = gathered[0]
+        r["gathered_ok"] = (tuple(ga.shape) == (n_total,) + tuple(adv.shape[1:])
+                            and torch.equal(ga[rank * B:(rank + 1) * B], adv))
     if prof:
-        # the e4e style heads run on side streams, so launches may overlap: a launch's own
-        # duration includes the time it shares the chip. The conv-busy time is the union of the
-        # launches' [start, end] event intervals (device clock, origin t_ref); achieved =
-        # algorithmic FLOPs ÷ conv-busy time, avg_launch_us = conv-busy time per launch.
+        # The conv-busy time is the union of the conv API calls' [start, end] event intervals
+        # (device clock, origin t_ref; one stream, so no overlap); achieved = algorithmic FLOPs ÷
+        # conv-busy time, avg_launch_us = conv-busy time per call. profiles/summarize_rocprof.py
+        # --bench-line reproduces it from the rocprofv3 trace of the same command.
         iv = [(t_ref.elapsed_time(a), t_ref.elapsed_time(b)) for a, b, _ in prof]
         r["conv_busy_ms"] = union_ms(iv)
         r["conv_sum_ms"] = sum(e - s0 for s0, e in iv)
         r["conv_flops"] = sum(f for _, _, f in prof)
         r["conv_launches"] = len(prof)
-    del eng, enc, x0, tgt
+    del eng, x0, tgt
     return r
 
 
@@ -255,6 +294,56 @@ def roofline_record(args, dtype, r):
     return rec
 
 
+def headline_record(args, r, world, dist_world):
+    """The JSON line's headline fields from run_leg's measurements (`value` = every rank's images
+    ÷ the max-over-ranks time)."""
+    S, B = args.size, args.batch
+    elapsed, n_total = r["elapsed"], r["n_total"]
+    ms = elapsed / args.steps * 1e3
+    value = n_total * args.steps / elapsed
+    flops_img_step = r["flops_img_step"]
+    timed_cw = r["timed_cw"]
+    out = {
+        "metric": METRIC if (S, args.pgd_steps, args.norm) == (256, 20, "linf") else
+                  (f"attacked images/sec, PGD-{args.pgd_steps} L∞ ε=8/255 at {S}², "
+                   if args.norm == "linf" else
+                   f"attacked images/sec, C&W-L2 (c=1e-4, lr=0.01, "
+                   + ("" if args.cw_fixed else "≤") + f"{args.pgd_steps} iterations"
+                   + (", no early stop" if args.cw_fixed else ", early stop")
+                   + f") with the VGG perceptual objective at {S}², ")
+                  + f"{world} MI355X (non-headline config)",
+        "value": value, "unit": "attacked images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": DT_NAME[args.dtype],
+        "data": f"synthetic: seeded U(-1,1) image/target pairs, seeded random-init StyleGAN2 "
+                f"({S}², cm=2), VGG16 trunk and "
+                + ("e4e Encoder4Editing(50,'ir_se')" if args.encoder == "e4e"
+                   else "linear stand-in encoder") + " (no checkpoints offline)",
+        "config": {"workload": (f"PGD-{args.pgd_steps} L∞ eps=8/255 alpha=2/255" if args.norm ==
+                                "linf" else f"C&W-L2 "
+                                + ("" if args.cw_fixed else "≤") + f"{args.pgd_steps} iterations")
+                               + f" at {S}², {B} images/GPU"
+                               + (" (BASELINE config #4 per-GPU share)" if (S, B) == (256, 128)
+                                  else "") + ", "
+                               f"RCCL all-gather of outputs when N>1",
+                   "encoder": args.encoder, "norm": args.norm, "images_per_gpu": B,
+                   "global_batch": n_total, "size": S,
+                   "pgd_steps": args.pgd_steps, "eps": EPS,
+                   **({"alpha": ALPHA} if args.norm == "linf" else {}),
+                   "parallelism": f"dp{world}",
+                   "dist_world_size": dist_world,
+                   **({"cw_iterations_run": timed_cw} if timed_cw else {}),
+                   "algorithmic_gflop_per_image_step": flops_img_step / 1e9,
+                   "effective_tflops": flops_img_step * B * r["iters"] * world
+                   / (elapsed / args.steps) / 1e12,
+                   "peak_hbm_gb_per_gpu": r["peak_hbm_gb"],
+                   "output_in_eps_ball_and_finite": r["output_ok"],
+                   **({"gathered_output_ok": r["gathered_ok"]} if "gathered_ok" in r else {}),
+                   **({"fp32_arithmetic": arith_key("fp32")} if args.dtype == "fp32" else {})},
+    }
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -269,46 +358,10 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
         dist_world = dist.get_world_size()
-    S, B = args.size, args.batch
+    S = args.size
     r = run_leg(args, args.dtype, args.steps, args.warmup, dev, world, rank,
                 not args.no_roofline)
-    elapsed, n_total = r["elapsed"], r["n_total"]
-    ms = elapsed / args.steps * 1e3
-    value = n_total * args.steps / elapsed
-    flops_img_step = r["flops_img_step"]
-    timed_cw = r["timed_cw"]
-    out = {
-        "metric": METRIC if (S, args.pgd_steps, args.norm) == (256, 20, "linf") else
-                  (f"attacked images/sec, PGD-{args.pgd_steps} L∞ ε=8/255 at {S}², "
-                   if args.norm == "linf" else
-                   f"attacked images/sec, C&W-L2 (c=1e-4, lr=0.01, ≤{args.pgd_steps} iterations, "
-                   f"early stop) with the VGG perceptual objective at {S}², ")
-                  + f"{world} MI355X (non-headline config)",
-        "value": value, "unit": "attacked images/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": DT_NAME[args.dtype],
-        "data": f"synthetic: seeded U(-1,1) image/target pairs, seeded random-init StyleGAN2 "
-                f"({S}², cm=2), VGG16 trunk and "
-                + ("e4e Encoder4Editing(50,'ir_se')" if args.encoder == "e4e"
-                   else "linear stand-in encoder") + " (no checkpoints offline)",
-        "config": {"workload": (f"PGD-{args.pgd_steps} L∞ eps=8/255 alpha=2/255" if args.norm ==
-                                "linf" else f"C&W-L2 ≤{args.pgd_steps} iterations") + f" at {S}², "
-                               f"{B} images/GPU"
-                               + (" (BASELINE config #4 per-GPU share)" if (S, B) == (256, 128)
-                                  else "") + ", "
-                               f"RCCL all-gather of outputs when N>1",
-                   "encoder": args.encoder, "norm": args.norm, "images_per_gpu": B,
-                   "global_batch": n_total, "size": S,
-                   "pgd_steps": args.pgd_steps, "parallelism": f"dp{world}",
-                   "dist_world_size": dist_world,
-                   **({"cw_iterations_run": timed_cw} if timed_cw else {}),
-                   "algorithmic_gflop_per_image_step": flops_img_step / 1e9,
-                   "effective_tflops": flops_img_step * B * r["iters"] * world
-                   / (elapsed / args.steps) / 1e12,
-                   "peak_hbm_gb_per_gpu": r["peak_hbm_gb"],
-                   "output_in_eps_ball_and_finite": r["output_ok"],
-                   **({"fp32_arithmetic": arith_key("fp32")} if args.dtype == "fp32" else {})},
-    }
+    out = headline_record(args, r, world, dist_world)
     if "conv_busy_ms" in r:
         out["roofline"] = roofline_record(args, args.dtype, r)
     if world == 1 and args.lowp != "none" and args.lowp != args.dtype:

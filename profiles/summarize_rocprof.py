@@ -17,16 +17,22 @@ import os
 import re
 from collections import defaultdict
 
-# every kernel a conv API call of the attack launches (ops.conv3x3 / upconv_fwd / upconv_dgrad):
-# the implicit-GEMM tiles, the halo tiles, the halo up-conv and the thin-channel VGG input layer
-CONV = re.compile(r"conv_(halo_|wres_|halo_x6_)?kernel|upconv_halo_kernel|conv_thin(_in|_out|32)_kernel")
-# (e4e: mia_conv2d launches conv_kernel / conv_halo_kernel; mia_conv_s2_dgrad_halo launches the
-# up-conv halo kernel in DG mode)
-# mia_upconv_fwd_halo is ONE API call that launches TWO kernels (upconv_halo_kernel for the
-# interior + a generic conv_kernel for the last row / column), so the per-call average that
-# bench.py's HIP events measure divides by launches − upconv_halo launches
-# (only the up-conv form pairs: its input-gradient mode, template flag DG = 1, is one launch)
-PAIRED = re.compile(r"upconv_halo_kernelI\w+?Lb[01]ELb0E")
+# every kernel a conv API call of the attack launches (ops.conv3x3 / conv2d / upconv_fwd /
+# upconv_dgrad / s2_dgrad_halo — the calls bench.py brackets with HIP events): the implicit-GEMM
+# tiles, the halo tiles (fp32 x6 and fp16 / bf16), the halo up-convs (fp32 upconv_x6_kernel and
+# fp16 / bf16 upconv_halo_kernel, both also in DG mode for the stride-2 input gradients), the
+# weights-resident and thin-channel kernels (the fp32 VALU VGG / e4e input layers included)
+CONV = re.compile(r"conv_(halo_|wres_|halo_x6_)?kernel|upconv_(halo|x6)_kernel|"
+                  r"conv_thin(_in|_out|32)(_f32)?_kernel")
+# the up-conv FORWARD through the halo kernel (mia_upconv_fwd_halo[_split]) is ONE API call that
+# launches TWO kernels (the halo up-conv for the interior + a generic conv_kernel for the last row
+# / column), so the per-call count that bench.py's HIP events see is launches − these launches
+# (the DG = 1 input-gradient mode is one launch: fp16 upconv_halo_kernel<T, PRO, DG>,
+# fp32 upconv_x6_kernel<DG, PRO, …>)
+# fp32 upconv_x6_kernel<DG, PRO, …>; (rocprofv3 writes demangled names; mangled forms too)
+PAIRED = re.compile(r"upconv_halo_kernel<[^<>]*(<[^<>]*>)?[^<>]*, (true|false), false>|"
+                    r"upconv_x6_kernel<false,|upconv_halo_kernelI\w+?Lb[01]ELb0E|"
+                    r"upconv_x6_kernelILb0E")
 # names of the bool template parameters of the elementwise kernels (csrc/pointwise.hip)
 KFLAGS = {"blur4_strip_kernel": ("fwd", "noise"), "torgb_bwd_kernel": ("front",),
           "upconv_halo_kernel": ("pro", "dgrad"),
@@ -107,6 +113,9 @@ def main():
     ap.add_argument("--steps", type=int, default=3, help="bench steps in the trace (warmup+timed)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--title", default="")
+    ap.add_argument("--bench-line", help="the bench JSON line of the same command: its conv FLOPs "
+                    "per step ÷ this trace's conv-busy time per step is the roofline `achieved` "
+                    "reproduced from the profile")
     a = ap.parse_args()
     rows = read_stats(a.stats)
     tot = sum(r[2] for r in rows)
@@ -132,7 +141,24 @@ def main():
                   f"streams overlap, so per-kernel times below sum to more than the busy time. "
                   f"Conv-busy time (union of the conv dispatches) {cbusy / 1e6 / a.steps:.1f} ms "
                   f"per step = {cbusy / conv_calls / 1e3:.1f} µs per conv API call (bench.py's "
-                  f"avg_launch_us is the same union over its HIP-event intervals).", ""]
+                  f"avg_launch_us is the union of its HIP-event intervals around the same calls, "
+                  f"which also hold each call's launch gap and reduction finish).", ""]
+        if a.bench_line:
+            bl = json.loads(open(a.bench_line).read().strip().splitlines()[-1])
+            rf = bl["roofline"]
+            flops_step = rf["algorithmic_gflop_per_launch"] * 1e9 * rf["launches"] / bl["steps"]
+            calls_step = rf["launches"] / bl["steps"]
+            ach = flops_step / (cbusy / a.steps * 1e-9) / 1e12
+            out["conv_kernel"]["bench_calls_per_step"] = calls_step
+            out["conv_kernel"]["trace_calls_per_step"] = conv_calls / a.steps
+            out["conv_kernel"]["achieved_tflops_from_trace"] = ach
+            out["conv_kernel"]["achieved_tflops_bench"] = rf["achieved"]
+            lines += [f"Roofline reproduced from this trace: the bench line's conv work "
+                      f"{flops_step / 1e12:.1f} TFLOP per step ({calls_step:.0f} conv API calls; "
+                      f"this trace: {conv_calls / a.steps:.0f} per step) ÷ the trace's conv-busy "
+                      f"time = {ach:.1f} TFLOP/s; the bench line's live HIP-event figure "
+                      f"{rf['achieved']:.1f} TFLOP/s ({100 * (rf['achieved'] / ach - 1):+.1f} %).",
+                      ""]
     lines += [
              "| kernel | calls/step | ms/step | avg µs | share |", "|---|---|---|---|---|"]
     for n, c, t in sorted(rows, key=lambda r: -r[2]):

@@ -1,0 +1,80 @@
+"""bench.py's N>1 leg on CPU (gloo, world 2, a stub attack engine): the timed region's
+barrier + max-over-ranks clock, the per-step all-gather of the shards (gather_shards, the RCCL
+all_gather_into_tensor on the GPU node) and the JSON record's whole-job fields — the path the
+driver's 8-GPU run takes (BASELINE config #4), which no GPU run of this builder exercises."""
+import os
+import socket
+import sys
+import time
+import types
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _StubEngine:
+    """CPU stand-in for pgd.AttackEngine: an elementwise 'attack' with a rank-dependent delay
+    (so the max over ranks is visible) and the flop attributes bench.py reports."""
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.G = types.SimpleNamespace(flops_fwd_per_image=10.0)
+        self.V = types.SimpleNamespace(flops_fwd_per_image=1.0)
+        self.E = types.SimpleNamespace(flops_fwd_per_image=3.0)
+
+    def run(self, x0, t, steps, eps, alpha):
+        time.sleep(0.05 * (1 + self.rank))
+        return torch.clamp(x0 + 2 * eps * torch.sign(t - x0), -1.0, 1.0)
+
+
+def _worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    import bench
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        args = bench.parse(["--gpus", str(world), "--steps", "2", "--warmup", "1", "--batch", "3",
+                            "--size", "16", "--no-roofline", "--no-cpu-baseline"])
+        r = bench.run_leg(args, "fp32", args.steps, args.warmup, torch.device("cpu"), world, rank,
+                          False, make_engine=lambda a, d, dev: _StubEngine(rank))
+        out = bench.headline_record(args, r, world, dist.get_world_size())
+        out_q.put((rank, out, r["elapsed"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_multi_rank_leg_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=180) for _ in procs), key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    (_, out0, el0), (_, out1, el1) = res
+    assert el0 == el1  # max over ranks on every rank
+    assert el0 >= 2 * 0.1  # the slow rank's 2 timed steps (0.1 s each) bound the job
+    for out in (out0, out1):
+        c = out["config"]
+        assert out["n_gpus"] == 2 and c["dist_world_size"] == 2 and c["parallelism"] == "dp2"
+        assert c["global_batch"] == 6 and c["images_per_gpu"] == 3
+        assert c["gathered_output_ok"] is True and c["output_in_eps_ball_and_finite"] is True
+        assert out["value"] == pytest.approx(6 * 2 / el0)
+        assert out["scaling"] == "weak" and out["steps"] == 2 and out["warmup"] == 1
+        assert c["algorithmic_gflop_per_image_step"] == pytest.approx((2 * 10 + 4 * 1 + 6) / 1e9)

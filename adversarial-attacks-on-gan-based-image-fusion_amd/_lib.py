@@ -16,6 +16,10 @@ if F32_ARITH not in ("bf16x6", "native"):
     raise ValueError(f"MIA_F32_ARITH must be bf16x6 or native, not {F32_ARITH!r}")
 LIB_PATH = os.path.join(HERE, "libmiattack.so" if F32_ARITH == "bf16x6"
                         else "libmiattack_f32native.so")
+# Tuning A/B only (tools/gpu/*_ab.sh): MIA_LIB_VARIANT=<name> loads libmiattack_<name>.so, a build
+# of the same sources with extra compile-time switches (csrc/Makefile `variant`).
+if os.environ.get("MIA_LIB_VARIANT"):
+    LIB_PATH = os.path.join(HERE, f"libmiattack_{os.environ['MIA_LIB_VARIANT']}.so")
 
 c_int, c_float, c_int64, c_void_p = ctypes.c_int, ctypes.c_float, ctypes.c_int64, ctypes.c_void_p
 P = c_void_p

@@ -24,6 +24,12 @@
 #include "conv_common.h"
 #include "halo_epilogue.h"
 
+// PRO launches: 1 = the landed halo modulated once in LDS (default); 0 = every fragment read
+// modulated (round-2 form, tuning A/B: `make variant VARIANT_FLAGS=-DMIA_HALO_PREMOD=0`).
+#ifndef MIA_HALO_PREMOD
+#define MIA_HALO_PREMOD 1
+#endif
+
 namespace mia {
 
 // Tile: a PH × 16 output patch (PH = 16: 8 waves, 1 block per CU; PH = 8: 4 waves, 2 blocks per
@@ -163,8 +169,22 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
                                      0, 0);
   };
 
-  // ---- prologue: style row, halo of channel block 0, weights of steps 0 … STAGES−2 -----------
+  // PRO: modulate the landed halo of channel block cb (buffer buf) in place ONCE — act(x)·s
+  // rounded to T exactly as modulate<T> would on every fragment read (9 taps × 2 column waves).
+  // Zero padding stays zero.
   const bool lrelu_in = p.act_in == MIA_ACT_LRELU_S2;
+  auto premod = [&](int cb, int buf) {
+    char* hb = hbuf + buf * HBUF;
+    for (int c = tid; c < HROWS * 8; c += NT) {
+      const int hr = c >> 3, pc = c & 7, lc = pc ^ fsw(hr);
+      VT v = *(const VT*)(hb + hr * ROWB + pc * 16);
+      const VT sv = *(const VT*)(stab + cb * BK + lc * VEC);
+      modulate<T>(v, sv, lrelu_in);
+      *(VT*)(hb + hr * ROWB + pc * 16) = v;
+    }
+  };
+
+  // ---- prologue: style row, halo of channel block 0, weights of steps 0 … STAGES−2 -----------
   if constexpr (PRO) {
     const float mul = lrelu_in ? SQRT2 : 1.f;
     for (int i = tid; i < Cin; i += NT) {
@@ -183,6 +203,10 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
     wait_vmcnt(0);
   }
   __syncthreads();
+  if constexpr (PRO && MIA_HALO_PREMOD) {
+    premod(0, 0);
+    __syncthreads();
+  }
   HT_STAMP(t_pro);
 #ifdef MIA_HALO_TIMING
   unsigned long long c_vm = 0, c_mma = 0, c_bar = 0;
@@ -195,6 +219,86 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int frow = lane & 15, fq = lane >> 4;
+  if constexpr (EPI >= 0) {
+    // The taps unrolled (the specialised-epilogue launches): every fragment address is a
+    // lane-constant LDS offset — for the A fragments one per (row shift q = i + dy, column shift
+    // dx), for the B fragments one per column fragment — computed once here instead of ≈ 6 VALU
+    // per fragment per step; the second MFMA half reads chunk ^ 4 (byte offset ^ 64). Same reads
+    // and MFMAs in the same order as the rolled loop below (bit-identical outputs).
+    int oh[FM + 2][3], ob[FN];
+#pragma unroll
+    for (int q = 0; q < FM + 2; ++q)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int hr = (wm * FM + q) * HSIDE + frow + c;
+        int v = hr * ROWB + ((fq ^ fsw(hr)) << 4);
+        asm volatile("" : "+v"(v));  // kept in registers, not recomputed per step
+        oh[q][c] = v;
+      }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int row = wn * FN * 16 + 16 * j + frow;
+      int v = row * ROWB + ((fq ^ fsw(row)) << 4);
+      asm volatile("" : "+v"(v));
+      ob[j] = v;
+    }
+    int st = 0;
+    for (int cb = 0; cb < ncb; ++cb) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int s = cb * 9 + t;
+        int hoff = (cb & (TL::NHBUF - 1)) * HBUF, soff = st * BSTAGE, x1 = 64;
+        asm volatile("" : "+s"(hoff), "+s"(soff), "+s"(x1));
+        const char* ha = hbuf + hoff;
+        const char* sb = bring + soff;
+        const int dy = t / 3, dx = t % 3;
+        if (bwave && s + STAGES - 1 < nk) issue_b(s + STAGES - 1, st == 0 ? STAGES - 1 : st - 1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          VT af[FM], bf[FN];
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+            af[i] = *(const VT*)(ha + (h ? oh[i + dy][dx] ^ x1 : oh[i + dy][dx]));
+#pragma unroll
+          for (int j = 0; j < FN; ++j) bf[j] = *(const VT*)(sb + (h ? ob[j] ^ x1 : ob[j]));
+          if constexpr (PRO && !MIA_HALO_PREMOD) {
+            const VT sv = *(const VT*)(stab + cb * BK + (h * 4 + fq) * VEC);
+#pragma unroll
+            for (int i = 0; i < FM; ++i) modulate<T>(af[i], sv, lrelu_in);
+          }
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+              acc[i][j] = mfma_chunk<T>(bf[j], af[i], acc[i][j]);  // D[channel][pixel]
+          __builtin_amdgcn_s_setprio(0);
+          if (h == 0 && !bwave && TL::NHBUF > 1 && cb + 1 < ncb && t * HPS < H_INS) {
+            // H-waves: the next block's halo between the two MFMA halves, HPS pieces per tap
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < HPS; ++q) {
+              const int j = t * HPS + q;
+              if (j < H_INS && j < my_pieces) issue_h(cb + 1, j, (cb + 1) & (TL::NHBUF - 1));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        if (bwave) wait_vmcnt(B_INS * max(0, min(STAGES - 2, nk - 2 - s)));
+        else if (t == 8) wait_vmcnt(0);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of stage st are done
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (PRO && MIA_HALO_PREMOD && TL::NHBUF > 1) {
+          if (t == 8 && cb + 1 < ncb) {  // the next block's halo landed: modulate it once
+            premod(cb + 1, (cb + 1) & 1);
+            __syncthreads();
+          }
+        }
+        st = st + 1 == STAGES ? 0 : st + 1;
+      }
+    }
+  } else {
   int st = 0, cb = 0, t = 0;
   for (int s = 0; s < nk; ++s) {
     HT_STEP_STAMP(ts1);
@@ -220,7 +324,7 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
         const int row = wn * FN * 16 + 16 * j + frow;
         bf[j] = *(const VT*)(sb + row * ROWB + ((ch ^ fsw(row)) << 4));
       }
-      if constexpr (PRO) {
+      if constexpr (PRO && !MIA_HALO_PREMOD) {
         const VT sv = *(const VT*)(stab + cb * BK + ch * VEC);
 #pragma unroll
         for (int i = 0; i < FM; ++i) modulate<T>(af[i], sv, lrelu_in);
@@ -268,9 +372,16 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
     c_vm += ts3 - ts2;
     c_bar += ts4 - ts3;
 #endif
+    if constexpr (PRO && MIA_HALO_PREMOD && TL::NHBUF > 1) {
+      if (t == 8 && cb + 1 < ncb) {  // the next block's halo landed: modulate it once
+        premod(cb + 1, (cb + 1) & 1);
+        __syncthreads();
+      }
+    }
     st = st + 1 == STAGES ? 0 : st + 1;
     if (++t == 9) { t = 0; ++cb; }
   }
+  }  // rolled loop
   HT_STAMP(t_loop);
   if constexpr (EPI >= 0) {
     // (the LDS is idle after the main loop's last barrier: the pre-reduction reuses it)

@@ -31,7 +31,9 @@
 // Measured neutral or slower for the loop (not kept): both halves' fragment reads up front, a
 // fragment-level read/MFMA pipeline with (lo, hi) windows loaded in place (no register copies),
 // every wave streaming a share of the weights and of the halo, a 4-stage weight ring (64-channel
-// tile), and a persistent form.
+// tile), a persistent form, and (round 3) per-stage LDS counters instead of the per-step block
+// barrier (B-waves refill a stage once all 8 waves have read it, readers start once its 4 pieces
+// landed, barriers only at channel-block ends): step 7564 → 7568 ms, ±3 % per layer.
 #include "conv_common.h"
 #include "halo_epilogue.h"
 

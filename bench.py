@@ -95,6 +95,21 @@ def encoder_weights(kind, size):
     return make_e4e_weights(size, seed=1) if kind == "e4e" else make_encoder_weights(size, seed=1)
 
 
+def log(msg):
+    """Liveness / progress line on stderr (stdout carries only the JSON line)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def _progress(tag):
+    t0 = time.perf_counter()
+    n = [0]
+
+    def cb(_):
+        n[0] += 1
+        log(f"{tag}: iteration {n[0]} done, {time.perf_counter() - t0:.1f} s")
+    return cb
+
+
 def cpu_baseline(size, pgd_steps, encoder, batch8=True):
     """The oracle (CPU restatement, fp32, all host cores) on a bounded sample of the same
     workload, wall-clocked end to end (target precompute + every iteration; SURVEY.md §8(d): B=1
@@ -114,7 +129,8 @@ def cpu_baseline(size, pgd_steps, encoder, batch8=True):
     eps, alpha = 8 / 255, 2 / 255
     attack_ref.pgd(gp, vp, ep, x0[:1], t[:1], size, eps, alpha, 1)  # warm-up (allocator, threads)
     t0 = time.perf_counter()
-    adv = attack_ref.pgd(gp, vp, ep, x0[:1], t[:1], size, eps, alpha, pgd_steps)
+    adv = attack_ref.pgd(gp, vp, ep, x0[:1], t[:1], size, eps, alpha, pgd_steps,
+                         progress=_progress("cpu baseline B=1"))
     dt = time.perf_counter() - t0
     assert adv.shape == x0[:1].shape
     out = {"value": 1.0 / dt, "unit": "attacked images/s", "cores": cores, "kind": "port",
@@ -123,7 +139,8 @@ def cpu_baseline(size, pgd_steps, encoder, batch8=True):
                      f"torch.set_num_threads({cores})"}
     if batch8:
         t0 = time.perf_counter()
-        adv = attack_ref.pgd(gp, vp, ep, x0, t, size, eps, alpha, pgd_steps)
+        adv = attack_ref.pgd(gp, vp, ep, x0, t, size, eps, alpha, pgd_steps,
+                             progress=_progress("cpu baseline B=8"))
         dt8 = time.perf_counter() - t0
         assert adv.shape == x0.shape
         out["batch8"] = {"value": 8.0 / dt8, "unit": "attacked images/s", "cores": cores,
@@ -217,6 +234,7 @@ def run_leg(args, dtype, steps, warmup, dev, world, rank, roofline, make_engine=
     for _ in range(warmup):
         one_step()
     _sync(dev)
+    log(f"{dtype}: {warmup} warm-up step(s) done")
     prof = []
     if roofline and cuda:
         ops.PROFILE = prof
@@ -233,6 +251,7 @@ def run_leg(args, dtype, steps, warmup, dev, world, rank, roofline, make_engine=
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    log(f"{dtype}: {steps} timed step(s), {elapsed:.2f} s")
     ops.PROFILE = None
     if world > 1:
         tt = torch.tensor([elapsed], device=dev)

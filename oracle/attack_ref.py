@@ -91,10 +91,11 @@ def project_step(adv, x0, g, e, a, lo=-1.0, hi=1.0):
 
 
 def pgd(gp, vp, ep, x0, t, size, eps, alpha, steps, random_start=False, start_noise=None,
-        dtype=torch.float32, return_grads=False):
+        dtype=torch.float32, return_grads=False, progress=None):
     """PGD-`steps` in [-1,1] space (FGSM = steps 1, alpha = eps, no random start).
 
-    ``start_noise``: U(-1,1) draws, scaled by e here (host-seeded so the GPU path shares it)."""
+    ``start_noise``: U(-1,1) draws, scaled by e here (host-seeded so the GPU path shares it).
+    ``progress``: called with the iteration index after each step (bench.py's liveness lines)."""
     e, a = 2.0 * eps, 2.0 * alpha
     x0 = x0.to(dtype)
     t = t.to(dtype)
@@ -108,6 +109,8 @@ def pgd(gp, vp, ep, x0, t, size, eps, alpha, steps, random_start=False, start_no
         if return_grads:
             grads.append(g)
         adv = project_step(adv, x0, g, e, a)
+        if progress is not None:
+            progress(len(grads) if return_grads else None)
     return (adv, grads) if return_grads else adv
 
 

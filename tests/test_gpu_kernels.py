@@ -999,3 +999,84 @@ def test_x6_halo_variants_bitwise(cuda, monkeypatch, C, H, W, mode):
     y_gen = run()
     assert torch.equal(y_def, y_gen)
     assert rel_err(nchw(y_def), ref) < 2 * TOL[torch.float32]
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("C,H,W", [(128, 32, 16), (256, 16, 32)])
+@pytest.mark.parametrize("mode", ["plain", "bias_relu", "mask", "tap", "mod", "sdot_bab"])
+def test_halo_lowp_unrolled_bitwise(cuda, monkeypatch, dtype, C, H, W, mode):
+    """fp16 / bf16 halo kernel (conv_halo.hip): the specialised-epilogue launches run the taps
+    unrolled over lane-constant fragment offsets; the runtime-feature epilogue (MIA_HALO_EPI=2)
+    runs the rolled loop. Same reads, same MFMAs in the same order: outputs (and sdot / q sums)
+    bit-identical; both within the dtype's tolerance of fp64. 'mod' = the StyledConv forward
+    (modulated input, halo modulated once in LDS; demod, noise, bias, LeakyReLU·√2)."""
+    g = torch.Generator().manual_seed(C + H + W + len(mode) + (dtype == torch.bfloat16))
+    N = 2
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
+    wq = w.to(dtype).double()
+    y0 = torch.randn(N, C, H, W, generator=g)
+    b = torch.randn(C, generator=g) * 0.1
+    m = torch.randn(N, C, H, W, generator=g)
+    a = torch.randn(N, C, H, W, generator=g).relu()
+    t = torch.randn(N, C, H, W, generator=g)
+    s = torch.rand(N, C, generator=g) + 0.5
+    d = torch.rand(N, C, generator=g) + 0.5
+    noise = torch.randn(H * W, generator=g)
+    xq = x.to(dtype).double()
+    f32 = torch.float32
+
+    def run():
+        y = nhwc(y0, dtype).to(cuda)
+        xc = nhwc(x, dtype).to(cuda)
+        sd = torch.zeros(N * C, device=cuda) if mode == "sdot_bab" else None
+        q = torch.zeros(N * C, device=cuda) if mode == "sdot_bab" else None
+        kw = {}
+        if mode == "bias_relu":
+            kw = dict(bias=b.to(cuda), act_out=ops.ACT_RELU)
+        elif mode == "mask":
+            kw = dict(mask_a=nhwc(m, dtype).to(cuda))
+        elif mode == "tap":
+            kw = dict(tap_a=nhwc(a, dtype).to(cuda), tap_t=nhwc(t, dtype).to(cuda), tap_coef=0.37)
+        elif mode == "mod":
+            kw = dict(in_scale=s.to(cuda), act_in=ops.ACT_LRELU_S2, out_scale=d.to(cuda),
+                      noise=noise.to(cuda), noise_w=0.3, bias=b.to(cuda),
+                      act_out=ops.ACT_LRELU_S2)
+        elif mode == "sdot_bab":
+            kw = dict(out_scale=s.to(cuda), aux_x=nhwc(a, dtype).to(cuda), sdot=sd,
+                      bab=dict(demod=d.to(cuda), noise=noise.to(cuda), noise_w=0.3,
+                               bias=b.to(cuda), q=q))
+        ops.conv3x3(xc, layouts.fwd_matrix(w, dtype).to(cuda), y, cout=C, **kw)
+        torch.cuda.synchronize()
+        return y.clone(), sd, q
+
+    y_def, sd_def, q_def = run()
+    monkeypatch.setenv("MIA_HALO_EPI", "2")
+    y_rol, sd_rol, q_rol = run()
+    if mode != "sdot_bab":
+        assert torch.equal(y_def, y_rol), (mode, (y_def.float() - y_rol.float()).abs().max().item())
+    else:
+        # the main loop is the same code for every EPI ≥ 0 (bit-identity shown by the other
+        # modes); the runtime-feature epilogue's backward front rounds its fp32 chain differently
+        # from the specialised one in rare elements: ≤ 1 ulp of T on the outputs
+        ulp = torch.finfo(dtype).eps * y_rol.float().abs().clamp_min(1e-3)
+        assert ((y_def.float() - y_rol.float()).abs() <= ulp).all()
+        for u, v in ((sd_def, sd_rol), (q_def, q_rol)):
+            assert ((u - v).abs().max() / v.abs().max()).item() < 1e-5
+    # against fp64 on the same rounded operands
+    if mode == "mod":
+        xa = torch.where(xq > 0, xq, 0.2 * xq) * math.sqrt(2)
+        xm = (xa * s.double().view(N, C, 1, 1)).to(dtype).double()
+        pre = F.conv2d(xm, wq, padding=1) * d.double().view(N, C, 1, 1) \
+            + 0.3 * noise.double().view(1, 1, H, W) + b.double().view(1, C, 1, 1)
+        ref = torch.where(pre > 0, pre, 0.2 * pre) * math.sqrt(2)
+    else:
+        conv = F.conv2d(xq, wq, padding=1)
+        ref = {"plain": conv, "bias_relu": F.relu(conv + b.double().view(1, C, 1, 1)),
+               "mask": conv * (m.to(dtype).double() > 0),
+               "tap": conv + 0.37 * (a.to(dtype).double() - t.to(dtype).double()),
+               "sdot_bab": None}[mode]
+    if ref is not None:
+        got = y_def.permute(0, 3, 1, 2).double().cpu()
+        tol = 2e-2 if dtype == torch.float16 else 1e-1
+        assert ((got - ref).abs().max() / ref.abs().max()).item() < tol, mode

@@ -12,6 +12,7 @@ on gfx950 (it tallies 128-B requests at 64 B).
 """
 import argparse
 import csv
+import gzip
 import json
 import os
 import re
@@ -88,7 +89,8 @@ def busy_union_ns(trace_path, pattern=None):
     run on side streams, so kernel durations overlap and their sum exceeds the busy time).
     pattern: only the kernels whose name it matches (the conv kernels: conv-busy time)."""
     iv = []
-    with open(trace_path) as f:
+    opener = gzip.open if trace_path.endswith(".gz") else open
+    with opener(trace_path, "rt") as f:
         for r in csv.DictReader(f):
             if pattern is None or pattern.search(r["Kernel_Name"]):
                 iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
@@ -130,6 +132,8 @@ def main():
     lines = [f"# {a.title}", "", f"rocprofv3 --kernel-trace --stats; {a.steps} bench steps in the "
              f"trace; kernel time per step {tot / 1e6 / a.steps:.1f} ms", ""]
     trace = a.stats.replace("kernel_stats.csv", "kernel_trace.csv")
+    if trace != a.stats and not os.path.exists(trace) and os.path.exists(trace + ".gz"):
+        trace += ".gz"  # the committed traces are gzipped
     if trace != a.stats and os.path.exists(trace):
         busy = busy_union_ns(trace)
         cbusy = busy_union_ns(trace, CONV)
@@ -137,8 +141,8 @@ def main():
         out["conv_kernel"]["busy_ms"] = cbusy / 1e6
         out["conv_kernel"]["avg_busy_us_per_call"] = cbusy / conv_calls / 1e3
         lines += [f"GPU busy (union of dispatch intervals, incl. the one-off setup before the first "
-                  f"step) {busy / 1e6 / a.steps:.1f} ms per step: kernels of the style-head side "
-                  f"streams overlap, so per-kernel times below sum to more than the busy time. "
+                  f"step) {busy / 1e6 / a.steps:.1f} ms per step (one stream: the kernels do not "
+                  f"overlap). "
                   f"Conv-busy time (union of the conv dispatches) {cbusy / 1e6 / a.steps:.1f} ms "
                   f"per step = {cbusy / conv_calls / 1e3:.1f} µs per conv API call (bench.py's "
                   f"avg_launch_us is the union of its HIP-event intervals around the same calls, "

@@ -80,6 +80,8 @@ SIGNATURES = {
     "mia_reserve_reduction_scratch": (c_int, [c_int64, P]),
     "mia_reduction_scratch_bytes": (c_int64, [P]),
     "mia_release_reduction_scratch": (c_int, [P]),
+    "mia_set_tuning": (c_int, [ctypes.c_char_p, c_int]),
+    "mia_get_tuning": (c_int, [ctypes.c_char_p, ctypes.POINTER(c_int)]),
     "mia_conv_kpad": (c_int, [c_int, c_int]),
     "mia_conv3x3": (c_int, [ctypes.POINTER(ConvArgs), c_int, P]),
     "mia_modconv_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P,
@@ -204,3 +206,16 @@ def call(name, *args):
     if rc != 0:
         raise MiaError(f"{name} failed ({rc}): {lib.mia_last_error_string().decode()}")
     return rc
+
+
+def set_tuning(name, value):
+    """Set a kernel-variant switch (include/miattack.h); returns the previous value."""
+    old = get_tuning(name)
+    call("mia_set_tuning", name.encode(), int(value))
+    return old
+
+
+def get_tuning(name):
+    v = c_int(0)
+    call("mia_get_tuning", name.encode(), ctypes.byref(v))
+    return v.value

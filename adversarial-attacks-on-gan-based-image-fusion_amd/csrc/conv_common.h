@@ -26,8 +26,6 @@ constexpr int MIA_MAX_GROUPS = 16;
 struct ConvK {
   mia_conv_args a;  // x, y, N, H/W = INPUT dims, Cin, Cout and the epilogue fields
   int stride, HT, WT, ystride, cout_mod, log2cin, n_first_max, ng, nblk, nbn;
-  int stagger_blocks;            // halo kernel: blocks of the first dispatch wave …
-  unsigned stagger_cycles;       // … of which every other one starts this many clocks late
   int prered;                    // register epilogues: pre-reduce the sums across the M waves in
                                  // LDS before the atomics; on for the channel sum (SE pool) only:
                                  // measured, the extra barrier costs more than it saves for the
@@ -85,11 +83,8 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
 // tap-shifted reads do not respect).
 __device__ __forceinline__ int fsw(int row) { return ((row >> 1) & 3) << 1; }
 
-// MIA_EPI_PRERED=0 turns the register epilogues' LDS pre-reduction off (A/B switch, per launch)
-inline int prered_enabled() {
-  const char* e = getenv("MIA_EPI_PRERED");
-  return e ? atoi(e) != 0 : 1;
-}
+// the register epilogues' LDS pre-reduction of the channel sums (T_EPI_PRERED, default on)
+inline int prered_enabled() { return tune(T_EPI_PRERED) != 0; }
 
 __device__ __forceinline__ int div_kw(int t, int kw) {
   return kw == 3 ? (t * 11) >> 5 : (kw == 2 ? t >> 1 : t);  // exact for t < 9

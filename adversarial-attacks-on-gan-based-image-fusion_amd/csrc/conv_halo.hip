@@ -83,14 +83,6 @@ __device__ unsigned long long g_halo_dbg[HT_SLOTS][8];
 // features (halo_epilogue), ≥ 0 = register epilogue specialised for feature mask EPI.
 template <typename T, typename TL, bool PRO, int EPI>
 __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(const ConvK k) {
-  // Blocks of equal work launched together stay in lockstep: every block loads its halo at the
-  // same time and stores its tile at the same time, and HBM idles during the MFMA phase. Half of
-  // the first dispatch wave starts late, so the memory phases of the two halves interleave with
-  // each other's main loops for the rest of the launch (later blocks inherit their slot's phase).
-  if (k.stagger_cycles && (int)blockIdx.x < k.stagger_blocks && ((blockIdx.x >> 3) & 1)) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    while (__builtin_amdgcn_s_memtime() - t0 < k.stagger_cycles) __builtin_amdgcn_s_sleep(16);
-  }
   HT_STAMP(t_start);
   typedef typename Vec<T>::type VT;
   constexpr int VEC = Vec<T>::N;
@@ -434,18 +426,6 @@ static int launch_halo_tile_(ConvK& k, hipStream_t st) {
       return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     attr_set = true;
   }
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      ncu = 256;
-  }
-  const int per_cu = TL::WAVES_PER_SIMD == 2 ? 2 : 1;
-  k.stagger_blocks = per_cu * ncu;
-  const char* es = getenv("MIA_HALO_STAGGER");  // clocks; tuning / A-B switch
-  k.stagger_cycles = es ? (unsigned)atoi(es) : 0u;
-  if (k.nblk < 4 * k.stagger_blocks) k.stagger_cycles = 0;  // short launches: not worth a tail
   k.prered = prered_enabled() && EPI >= 0 && (EPI & epi::CSUM);
   const int H = k.a.H, W = k.a.W;
   const int nslots = EPI >= 0    ? halo_red_slots(H, W, TL::FM, TL::WM, k.prered)
@@ -461,10 +441,9 @@ static int launch_halo_tile_(ConvK& k, hipStream_t st) {
 
 template <typename T, typename TL, bool PRO, bool SPEC>
 static int launch_halo_tile(ConvK& k, hipStream_t st) {
-  // tuning / A-B switch, read per launch: MIA_HALO_EPI=0 LDS-staged shared epilogue, 2 register
-  // epilogue with runtime features (no specialisation); default 1 = specialised where one exists
-  const char* e = getenv("MIA_HALO_EPI");
-  const int sel = e ? atoi(e) : 1;
+  // T_HALO_EPI (tests / tuning): 0 LDS-staged shared epilogue, 2 register epilogue with runtime
+  // features and the rolled tap loop; default 1 = specialised where one exists
+  const int sel = tune(T_HALO_EPI);
   if (sel == 0) return launch_halo_tile_<T, TL, PRO, -2>(k, st);
   if constexpr (SPEC && sizeof(T) == 2) {  // fp32 (reference dtype) keeps the generic path
     if (sel == 1) {
@@ -501,17 +480,14 @@ static int launch_halo_tile(ConvK& k, hipStream_t st) {
 // MFMAs; at Cout ≤ 32 — the VGG input gradient, 8 channels — the generic tile computes 64 columns
 // and gathers every input row 9 times, the 32-column halo tile is memory-bound on one halo pass).
 bool conv_halo_eligible(const ConvK& k, int dtype) {
-  const char* e = getenv("MIA_CONV_HALO");  // tuning / A-B switch: 0 disables the halo path
-  if (e && atoi(e) == 0) return false;
-  const char* e64 = getenv("MIA_HALO_N64");  // tuning: 1 = halo path for Cout = 64 too
-  const bool n64 = e64 && atoi(e64) == 1;
+  if (tune(T_CONV_HALO) == 0) return false;
   const mia_conv_args& a = k.a;
   const ConvGroup& G = k.g[0];
   const int bk = dtype == MIA_F32 ? 32 : 64;
   return k.ng == 1 && k.stride == 1 && G.kh == 3 && G.kw == 3 && G.pad_y == 1 && G.pad_x == 1 &&
          G.ho == a.H && G.wo == a.W && G.ay == 1 && G.ax == 1 && G.by == 0 && G.bx == 0 &&
          !a.shuffle_out && a.H % 16 == 0 && a.W % 16 == 0 && a.Cin % bk == 0 &&
-         (a.Cout > 64 || a.Cout <= 32 || (n64 && a.Cout == 64)) &&
+         (a.Cout > 64 || a.Cout <= 32) &&
          k.HT == a.H && k.WT == a.W;
 }
 
@@ -521,6 +497,8 @@ int launch_conv_halo(ConvK& k, int dtype, hipStream_t st) {
   // 16×16 patches on 8 waves (1 block per CU, 4 stages) and 25–40 % faster than 16×16 patches on
   // 4 waves (FM = 8, one wave per SIMD) on every attack shape — two waves per SIMD keep the
   // matrix pipe fed through each other's LDS reads, DMA issue and barriers.
+  // (round 3, fp16 / bf16 modulated forward at 256² / 128² / 64², bit-identical outputs:
+  // 16×16 patches on 8 waves with a 3-stage ring −1.9 … +2.1 %, on 4 waves −9 … −18 %)
   typedef HaloTile<128, 8, 2> Small;
   typedef HaloTile<64, 8, 3> Small64;
   // Cout ≤ 32 (VGG input gradient): little MFMA work per K-step, so the weights of all nine taps

@@ -453,22 +453,13 @@ static int launch_x6_e(ConvK& k, hipStream_t st) {
 
 template <int BN_, bool PRO, int EPI>
 static int launch_x6_(ConvK& k, hipStream_t st) {
-  // the next block's halo DMA at the step start (default; measured +2-3 % on the stride-1 layers,
-  // neutral on the up-conv) or between the two MFMA halves (MIA_X6_EARLY=0, A/B)
-  // + s_setprio(1) around each MFMA block (default; +1-4 %; MIA_X6_PRIO=0 disables): the wave in
-  // its MFMA phase keeps issue priority over the co-resident wave's LDS reads
-  const char* e = getenv("MIA_X6_EARLY");
-  const char* pe = getenv("MIA_X6_PRIO");
-  const bool prio = !pe || atoi(pe) != 0;
+  // the next block's halo DMA at the step start (measured +2-3 % on the stride-1 layers over
+  // issuing it between the two MFMA halves) + s_setprio(1) around each MFMA block (+1-4 %): the
+  // wave in its MFMA phase keeps issue priority over the co-resident wave's LDS reads
   if constexpr (EPI >= 0) {  // + the taps unrolled with lane-constant fragment offsets
-    const char* u = getenv("MIA_X6_UNR");  // (A/B: MIA_X6_UNR=0)
-    if ((!u || atoi(u) != 0) && (!e || atoi(e) != 0) && prio)
-      return launch_x6_e<BN_, PRO, EPI, true, true, true>(k, st);
+    if (tune(T_X6_UNR) != 0) return launch_x6_e<BN_, PRO, EPI, true, true, true>(k, st);
   }
-  if (!e || atoi(e) != 0)
-    return prio ? launch_x6_e<BN_, PRO, EPI, true, true>(k, st)
-                : launch_x6_e<BN_, PRO, EPI, true, false>(k, st);
-  return launch_x6_e<BN_, PRO, EPI, false>(k, st);
+  return launch_x6_e<BN_, PRO, EPI, true, true>(k, st);  // the rolled loop (T_X6_UNR = 0)
 }
 
 // The register epilogue specialised for the feature masks of the attack's fp32 launches (every aux
@@ -514,10 +505,7 @@ static int launch_x6_spec(ConvK& k, hipStream_t st) {
 }
 
 // MIA_X6_64AUX=1: the 64-column tile also for launches with the tap pair (A/B)
-static bool x6_64_aux() {
-  const char* e = getenv("MIA_X6_64AUX");
-  return e && atoi(e) != 0;
-}
+static bool x6_64_aux() { return tune(T_X6_64AUX) != 0; }
 
 // Eligible: fp32 with pre-split weights (mia_conv_args.w_split / mia_conv_group.w_split), one
 // group, stride 1, 3×3 pad 1, identity placement, 16-divisible maps, Cin % 32 == 0, Cout ≥ 64.
@@ -527,8 +515,7 @@ bool conv_halo_x6_eligible(const ConvK& k, int dtype) {
   (void)dtype;
   return false;  // the native-fp32 A/B build keeps every fp32 conv on v_mfma_f32_16x16x4_f32
 #endif
-  const char* e = getenv("MIA_CONV_X6");  // A/B switch: 0 = the on-the-fly split kernels
-  if (e && atoi(e) == 0) return false;
+  if (tune(T_CONV_X6) == 0) return false;  // the on-the-fly split kernels
   const mia_conv_args& a = k.a;
   const ConvGroup& G = k.g[0];
   return dtype == MIA_F32 && G.w_split != nullptr && k.ng == 1 && k.stride == 1 && G.kh == 3 &&
@@ -569,8 +556,7 @@ int launch_conv_halo_x6(ConvK& k, hipStream_t st) {
     }
   }
 #endif
-  const char* e = getenv("MIA_HALO_EPI");  // A/B: 0 = LDS-staged shared epilogue, 2 = runtime
-  const int sel = e ? atoi(e) : 1;          // register epilogue; default 1 = specialised
+  const int sel = tune(T_HALO_EPI);  // 0 LDS-staged epilogue, 2 runtime; default 1 specialised
   if (k.a.Cout == 64) {
     if (sel == 0) return pro ? launch_x6_<64, true, -2>(k, st) : launch_x6_<64, false, -2>(k, st);
     if (sel == 1) return pro ? launch_x6_spec<64, true>(k, st) : launch_x6_spec<64, false>(k, st);

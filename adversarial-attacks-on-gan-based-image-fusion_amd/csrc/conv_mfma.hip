@@ -344,10 +344,8 @@ static int launch_tile(ConvK& k, hipStream_t st) {
     attr_set = true;
   }
   k.prered = prered_enabled() && EPI >= 0 && (EPI & epi::CSUM);
-  // X6B: s_setprio(1) around the MFMA blocks measured 1-2 % slower on this 2-blocks-per-CU tile;
-  // off unless MIA_X6B_PRIO=1 (A/B)
-  const char* pe = getenv("MIA_X6B_PRIO");
-  k.prio = pe && atoi(pe) != 0;
+  // X6B: s_setprio(1) around the MFMA blocks measured 1-2 % slower on this 2-blocks-per-CU tile
+  k.prio = 0;
   // deterministic sums: contributor slots per (image, channel) (sums need one group, identity
   // placement: run_conv)
   const int HWo = k.g[0].ho * k.g[0].wo;
@@ -374,11 +372,10 @@ typedef Tile<2, 2, 2, 2, 2> Tile64x64;
 // Register epilogue on the 128x128 tile: 2-byte types, one group, identity output placement,
 // every tile inside one image (HWo % 128 == 0), the feature masks of the heavy short-K launches
 // (the StyleGAN2 up-conv adjoint with its fused backward front; the e4e style-head convs).
-// MIA_CONV_REGEPI=0 disables (A/B switch, read per launch).
+// T_CONV_REGEPI = 0 disables (tests / tuning).
 static int reg_epi_mask(const ConvK& k, int bytes) {
-  const char* e = getenv("MIA_CONV_REGEPI");
   (void)bytes;
-  if ((e && atoi(e) == 0) || k.ng != 1 || k.batched || k.a.shuffle_out) return -1;
+  if (tune(T_CONV_REGEPI) == 0 || k.ng != 1 || k.batched || k.a.shuffle_out) return -1;
   const ConvGroup& G = k.g[0];
   if (G.ay != 1 || G.ax != 1 || G.by != 0 || G.bx != 0 || G.ho != k.HT || G.wo != k.WT ||
       (G.ho * G.wo) % 128 != 0)
@@ -398,21 +395,19 @@ template <typename T, bool PRO, bool SMALLC>
 static int launch_bn(ConvK& k, hipStream_t st) {
   int64_t m = 0;
   for (int g = 0; g < k.ng; ++g) m += k.g[g].m;
-  // Tuning override MIA_CONV_TILE (read per launch): 2 = 256x128 3-stage tile where the launch
+  // Tuning override T_CONV_TILE (tests / tuning): 2 = 256x128 3-stage tile where the launch
   // has ≥ 2 waves of them. Default 128x128: measured faster on every StyleGAN2/VGG shape of the
   // 256² attack step (2 blocks/CU hide each other's DMA waits better than 1 deeper ring).
-  const char* e = getenv("MIA_CONV_TILE");
-  const int force = e ? atoi(e) : 0;
+  const int force = tune(T_CONV_TILE);
   if (k.a.Cout <= 64) return launch_tile<T, Tile128x64, PRO, SMALLC>(k, st);
   // Launches with fewer 128x128 tiles than 2 per CU (the e4e style heads at 8²…1² outputs,
   // K = 9·512) run one block per CU and serialise each wave's LDS reads, MFMAs and the step
-  // barrier; 64x64 tiles put 4× the blocks (and waves) on the chip. MIA_CONV_SMALLTILE = the
-  // 128x128-tile count below which this applies (A/B switch, read per launch; 0 disables).
-  const char* es = getenv("MIA_CONV_SMALLTILE");
+  // barrier; 64x64 tiles put 4× the blocks (and waves) on the chip. T_CONV_SMALLTILE = the
+  // 128x128-tile count below which this applies (T_CONV_SMALLTILE; 0 disables).
   int64_t tiles = 0;
   for (int g = 0; g < k.ng; ++g) tiles += (k.g[g].m + 127) / 128;
   tiles *= (k.a.Cout + 127) / 128;
-  const int64_t small_below = es ? atoi(es) : 512;
+  const int64_t small_below = tune(T_CONV_SMALLTILE);
   // (2-byte types only: in fp32, the reference-precision path, a small image keeps one tile per
   // image row block, so its sdot / csum sums stay single-atomic and run-to-run deterministic)
   if (sizeof(T) == 2 && tiles < small_below) return launch_tile<T, Tile64x64, PRO, SMALLC>(k, st);
@@ -442,8 +437,7 @@ static bool x6b_ok(const ConvK& k) {
   (void)k;
   return false;
 #else
-  const char* e = getenv("MIA_CONV_X6");
-  if (e && atoi(e) == 0) return false;
+  if (tune(T_CONV_X6) == 0) return false;
   for (int g = 0; g < k.ng; ++g)
     if (!k.g[g].w_split) return false;
   return k.a.in_scale == nullptr && k.a.act_in == MIA_ACT_NONE && k.a.Cin >= 32 && k.a.Cout > 64;

@@ -574,7 +574,7 @@ __global__ __launch_bounds__(256) void conv_thin_out_f32_kernel(
 
 // 32 → 32 layers: 2-byte type, one group, stride 1, 3×3 pad 1, identity placement, W % 16 == 0,
 // an epilogue feature mask with a specialisation (the StyledConv forward and input gradient).
-// MIA_CONV_THIN32=0 disables (A/B switch, read per launch).
+// T_CONV_THIN32 = 0 disables (tests / tuning).
 static bool thin32_mask_ok(int f, bool pro) {
   using namespace epi;
   if (pro) return f == (OSC | NOISE | BIAS | LRELU);
@@ -588,8 +588,7 @@ static bool thin32_mask_ok(int f, bool pro) {
 }
 
 bool conv_thin32_eligible(const ConvK& k, int dtype) {
-  const char* e = getenv("MIA_CONV_THIN32");
-  if (e && atoi(e) == 0) return false;
+  if (tune(T_CONV_THIN32) == 0) return false;
   const mia_conv_args& a = k.a;
   const ConvGroup& G = k.g[0];
   if (dtype == MIA_F32 || k.ng != 1 || k.stride != 1 || G.kh != 3 || G.kw != 3 || G.pad_y != 1 ||
@@ -645,8 +644,7 @@ int launch_conv_thin32(ConvK& k, int dtype, hipStream_t st) {
 // group, stride 1, 3×3 pad 1, identity output placement, W % 16 == 0, and either (Cin 8 → Cout
 // 64, epilogue = bias + ReLU / PReLU: the VGG and e4e input layers) or (Cin 64 → Cout 8, plain or accumulating: their input gradients).
 bool conv_thin_eligible(const ConvK& k, int dtype) {
-  const char* e = getenv("MIA_CONV_THIN");  // tuning / A-B switch: 0 disables the thin kernels
-  if (e && atoi(e) == 0) return false;
+  if (tune(T_CONV_THIN) == 0) return false;
   const mia_conv_args& a = k.a;
   const ConvGroup& G = k.g[0];
   if (k.ng != 1 || k.stride != 1 || G.kh != 3 || G.kw != 3 || G.pad_y != 1 ||

@@ -369,8 +369,7 @@ static int launch_upconv_halo(UpK& k, hipStream_t st) {
 }
 
 bool upconv_halo_eligible(int dtype, int R, int Cin, int Cout) {
-  const char* e = getenv("MIA_UPCONV_HALO");  // tuning / A-B switch: 0 = generic phase GEMMs
-  if (e && atoi(e) == 0) return false;
+  if (tune(T_UPCONV_HALO) == 0) return false;  // the generic phase GEMMs
   return R % 16 == 0 && Cin % 64 == 0 && Cout % 32 == 0 &&
          (int64_t)(2 * R + 1) * (2 * R + 1) < (1LL << 31);
 }
@@ -706,34 +705,25 @@ static int launch_upconv_x6_e(UpK& k, hipStream_t st) {
 
 template <bool DG, bool PRO>
 static int launch_upconv_x6(UpK& k, hipStream_t st) {
-  // the next block's halo DMA at the step start (default; measured +2-3 % on the stride-1 layers,
-  // neutral on the up-conv) or between the two MFMA halves (MIA_X6_EARLY=0, A/B)
-  const char* e = getenv("MIA_X6_EARLY");
-  // s_setprio(1) around the MFMA blocks: neutral here (+1 / −1 % by layer), off unless
-  // MIA_UPX6_PRIO=1 (A/B)
-  const char* pe = getenv("MIA_UPX6_PRIO");
-  const bool prio = pe && atoi(pe) != 0;
-  if (!e || atoi(e) != 0)
-    return prio ? launch_upconv_x6_e<DG, PRO, true, true>(k, st)
-                : launch_upconv_x6_e<DG, PRO, true, false>(k, st);
-  return launch_upconv_x6_e<DG, PRO, false, false>(k, st);
+  // the next block's halo DMA at the step start (as the x6 halo kernel; neutral here against
+  // issuing it between the two MFMA halves); no s_setprio (neutral, +1 / −1 % by layer)
+  return launch_upconv_x6_e<DG, PRO, true, false>(k, st);
 }
 
-// the split-once kernel: fp32 with pre-split weights, R % 16 == 0, Cx % 64 == 0 (MIA_S2DG_X6=0
-// disables: A/B switch, read per launch). Measured against the on-the-fly split kernel (fp32,
+// the split-once kernel: fp32 with pre-split weights, R % 16 == 0, Cx % 64 == 0 (T_S2DG_X6 = 0
+// disables: tests / tuning). Measured against the on-the-fly split kernel (fp32,
 // 128 images, tools/layer_table.py): the 7 concatenated fine heads 146 → 210 TFLOP/s, single
 // 512-channel heads at 16² 133 → 197, the bottleneck units (Cg 64 / 128 / 256) 69 / 97 / 122 →
 // 96 / 147 / 176 — faster at every shape of the attack despite the exposed prologue / epilogue.
 // the split-once kernel for the up-sampling conv forward (fp32, w_up_split given; the last row /
-// column still goes to the generic kernel). MIA_UPCONV_X6=0 disables (A/B switch, per launch).
+// column still goes to the generic kernel). T_UPCONV_X6 = 0 disables (tests / tuning).
 static bool upconv_x6_ok(const UpK& k, int dtype) {
 #ifdef MIA_F32_NATIVE
   (void)k;
   (void)dtype;
   return false;
 #else
-  const char* e = getenv("MIA_UPCONV_X6");
-  if (e && atoi(e) == 0) return false;
+  if (tune(T_UPCONV_X6) == 0) return false;
   return dtype == MIA_F32 && k.w_split && k.R % DgX6::PH == 0 && k.Cout % DgX6::BN == 0 &&
          k.Cin % DgX6::BK == 0;
 #endif
@@ -745,16 +735,14 @@ static bool s2dg_x6_ok(const UpK& k, int dtype) {
   (void)dtype;
   return false;
 #else
-  const char* e = getenv("MIA_S2DG_X6");
-  if (e && atoi(e) == 0) return false;
+  if (tune(T_S2DG_X6) == 0) return false;
   return dtype == MIA_F32 && k.w_split && k.R % DgX6::PH == 0 && k.Cout % DgX6::BN == 0 &&
          k.cin_src % DgX6::BK == 0;
 #endif
 }
 
 bool s2_dgrad_halo_eligible(int dtype, int R, int Cg, int Cx) {
-  const char* e = getenv("MIA_S2DG_HALO");  // tuning / A-B switch: 0 = generic phase GEMMs
-  if (e && atoi(e) == 0) return false;
+  if (tune(T_S2DG_HALO) == 0) return false;  // the generic phase GEMMs
   (void)dtype;
   return R % 16 == 0 && Cg % 64 == 0 && Cx % HaloUp::BN == 0 &&
          (int64_t)4 * R * R < (1LL << 31);

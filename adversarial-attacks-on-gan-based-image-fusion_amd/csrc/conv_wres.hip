@@ -245,8 +245,7 @@ static bool wres_mask_ok(int f) {
 }
 
 bool conv_wres_eligible(const ConvK& k, int dtype) {
-  const char* e = getenv("MIA_CONV_WRES");  // tuning / A-B switch: 0 disables this kernel
-  if (e && atoi(e) == 0) return false;
+  if (tune(T_CONV_WRES) == 0) return false;
   const mia_conv_args& a = k.a;
   const ConvGroup& G = k.g[0];
   return dtype != MIA_F32 && k.ng == 1 && k.stride == 1 && G.kh == 3 && G.kw == 3 &&

@@ -48,6 +48,31 @@ __device__ __forceinline__ float wave_sum(float v) {
 int set_error(const std::string& msg);
 int check_launch(const char* what);
 
+// Kernel-variant switches (tests' bitwise A/B comparisons and the tuning tools; the product path
+// never changes them): read ONCE from the environment (MIA_<NAME>=value) at first use, then only
+// through mia_set_tuning() — no getenv on the launch path. The defaults are the measured-best
+// choices.
+enum TuneKey {
+  T_CONV_HALO,       // 0: the 2-byte stride-1 convs on the generic tile instead of the halo tile
+  T_CONV_X6,         // 0: the fp32 convs on the on-the-fly split kernels instead of split-once
+  T_HALO_EPI,        // halo tiles' epilogue: 0 LDS-staged, 1 specialised (default), 2 runtime
+  T_X6_UNR,          // 0: the x6 halo kernel's rolled tap loop
+  T_X6_64AUX,        // 1: the 64-column x6 tile for the tap-pair launches too
+  T_CONV_THIN,       // 0: no thin-channel input-layer kernels
+  T_CONV_THIN32,     // 0: no 32-channel thin kernel
+  T_CONV_WRES,       // 0: no weights-resident 64 → 64 kernel
+  T_CONV_TILE,       // 2: the 256×128 generic tile where it has ≥ 2 waves of blocks
+  T_CONV_REGEPI,     // 0: no register epilogue on the generic 128×128 tile
+  T_CONV_SMALLTILE,  // 64×64 generic tiles below this many 128×128 tiles (2-byte types)
+  T_S2DG_X6,         // 0: the stride-2 input gradients on the on-the-fly split up-conv kernel
+  T_S2DG_HALO,       // 0: the stride-2 input gradients as 4 sub-pixel phase GEMMs
+  T_UPCONV_X6,       // 0: the fp32 up-conv forward on the on-the-fly split kernel
+  T_UPCONV_HALO,     // 0: the up-conv forward as 4 sub-pixel phase GEMMs
+  T_EPI_PRERED,      // 0: no LDS pre-reduction of the channel sums in the register epilogues
+  T_NKEYS
+};
+int tune(TuneKey key);
+
 // ---- deterministic reductions (reduce.hip) ---------------------------------------------------
 // Per-(image, channel) sums that many blocks contribute to (the StyledConv style gradient sdot,
 // the backward front's q, the channel sums, per-image losses) never use float atomics: every

@@ -4,6 +4,8 @@
 // run to run (SURVEY.md §5 asks for bit-identical reruns; the reference runs with
 // cudnn.deterministic, code/attack/interpolation.py:195-200).
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <mutex>
 #include <unordered_map>
 
@@ -19,6 +21,32 @@ struct Scratch {
 std::mutex g_mu;
 std::unordered_map<hipStream_t, Scratch> g_scratch;
 }  // namespace
+
+// ---- kernel-variant switches (mia_common.h TuneKey) ------------------------------------------
+namespace {
+struct TuneDef {
+  const char* name;
+  int value;
+};
+TuneDef g_tune[T_NKEYS] = {
+    {"MIA_CONV_HALO", 1}, {"MIA_CONV_X6", 1},       {"MIA_HALO_EPI", 1},    {"MIA_X6_UNR", 1},
+    {"MIA_X6_64AUX", 0},  {"MIA_CONV_THIN", 1},     {"MIA_CONV_THIN32", 1}, {"MIA_CONV_WRES", 1},
+    {"MIA_CONV_TILE", 0}, {"MIA_CONV_REGEPI", 1},   {"MIA_CONV_SMALLTILE", 512},
+    {"MIA_S2DG_X6", 1},   {"MIA_S2DG_HALO", 1},     {"MIA_UPCONV_X6", 1},   {"MIA_UPCONV_HALO", 1},
+    {"MIA_EPI_PRERED", 1}};
+std::once_flag g_tune_once;
+void tune_init() {
+  for (auto& d : g_tune) {
+    const char* e = getenv(d.name);
+    if (e && *e) d.value = atoi(e);
+  }
+}
+}  // namespace
+
+int tune(TuneKey key) {
+  std::call_once(g_tune_once, tune_init);
+  return g_tune[key].value;
+}
 
 float* red_scratch(hipStream_t st, size_t bytes) {
   std::lock_guard<std::mutex> lock(g_mu);
@@ -124,4 +152,26 @@ extern "C" int mia_release_reduction_scratch(void* stream) {
   }
   g_scratch.erase(it);
   return MIA_OK;
+}
+
+extern "C" int mia_set_tuning(const char* name, int value) {
+  std::call_once(g_tune_once, tune_init);
+  MIA_CHECK_ARG(name != nullptr, "null name");
+  for (auto& d : g_tune)
+    if (strcmp(d.name, name) == 0) {
+      d.value = value;
+      return MIA_OK;
+    }
+  return set_error(std::string("unknown tuning switch ") + name);
+}
+
+extern "C" int mia_get_tuning(const char* name, int* value) {
+  std::call_once(g_tune_once, tune_init);
+  MIA_CHECK_ARG(name != nullptr && value != nullptr, "null argument");
+  for (auto& d : g_tune)
+    if (strcmp(d.name, name) == 0) {
+      *value = d.value;
+      return MIA_OK;
+    }
+  return set_error(std::string("unknown tuning switch ") + name);
 }

@@ -953,8 +953,7 @@ def s2_dgrad_halo(g, w_halo, gx, mask_a=None, mask_slope=None, accumulate=False,
 
 def s2_dgrad_halo_ok(dtype, R, Cg, Cx):
     """Host mirror of s2_dgrad_halo_eligible (csrc/conv_upconv.hip)."""
-    import os
-    if os.environ.get("MIA_S2DG_HALO") == "0":
+    if _lib.get_tuning("MIA_S2DG_HALO") == 0:
         return False
     return R % 16 == 0 and Cg % 64 == 0 and Cx % 64 == 0
 

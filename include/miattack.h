@@ -65,6 +65,15 @@ int mia_reserve_reduction_scratch(int64_t bytes, void* stream);
 int64_t mia_reduction_scratch_bytes(void* stream);
 /* free the stream's scratch (synchronises `stream`) */
 int mia_release_reduction_scratch(void* stream);
+
+/* ---- kernel-variant switches ------------------------------------------------------------------
+ * Every conv launch picks its kernel variant from a table of named switches (MIA_CONV_HALO,
+ * MIA_CONV_X6, MIA_HALO_EPI, ... — csrc/reduce.hip g_tune). The defaults are the measured-best
+ * choices; the table is read ONCE from the environment at first use, then changed only through
+ * mia_set_tuning (the A/B tools and the variant-coverage tests). No launch reads the environment.
+ * Replaces: nothing in the reference (cuDNN's algorithm choice is internal). */
+int mia_set_tuning(const char* name, int value);   /* MIA_ERR_ARG for an unknown name */
+int mia_get_tuning(const char* name, int* value);
 /* K-padding the conv weights need for `dtype` (weights are [Cout][Kpad], K = 9*Cin). */
 int mia_conv_kpad(int cin, int dtype);
 

@@ -43,3 +43,17 @@ def pytest_make_parametrize_id(config, val, argname):
     except Exception:
         pass
     return None
+
+
+@pytest.fixture
+def tune(cuda):
+    """Set libmiattack kernel-variant switches for one test (mia_set_tuning), restored after."""
+    from gfa_amd import _lib
+    saved = {}
+
+    def set_(name, value):
+        old = _lib.set_tuning(name, int(value))
+        saved.setdefault(name, old)
+    yield set_
+    for name, old in saved.items():
+        _lib.set_tuning(name, old)

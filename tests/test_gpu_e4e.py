@@ -156,12 +156,12 @@ def test_conv2d_batched_heads(cuda, dtype, N, H, S):
                                           (2, 16, 3, 64, 64), (1, 16, 4, 256, 192)])
 @pytest.mark.parametrize("mask", [False, True])
 @pytest.mark.parametrize("x6", ["1", "0"])
-def test_s2_dgrad_halo_multi_source(cuda, monkeypatch, dtype, N, R, ng, cg, cx, mask, x6):
+def test_s2_dgrad_halo_multi_source(cuda, tune, dtype, N, R, ng, cg, cx, mask, x6):
     """mia_conv_s2_dgrad_halo_multi: the summed input gradients of ng stride-2 convs reading the
     same tensor (the e4e style heads on one FPN map) in one K loop, vs autograd of the sum. fp32
     runs the split-once kernel (MIA_S2DG_X6=1, the default; 0 = the on-the-fly split kernel);
     the 7 × 512 case is the fine heads' shape at batch 1."""
-    monkeypatch.setenv("MIA_S2DG_X6", x6)
+    tune("MIA_S2DG_X6", x6)
     ws = [rnd((cg, cx, 3, 3), 80 + i, math.sqrt(2 / (9 * cx))) for i in range(ng)]
     gs = [rnd((N, cg, R, R), 90 + i) for i in range(ng)]
     a_below = rnd((N, cx, 2 * R, 2 * R), 98)

@@ -51,10 +51,10 @@ def test_conv3x3_bias_relu(cuda, dtype, N, H, Cin, Cout):
                                             (2, 32, 16, 64, 8), (1, 16, 16, 128, 24)])
 @pytest.mark.parametrize("mode", ["bias_relu", "modconv", "dgrad_sdot", "tap_mask"])
 @pytest.mark.parametrize("halo", ["1", "0"])
-def test_conv3x3_halo_and_generic_paths(cuda, monkeypatch, dtype, N, H, W, Cin, Cout, mode, halo):
+def test_conv3x3_halo_and_generic_paths(cuda, tune, dtype, N, H, W, Cin, Cout, mode, halo):
     """Stride-1 3×3 layers on 16-divisible maps take the halo-tiled kernel (conv_halo.hip) unless
     MIA_CONV_HALO=0; both paths, with every epilogue feature the attack uses, against torch."""
-    monkeypatch.setenv("MIA_CONV_HALO", halo)
+    tune("MIA_CONV_HALO", halo)
     g = torch.Generator().manual_seed(N * 7 + H + W + Cin + Cout)
     x = torch.randn(N, Cin, H, W, generator=g)
     w = torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)
@@ -509,10 +509,10 @@ def test_upconv_subpixel_fwd_bwd(cuda, dtype, N, cin, cout, R, store_act):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("kind", ["plain", "modconv", "dgrad_sdot"])
 @pytest.mark.parametrize("tile", ["1", "2"])
-def test_conv_large_m_tiles(cuda, dtype, kind, tile, monkeypatch):
+def test_conv_large_m_tiles(cuda, dtype, kind, tile, tune):
     """Large-M launches on the default 128×128 tile and on the 256×128 3-stage DMA-ring tile
     (MIA_CONV_TILE=2), checked against torch's conv."""
-    monkeypatch.setenv("MIA_CONV_TILE", tile)
+    tune("MIA_CONV_TILE", tile)
     g = torch.Generator().manual_seed(17)
     N, H, Cin, Cout = 8, 128, 64, 128
     x = torch.randn(N, Cin, H, H, generator=g)
@@ -608,7 +608,7 @@ def test_fused_backward_front_epilogue(cuda, dtype, N, H, Cin, Cout, up):
 @pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 17, 16), (3, 16, 64), (9, 256, 256)])
 @pytest.mark.parametrize("thin", ["1", "0"])
 @pytest.mark.parametrize("e4e", [False, True])
-def test_conv_thin_vgg_input_layer(cuda, monkeypatch, dtype, N, H, W, thin, e4e):
+def test_conv_thin_vgg_input_layer(cuda, tune, dtype, N, H, W, thin, e4e):
     """VGG conv1_1 forward (8-channel padded image → 64, bias, ReLU) and its input gradient
     (64 → 8 channels, 3 real) on the thin-channel kernels (conv_thin.hip; MIA_CONV_THIN=0 = the
     implicit-GEMM tiles), against torch fp64 on the same rounded operands. e4e: the encoder's
@@ -617,7 +617,7 @@ def test_conv_thin_vgg_input_layer(cuda, monkeypatch, dtype, N, H, W, thin, e4e)
     pixels exceed one pass of their persistent grid."""
     if (N, H, W) == (9, 256, 256) and dtype != torch.float32:
         pytest.skip("the persistent-loop shape is checked for the fp32 VALU kernels")
-    monkeypatch.setenv("MIA_CONV_THIN", thin)
+    tune("MIA_CONV_THIN", thin)
     if e4e:
         return _thin_e4e_input_layer(cuda, dtype, N, H, W)
     g = torch.Generator().manual_seed(N * 100 + H + W)
@@ -650,14 +650,14 @@ def test_conv_thin_vgg_input_layer(cuda, monkeypatch, dtype, N, H, W, thin, e4e)
                                           (1, 64, 64, 8), (2, 64, 32, 32), (1, 128, 96, 16)])
 @pytest.mark.parametrize("lrelu_in", [False, True])
 @pytest.mark.parametrize("x6", ["1", "0"])
-def test_upconv_halo_fwd(cuda, monkeypatch, dtype, N, cin, cout, R, lrelu_in, x6):
+def test_upconv_halo_fwd(cuda, tune, dtype, N, cin, cout, R, lrelu_in, x6):
     """mia_upconv_fwd_halo(_split) (halo-tiled interior + generic last row / column) against the
     transposed conv in fp64 on the same rounded operands, and against the phase-GEMM path
     (R = 8: the library falls back to it). fp32: the split-once kernel (MIA_UPCONV_X6=1, the
     default) and the on-the-fly split kernel (0)."""
     if x6 == "0" and dtype != torch.float32:
         pytest.skip("the split-once kernel exists for fp32 only")
-    monkeypatch.setenv("MIA_UPCONV_X6", x6)
+    tune("MIA_UPCONV_X6", x6)
     g = torch.Generator().manual_seed(N + cin + cout + R)
     x = torch.randn(N, cin, R, R, generator=g)
     w = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(9 * cin)
@@ -689,14 +689,14 @@ def test_upconv_halo_fwd(cuda, monkeypatch, dtype, N, cin, cout, R, lrelu_in, x6
 @pytest.mark.parametrize("mode", ["plain", "bias_relu", "tap_mask", "prelu", "bias_csum",
                                   "mask_slope", "acc"])
 @pytest.mark.parametrize("spec", ["1", "0"])
-def test_conv2d_register_epilogue_paths(cuda, monkeypatch, dtype, N, H, W, C, mode, spec):
+def test_conv2d_register_epilogue_paths(cuda, tune, dtype, N, H, W, C, mode, spec):
     """Stride-1 C→C 3×3 convs with every epilogue feature set of the attack step (vgg.py, e4e
     IR-SE50 body). spec=1: the specialised register epilogues — at C = 64 the weights-resident
     persistent kernel (conv_wres.hip; 192² = 288 patches > one per CU exercises the persistent
     loop and the halo prefetch), at C = 128 the halo kernel; spec=0: generic tile at 64
     (MIA_CONV_WRES=0) and the runtime-feature halo epilogue at 128 (MIA_HALO_EPI=2)."""
-    monkeypatch.setenv("MIA_CONV_WRES", spec)
-    monkeypatch.setenv("MIA_HALO_EPI", "1" if spec == "1" else "2")
+    tune("MIA_CONV_WRES", spec)
+    tune("MIA_HALO_EPI", "1" if spec == "1" else "2")
     g = torch.Generator().manual_seed(N * 11 + H + W + C + len(mode))
     x = torch.randn(N, C, H, W, generator=g)
     w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
@@ -831,13 +831,13 @@ def _thin_e4e_input_layer(cuda, dtype, N, H, W):
 @pytest.mark.parametrize("N,H,W", [(2, 32, 48), (3, 16, 16), (4, 256, 256)])
 @pytest.mark.parametrize("mode", ["modconv", "dgrad_sdot", "plain", "acc"])
 @pytest.mark.parametrize("thin", ["1", "0"])
-def test_conv_thin32_layers(cuda, monkeypatch, dtype, N, H, W, mode, thin):
+def test_conv_thin32_layers(cuda, tune, dtype, N, H, W, mode, thin):
     """32 → 32-channel layers (StyleGAN2 1024² StyledConvs) on the weights-in-VGPR thin kernel
     (conv_thin.hip conv_thin32_kernel; MIA_CONV_THIN32=0 = the implicit-GEMM tile): modulated
     forward with demod / noise / bias / lrelu·√2, the input gradient with the style-gradient sdot
     (partials kept per image run, flushed on image change: 4 × 256² exercises long runs), plain
     and accumulating, against torch fp64."""
-    monkeypatch.setenv("MIA_CONV_THIN32", thin)
+    tune("MIA_CONV_THIN32", thin)
     C = 32
     g = torch.Generator().manual_seed(N * 31 + H + W + len(mode))
     x = torch.randn(N, C, H, W, generator=g)
@@ -894,7 +894,7 @@ def test_memset_fill_kernel(cuda, off, nbytes, value):
 
 
 @pytest.mark.parametrize("path", ["halo", "halo_otf", "generic", "upconv"])
-def test_fp32_arithmetic_is_fp32_accurate(cuda, monkeypatch, path):
+def test_fp32_arithmetic_is_fp32_accurate(cuda, tune, path):
     """The fp32 convs run as exact three-way bf16 splits with six products (conv_common.h,
     mfma_chunk<float>; the dropped mid·lo, lo·mid, lo·lo terms are < 2^-23·|ab|). At the largest
     K of the attack (9·512 = 4608) the error against fp64 is set by the fp32 accumulation, as for
@@ -903,8 +903,8 @@ def test_fp32_arithmetic_is_fp32_accurate(cuda, monkeypatch, path):
     halo / generic / upconv; the split build: 1.18e-5 / 9.1e-6 / 5.6e-6 and 1.05e-6 / 1.05e-6 /
     5.8e-7). Bound: 2× the native figures. "halo" = the split-once kernel (conv_halo_x6.hip,
     pre-split weights), "halo_otf" = the on-the-fly split halo kernel (MIA_CONV_X6=0)."""
-    monkeypatch.setenv("MIA_CONV_HALO", "0" if path == "generic" else "1")
-    monkeypatch.setenv("MIA_CONV_X6", "0" if path == "halo_otf" else "1")
+    tune("MIA_CONV_HALO", "0" if path == "generic" else "1")
+    tune("MIA_CONV_X6", "0" if path == "halo_otf" else "1")
     g = torch.Generator().manual_seed(77)
     N, H, Cin, Cout = 2, 16, 512, 256
     x = torch.randn(N, Cin, H, H, generator=g)
@@ -935,7 +935,7 @@ def test_fp32_arithmetic_is_fp32_accurate(cuda, monkeypatch, path):
 @pytest.mark.parametrize("C,H,W", [(64, 32, 48), (128, 32, 16), (256, 16, 16)])
 @pytest.mark.parametrize("mode", ["plain", "bias_relu", "prelu", "mask_slope", "acc", "mask",
                                   "tap_mask", "bias"])
-def test_x6_halo_variants_bitwise(cuda, monkeypatch, C, H, W, mode):
+def test_x6_halo_variants_bitwise(cuda, tune, C, H, W, mode):
     """fp32 split-once halo kernel (conv_halo_x6.hip): the default launch (specialised register
     epilogue, taps unrolled over lane-constant fragment offsets, weight rows past Cout clamped)
     computes the same products in the same order as the rolled loop with the runtime-feature
@@ -992,10 +992,10 @@ def test_x6_halo_variants_bitwise(cuda, monkeypatch, C, H, W, mode):
 
     if mode == "tap_mask":
         ref = (conv + 0.37 * (a.double() - t.double())) * (a.double() > 0)
-    monkeypatch.setenv("MIA_X6_64AUX", "1")  # the 64-column tile for the tap launch too
+    tune("MIA_X6_64AUX", "1")  # the 64-column tile for the tap launch too
     y_def = run()
-    monkeypatch.setenv("MIA_X6_UNR", "0")
-    monkeypatch.setenv("MIA_HALO_EPI", "2")
+    tune("MIA_X6_UNR", "0")
+    tune("MIA_HALO_EPI", "2")
     y_gen = run()
     assert torch.equal(y_def, y_gen)
     assert rel_err(nchw(y_def), ref) < 2 * TOL[torch.float32]
@@ -1004,7 +1004,7 @@ def test_x6_halo_variants_bitwise(cuda, monkeypatch, C, H, W, mode):
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("C,H,W", [(128, 32, 16), (256, 16, 32)])
 @pytest.mark.parametrize("mode", ["plain", "bias_relu", "mask", "tap", "mod", "sdot_bab"])
-def test_halo_lowp_unrolled_bitwise(cuda, monkeypatch, dtype, C, H, W, mode):
+def test_halo_lowp_unrolled_bitwise(cuda, tune, dtype, C, H, W, mode):
     """fp16 / bf16 halo kernel (conv_halo.hip): the specialised-epilogue launches run the taps
     unrolled over lane-constant fragment offsets; the runtime-feature epilogue (MIA_HALO_EPI=2)
     runs the rolled loop. Same reads, same MFMAs in the same order: outputs (and sdot / q sums)
@@ -1051,7 +1051,7 @@ def test_halo_lowp_unrolled_bitwise(cuda, monkeypatch, dtype, C, H, W, mode):
         return y.clone(), sd, q
 
     y_def, sd_def, q_def = run()
-    monkeypatch.setenv("MIA_HALO_EPI", "2")
+    tune("MIA_HALO_EPI", "2")
     y_rol, sd_rol, q_rol = run()
     if mode != "sdot_bab":
         assert torch.equal(y_def, y_rol), (mode, (y_def.float() - y_rol.float()).abs().max().item())

@@ -75,7 +75,15 @@ def test_vgg_taps_and_grad_vs_reference_golden(cuda, golden, dtype, tol):
         st_mx = ((got - ref).abs()[stable].max() / ref.abs().max()).item()
         print(f"VGG golden grad {dtype} {tag}: norm {nrm:.2e} max {rel_err(got, ref):.2e} "
               f"max on |g| > 1e-3·max {st_mx:.2e}")
-        assert nrm < 30 * tol and rel_err(got, ref) < 100 * tol, (tag, "grad", nrm)
+        if full and dtype == torch.float32:
+            # 36²: no ReLU / pool branch within rounding of a tie here — fp32 arithmetic only
+            # (measured norm 3.6e-6, max 4.5e-6)
+            assert nrm < 1e-5 and rel_err(got, ref) < 2e-5, (tag, "grad", nrm)
+        else:
+            # 256² (and bf16): ReLU masks of pre-activations within rounding of 0 flip between
+            # the two summation orders (fp32 s256 measured: norm 1.1e-3, max 9.4e-3); the
+            # arithmetic is pinned mask-for-mask in test_gpu_parity / test_gpu_networks
+            assert nrm < 30 * tol and rel_err(got, ref) < 100 * tol, (tag, "grad", nrm)
         assert gx[..., 3:].abs().max().item() == 0.0
 
 

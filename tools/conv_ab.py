@@ -1,8 +1,8 @@
 """A/B timing of the 3×3 conv kernels on the attack step's layer shapes (GPU, tuning aid).
 
 Usage: python tools/conv_ab.py [--batch 128] [--iters 5] VAR=a,b ...
-Each VAR=v1,v2 names an environment switch read per launch by libmiattack (MIA_HALO_RB,
-MIA_CONV_HALO, ...); every combination is timed on every shape with HIP events on the current
+Each VAR=v1,v2 names a kernel-variant switch of libmiattack (mia_set_tuning: MIA_CONV_HALO,
+MIA_HALO_EPI, ...); every combination is timed on every shape with HIP events on the current
 stream, and the algorithmic TFLOP/s (2·M·9·Cin·Cout) is printed. Not part of the product path."""
 import argparse
 import itertools
@@ -15,7 +15,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import gfa_import  # noqa: E402,F401
-from gfa_amd import ops  # noqa: E402
+from gfa_amd import _lib, ops  # noqa: E402
 
 # (name, H, Cin, Cout, mode)
 SHAPES = [
@@ -180,7 +180,7 @@ def main():
         line = f"{name:28s}"
         for c in combos:
             for k, v in zip(keys, c):
-                os.environ[k] = v
+                _lib.set_tuning(k, int(v))
             ms, tf, ref = run(name, H, Cin, Cout, mode, a.batch, a.iters, dtype, dev)
             refs.append(ref)
             d = (ref - refs[0]).abs().max().item() / max(refs[0].abs().max().item(), 1e-30)

@@ -2,8 +2,7 @@
 
 Usage: python tools/e4e_ab.py [--batch 128] [--iters 5] [VAR=a,b ...]
 Times each conv shape of Encoder4Editing(50, 'ir_se') at 256² input (forward and input gradient)
-with HIP events and prints algorithmic TFLOP/s; VAR=v1,v2 environment switches (read per launch
-by libmiattack) are A/B-compared as in tools/conv_ab.py. Not part of the product path."""
+with HIP events and prints algorithmic TFLOP/s; VAR=v1,v2 kernel-variant switches (mia_set_tuning) are A/B-compared as in tools/conv_ab.py. Not part of the product path."""
 import argparse
 import itertools
 import math
@@ -15,7 +14,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import gfa_import  # noqa: E402,F401
-from gfa_amd import e4e, layouts, ops  # noqa: E402
+from gfa_amd import _lib, e4e, layouts, ops  # noqa: E402
 
 # (name, kind, H_in, Cin, Cout, stride, count per encoder pass)
 SHAPES = [
@@ -92,7 +91,7 @@ def main():
         ref = None
         for c in combos:
             for k, v in zip(keys, c):
-                os.environ[k] = v
+                _lib.set_tuning(k, int(v))
             ms, tf, y = run(kind, H, Cin, Cout, stride, a.batch, a.iters, torch.float16, dev)
             ref = y if ref is None else ref
             d = (y - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30)

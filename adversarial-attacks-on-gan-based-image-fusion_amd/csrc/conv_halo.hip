@@ -93,6 +93,14 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
   constexpr int HPIECES = TL::HPIECES, BWAVES = TL::BWAVES, HWAVES = TL::HWAVES;
   constexpr int HPS = TL::H_PER_STEP;
 
+  // AUXP: the StyledConv forward (modulated input; demod, noise, bias, lrelu) prefetches its
+  // epilogue operands into the free halo buffer during the last channel block
+  constexpr bool AUXP = PRO && EPI == (epi::OSC | epi::NOISE | epi::BIAS | epi::LRELU) &&
+                        TL::NHBUF == 2 && TL::BN == 128 && TL::FM <= 4;
+  constexpr int AUX_OFF = 4096;  // past the LDS pre-reduction rows (3 × WM × BN floats)
+  static_assert(!AUXP || (AUX_OFF + 2048 <= TL::HBUF && 3 * TL::WM * TL::BN * 4 <= AUX_OFF &&
+                          4 * TL::PH <= 32),
+                "aux prefetch layout");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const hbuf = smem;                        // 2 halo buffers
   char* const bring = smem + TL::NHBUF * HBUF;    // weight ring
@@ -176,7 +184,16 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
     }
   };
 
-  // ---- prologue: style row, halo of channel block 0, weights of steps 0 … STAGES−2 -----------
+  // ---- prologue: halo of channel block 0, weights of steps 0 … STAGES−2, style row -----------
+  // (the style row after the DMA issue: its load latency overlaps the DMA's instead of preceding it)
+  if (bwave) {
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s) issue_b(s, s);  // nk ≥ 9
+  } else {
+#pragma unroll
+    for (int j = 0; j < H_INS; ++j)
+      if (j < my_pieces) issue_h(0, j, 0);
+  }
   if constexpr (PRO) {
     const float mul = lrelu_in ? SQRT2 : 1.f;
     for (int i = tid; i < Cin; i += NT) {
@@ -184,16 +201,8 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
       stab[i] = from_f<T>(sv * mul);
     }
   }
-  if (bwave) {
-#pragma unroll
-    for (int s = 0; s < STAGES - 1; ++s) issue_b(s, s);  // nk ≥ 9
-    wait_vmcnt((STAGES - 2) * B_INS);  // step 0 landed, steps 1, 2 may stay in flight
-  } else {
-#pragma unroll
-    for (int j = 0; j < H_INS; ++j)
-      if (j < my_pieces) issue_h(0, j, 0);
-    wait_vmcnt(0);
-  }
+  if (bwave) wait_vmcnt((STAGES - 2) * B_INS);  // step 0 landed, steps 1, 2 may stay in flight
+  else wait_vmcnt(0);
   __syncthreads();
   if constexpr (PRO && MIA_HALO_PREMOD) {
     premod(0, 0);
@@ -234,11 +243,33 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
       asm volatile("" : "+v"(v));
       ob[j] = v;
     }
+    // The StyledConv forward's epilogue operands (demod, bias: BN floats each; the patch's noise:
+    // PH rows × 16 floats) are DMA'd by H-wave 0 into the halo buffer the last channel block leaves
+    // free (past the LDS pre-reduction rows), at its first tap: they land under its MFMAs instead
+    // of one dependent round trip in the epilogue.
+    char* const aux = hbuf + (ncb & (TL::NHBUF - 1)) * HBUF + AUX_OFF;
+    auto issue_aux = [&]() {
+      const int l = lane & 31;
+      const float* a0;
+      if (lane < 32) {  // demod (out_scale) | noise rows
+        a0 = n0 + 4 * l < Cout ? p.out_scale + (size_t)n * k.cout_mod + n0 + 4 * l
+                               : (const float*)g_zero16;
+      } else {          // bias
+        a0 = n0 + 4 * l < Cout ? p.bias + n0 + 4 * l : (const float*)g_zero16;
+      }
+      __builtin_amdgcn_global_load_lds((gptr_t)a0, (lptr_t)aux, 16, 0, 0);
+      const float* a1 = lane < 4 * PH ? p.noise + (size_t)(y0 + (l >> 2)) * W + x0 + 4 * (l & 3)
+                                      : (const float*)g_zero16;
+      __builtin_amdgcn_global_load_lds((gptr_t)a1, (lptr_t)(aux + 1024), 16, 0, 0);
+    };
     int st = 0;
     for (int cb = 0; cb < ncb; ++cb) {
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int s = cb * 9 + t;
+        if constexpr (AUXP) {
+          if (t == 0 && cb + 1 == ncb && !bwave && hw == 0) issue_aux();
+        }
         int hoff = (cb & (TL::NHBUF - 1)) * HBUF, soff = st * BSTAGE, x1 = 64;
         asm volatile("" : "+s"(hoff), "+s"(soff), "+s"(x1));
         const char* ha = hbuf + hoff;
@@ -375,7 +406,27 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
   }
   }  // rolled loop
   HT_STAMP(t_loop);
-  if constexpr (EPI >= 0) {
+  if constexpr (AUXP) {
+    // the prefetched operands (landed: H-wave 0 drained them before the last step's barrier)
+    const char* aux = hbuf + (ncb & (TL::NHBUF - 1)) * HBUF + AUX_OFF;
+    EpiChan<FN> E;
+    EpiRows<T, FM, FN> R;
+    const int cl = n0 + wn * FN * 16 + ((lane >> 4) << 2);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int c = cl + 16 * j - n0;
+      E.osc[j] = *(const f32x4*)(aux + 4 * c);
+      E.bia[j] = *(const f32x4*)(aux + 512 + 4 * c);
+      E.dmv[j] = E.bbv[j] = E.msl[j] = E.asl[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      R.nz[i] = p.noise_w * *(const float*)(aux + 1024 + 4 * ((wm * FM + i) * 16 + (lane & 15)));
+      R.bnz[i] = 0.f;
+    }
+    halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, n0, wm, wn, lane, -1, -1, &R, nullptr,
+                                TL::WM, TL::BN, nullptr, &E);
+  } else if constexpr (EPI >= 0) {
     // (the LDS is idle after the main loop's last barrier: the pre-reduction reuses it)
     halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, n0, wm, wn, lane, -1, -1, nullptr,
                                 k.prered ? (float*)smem : nullptr, TL::WM, TL::BN);
@@ -484,10 +535,15 @@ bool conv_halo_eligible(const ConvK& k, int dtype) {
   const mia_conv_args& a = k.a;
   const ConvGroup& G = k.g[0];
   const int bk = dtype == MIA_F32 ? 32 : 64;
+  // Cout = 64 (T_HALO_C64: 0 never, 1 always, 2 = the bf16 modulated forward only): measured
+  // +39 % for the bf16 512² StyledConv forward (the generic tile's per-fragment bf16 modulation),
+  // −2 % fp16, −50 % for the input gradient with the sdot sums (r03_wres32_ab.log)
+  const int c64s = tune(T_HALO_C64);
+  const bool c64 = c64s == 1 || (c64s == 2 && dtype == MIA_BF16 && a.in_scale != nullptr);
   return k.ng == 1 && k.stride == 1 && G.kh == 3 && G.kw == 3 && G.pad_y == 1 && G.pad_x == 1 &&
          G.ho == a.H && G.wo == a.W && G.ay == 1 && G.ax == 1 && G.by == 0 && G.bx == 0 &&
          !a.shuffle_out && a.H % 16 == 0 && a.W % 16 == 0 && a.Cin % bk == 0 &&
-         (a.Cout > 64 || a.Cout <= 32) &&
+         (a.Cout > 64 || a.Cout <= 32 || (a.Cout == 64 && c64)) &&
          k.HT == a.H && k.WT == a.W;
 }
 

@@ -232,12 +232,9 @@ __device__ __forceinline__ void thin32_flush(const ConvK& k, EpiSums<2>& sums, i
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float a = sums.part[j][e], b = sums.partq[j][e], cs = sums.pcs[j][e];
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        if constexpr ((EPI & epi::SDOT) != 0) a += __shfl_xor(a, o, 64);
-        if constexpr ((EPI & epi::BAB) != 0) b += __shfl_xor(b, o, 64);
-        if constexpr ((EPI & epi::CSUM) != 0) cs += __shfl_xor(cs, o, 64);
-      }
+      if constexpr ((EPI & epi::SDOT) != 0) a = row16_sum(a);
+      if constexpr ((EPI & epi::BAB) != 0) b = row16_sum(b);
+      if constexpr ((EPI & epi::CSUM) != 0) cs = row16_sum(cs);
       const int c = 16 * j + 4 * fq + e;
       if (frow == 0) {
         if constexpr ((EPI & epi::SDOT) != 0) red_put(k, 0, slot, n * 32 + c, a);
@@ -445,18 +442,6 @@ __global__ __launch_bounds__(256) void conv_thin_in_f32_kernel(
   if (act == MIA_ACT_PRELU) sl = *(const f32x4*)(slope + c0);
   if (cmask == 0x07) thin_in_f32_body<0x07>(x, wl, cmask, bs, sl, act, y, N, H, W);
   else thin_in_f32_body<0xff>(x, wl, cmask, bs, sl, act, y, N, H, W);
-}
-
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float a) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, a), CTRL,
-                                                               0xf, 0xf, false));
-}
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]: every lane holds its quad's sum
-  v += dpp_f<0x141>(v);  // row_half_mirror: lane i ↔ 7 − i of its 8-lane half
-  return v + dpp_f<0x140>(v);  // row_mirror: lane i ↔ 15 − i
 }
 
 // input gradient, Cin = 64 → 8 output channels (store or accumulate). Lane q of a group holds

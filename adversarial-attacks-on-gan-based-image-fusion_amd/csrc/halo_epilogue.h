@@ -170,12 +170,9 @@ __device__ __forceinline__ void halo_epilogue(const ConvK& k, const f32x4 (&acc)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float a = part[j][e], b = partq[j][e], cs = pcs[j][e];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          a += __shfl_xor(a, o, 64);
-          b += __shfl_xor(b, o, 64);
-          cs += __shfl_xor(cs, o, 64);
-        }
+        a = row16_sum(a);
+        b = row16_sum(b);
+        cs = row16_sum(cs);
         if (px == 0 && c < Cout) {
           const int i = n * Cout + c + e;
           if (p.sdot) red_put(k, 0, slot, i, a);
@@ -224,6 +221,40 @@ struct EpiSums {
   float part[FN][4], partq[FN][4], pcs[FN][4];
 };
 
+// Per-channel epilogue constants of one image (demod / out scale, bias, the bias-act backward's
+// demod and bias, mask and PReLU slopes). A persistent caller that keeps a DMA in flight across
+// its epilogue loads them BEFORE issuing the DMA (epi_chan_load) and passes them in: loaded inside
+// the epilogue, their wait (vmcnt counts in issue order) would also wait for the DMA.
+template <int FN>
+struct EpiChan {
+  f32x4 osc[FN], bia[FN], dmv[FN], bbv[FN], msl[FN], asl[FN];
+};
+
+template <int F, int FN>
+__device__ __forceinline__ void epi_chan_load(const ConvK& k, EpiChan<FN>& E, int n, int cl) {
+  const mia_conv_args& p = k.a;
+  const int Cout = p.Cout;
+  const f32x4 one = {1.f, 1.f, 1.f, 1.f}, zero = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int c = cl + 16 * j;
+    E.osc[j] = one;
+    E.bia[j] = E.dmv[j] = E.bbv[j] = E.msl[j] = E.asl[j] = zero;
+    if (c < Cout) {  // c ≡ 0 mod 4, Cout ≡ 0 mod 8: the whole quad is in range
+      if constexpr ((F & epi::OSC) != 0)
+        E.osc[j] = *(const f32x4*)(p.out_scale + (size_t)n * k.cout_mod + c);
+      if constexpr ((F & epi::BIAS) != 0) E.bia[j] = *(const f32x4*)(p.bias + c);
+      if constexpr ((F & epi::MSL) != 0) E.msl[j] = *(const f32x4*)(p.mask_slope + c);
+      if constexpr (((F >> 8) & 3) == MIA_ACT_PRELU) E.asl[j] = *(const f32x4*)(p.act_slope + c);
+      if constexpr ((F & epi::BAB) != 0) {
+        E.dmv[j] = *(const f32x4*)(p.bab_demod + (size_t)n * Cout + c);
+        // no bias: four zeros from the zero page (a load either way: no branch around it)
+        E.bbv[j] = *(const f32x4*)(p.bab_bias ? p.bab_bias + c : (const float*)g_zero16);
+      }
+    }
+  }
+}
+
 // (Hg, Wg): the output grid the rows index; default (p.H, p.W). The generic tile passes a virtual
 // grid of 16-pixel rows (HWo / 16, 16), so that its linear pixel rows use the same indexing.
 // pre: the per-pixel operands of a single-chunk wave tile already gathered by the caller (the
@@ -233,7 +264,7 @@ __device__ __forceinline__ void halo_epilogue_f(
     const ConvK& k, const f32x4 (&acc)[TL::FM][TL::FN], int n, int y0, int x0, int n0, int wm,
     int wn, int lane, int Hg = -1, int Wg = -1,
     const EpiRows<T, EpiChunk<TL>::FMC, TL::FN>* pre = nullptr, float* red = nullptr, int nwm = 1,
-    int cw = 0, EpiSums<TL::FN>* keep = nullptr) {
+    int cw = 0, EpiSums<TL::FN>* keep = nullptr, const EpiChan<TL::FN>* chan = nullptr) {
   constexpr int FM = TL::FM, FN = TL::FN;
   constexpr bool OSC = F & epi::OSC, NOISE = F & epi::NOISE, BIAS = F & epi::BIAS;
   constexpr bool TAP = F & epi::TAP, MASK = F & epi::MASK, ACC = F & epi::ACC;
@@ -254,28 +285,18 @@ __device__ __forceinline__ void halo_epilogue_f(
   const T* MA = (const T*)p.mask_a;
   const bool ma_is_ta = MA == TA;
 
-  float osc[FN][4], bia[FN][4], dmv[FN][4], bbv[FN][4], msl[FN][4], asl[FN][4];
   bool cok[FN];
 #pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int c = cl + 16 * j;
-    cok[j] = c < Cout;  // c ≡ 0 mod 4, Cout ≡ 0 mod 8: the whole quad is in range
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      osc[j][e] = 1.f;
-      bia[j][e] = dmv[j][e] = bbv[j][e] = msl[j][e] = asl[j][e] = 0.f;
-    }
-    if (cok[j]) {
-      if constexpr (OSC) ld4f(p.out_scale + (size_t)n * k.cout_mod + c, osc[j]);
-      if constexpr (BIAS) ld4f(p.bias + c, bia[j]);
-      if constexpr (MSL) ld4f(p.mask_slope + c, msl[j]);
-      if constexpr (ACT == MIA_ACT_PRELU) ld4f(p.act_slope + c, asl[j]);
-      if constexpr (BAB) {
-        ld4f(p.bab_demod + (size_t)n * Cout + c, dmv[j]);
-        if (p.bab_bias) ld4f(p.bab_bias + c, bbv[j]);
-      }
-    }
-  }
+  for (int j = 0; j < FN; ++j) cok[j] = cl + 16 * j < Cout;
+  EpiChan<FN> El;
+  EpiChan<FN>& E = chan != nullptr ? *const_cast<EpiChan<FN>*>(chan) : El;
+  if (chan == nullptr) epi_chan_load<F, FN>(k, El, n, cl);
+  const auto& osc = E.osc;
+  const auto& bia = E.bia;
+  const auto& dmv = E.dmv;
+  const auto& bbv = E.bbv;
+  const auto& msl = E.msl;
+  const auto& asl = E.asl;
   float part[FN][4], partq[FN][4], pcs[FN][4];
 #pragma unroll
   for (int j = 0; j < FN; ++j)
@@ -414,12 +435,9 @@ __device__ __forceinline__ void halo_epilogue_f(
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float a = part[j][e], b = partq[j][e], cs = pcs[j][e];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          if constexpr (SDOT) a += __shfl_xor(a, o, 64);
-          if constexpr (BAB) b += __shfl_xor(b, o, 64);
-          if constexpr (CSUM) cs += __shfl_xor(cs, o, 64);
-        }
+        if constexpr (SDOT) a = row16_sum(a);
+        if constexpr (BAB) b = row16_sum(b);
+        if constexpr (CSUM) cs = row16_sum(cs);
         if (lds_red) {  // (quantity, wave row, block channel) in LDS
           if (px == 0) {
             const int lc = c - n0 + e;
@@ -438,8 +456,11 @@ __device__ __forceinline__ void halo_epilogue_f(
     }
     if (lds_red) {
       // the waves of one channel range meet here; the first wave row sums them (in wave order)
-      // and stores one partial per channel for the block (nwm× fewer partials)
-      __syncthreads();
+      // and stores one partial per channel for the block (nwm× fewer partials). LDS-only
+      // hand-off: lgkmcnt(0) + s_barrier, no memory fence (a fence would also wait for a
+      // persistent caller's halo DMA in flight)
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      __builtin_amdgcn_s_barrier();
       if (wm == 0 && px == 0) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) {

@@ -38,6 +38,20 @@ __device__ __forceinline__ float lrelu_s2_inv_grad(float pre) {
   return pre > 0.f ? 0.70710678118654752f : 3.5355339059327376f;
 }
 
+// Sum over each 16-lane row, the same butterfly as v += shfl_xor(v, 1, 2, 4, 8) (pairs, quads,
+// halves, rows: each add is own + partner, so every lane ends with the bit-identical value the
+// shuffles give) on the DPP crossbar — four VALU adds, no LDS round trips (ds_bpermute + a
+// lgkmcnt wait per step, serialised per value).
+#define MIA_DPP(v, ctrl) \
+  __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, (v)), (ctrl), 0xf, 0xf, false))
+__device__ __forceinline__ float row16_sum(float v) {
+  v += MIA_DPP(v, 0xB1);   // quad_perm [1,0,3,2]: lane ^ 1
+  v += MIA_DPP(v, 0x4E);   // quad_perm [2,3,0,1]: lane ^ 2
+  v += MIA_DPP(v, 0x141);  // row_half_mirror: lane i ↔ 7 − i within 8 (the other quad)
+  v += MIA_DPP(v, 0x140);  // row_mirror: lane i ↔ 15 − i (the other half-row)
+  return v;
+}
+
 // Wave-level sum (64 lanes).
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -69,6 +83,8 @@ enum TuneKey {
   T_UPCONV_X6,       // 0: the fp32 up-conv forward on the on-the-fly split kernel
   T_UPCONV_HALO,     // 0: the up-conv forward as 4 sub-pixel phase GEMMs
   T_EPI_PRERED,      // 0: no LDS pre-reduction of the channel sums in the register epilogues
+  T_CONV_WRES32,     // 0: the 32 → 32 layers on the global-gather kernel (conv_thin32)
+  T_HALO_C64,        // Cout = 64 on the 64-channel halo tile: 0 never, 1 always, 2 bf16 modulated fwd
   T_NKEYS
 };
 int tune(TuneKey key);
@@ -92,7 +108,8 @@ float* red_scratch(hipStream_t st, size_t bytes);
 // launches in which some slots may have no contributor). Returns MIA_OK or an error code.
 int red_begin(RedQ& r, float* d0, float* d1, float* d2, int nslots, int count, hipStream_t st,
               bool zero = false);
-// dst_q[i] += Σ_{slot = 0 … nslots−1} part[q][slot][i], in slot order
+// dst_q[i] += Σ_{slot = 0 … nslots−1} part[q][slot][i] in a fixed order that depends on nslots
+// only (slot order; beyond 128 slots the in-order sums of 64-slot chunks, added in chunk order)
 int red_finish(const RedQ& r, hipStream_t st);
 
 __device__ __forceinline__ void red_store(float* part, int nslots, int count, int q, int slot,

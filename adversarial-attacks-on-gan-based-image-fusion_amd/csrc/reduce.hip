@@ -33,7 +33,8 @@ TuneDef g_tune[T_NKEYS] = {
     {"MIA_X6_64AUX", 0},  {"MIA_CONV_THIN", 1},     {"MIA_CONV_THIN32", 1}, {"MIA_CONV_WRES", 1},
     {"MIA_CONV_TILE", 0}, {"MIA_CONV_REGEPI", 1},   {"MIA_CONV_SMALLTILE", 512},
     {"MIA_S2DG_X6", 1},   {"MIA_S2DG_HALO", 1},     {"MIA_UPCONV_X6", 1},   {"MIA_UPCONV_HALO", 1},
-    {"MIA_EPI_PRERED", 1}};
+    {"MIA_EPI_PRERED", 1},    {"MIA_CONV_WRES32", 1},
+    {"MIA_HALO_C64", 2}};
 std::once_flag g_tune_once;
 void tune_init() {
   for (auto& d : g_tune) {
@@ -67,6 +68,13 @@ float* red_scratch(hipStream_t st, size_t bytes) {
   return s.p;
 }
 
+// Slots are summed in chunks of RED_CHUNK (in slot order within a chunk, then the chunk sums in
+// chunk order): a fixed tree that depends on nslots only, so the result stays bit-reproducible
+// and independent of the other images of the call; one finishing thread per output walking
+// 16 K slots serially took milliseconds (the 512² / 1024² layers' per-row-segment slots).
+constexpr int RED_CHUNK = 64;
+static inline int red_nchunks(int nslots) { return nslots <= 2 * RED_CHUNK ? 1 : (nslots + RED_CHUNK - 1) / RED_CHUNK; }
+
 int red_begin(RedQ& r, float* d0, float* d1, float* d2, int nslots, int count, hipStream_t st,
               bool zero) {
   r.dst[0] = d0;
@@ -77,10 +85,12 @@ int red_begin(RedQ& r, float* d0, float* d1, float* d2, int nslots, int count, h
   r.part = nullptr;
   if (!d0 && !d1 && !d2) return MIA_OK;
   if (nslots < 1 || count < 1) return set_error("red_begin: empty reduction");
-  const size_t bytes = (size_t)3 * nslots * count * sizeof(float);
+  const int nch = red_nchunks(nslots);
+  const size_t part_bytes = (size_t)3 * nslots * count * sizeof(float);
+  const size_t bytes = part_bytes + (nch > 1 ? (size_t)3 * nch * count * sizeof(float) : 0);
   r.part = red_scratch(st, bytes);
   if (!r.part) return set_error("red_begin: scratch allocation failed");
-  if (zero && hipMemsetAsync(r.part, 0, bytes, st) != hipSuccess)
+  if (zero && hipMemsetAsync(r.part, 0, part_bytes, st) != hipSuccess)
     return set_error("red_begin: memset failed");
   return MIA_OK;
 }
@@ -99,10 +109,38 @@ __global__ __launch_bounds__(256) void red_finish_kernel(const float* __restrict
   dst[i] += s;
 }
 
+// chunk c of quantity q: tmp[q][c][i] = Σ_{slot in chunk c} part[q][slot][i], in slot order
+__global__ __launch_bounds__(256) void red_chunk_kernel(const float* __restrict__ part,
+                                                        float* __restrict__ tmp, int has0,
+                                                        int has1, int has2, int nslots,
+                                                        int count) {
+  const int q = blockIdx.z, c = blockIdx.y;
+  if (!(q == 0 ? has0 : (q == 1 ? has1 : has2))) return;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= count) return;
+  const int k0 = c * RED_CHUNK, k1 = min(k0 + RED_CHUNK, nslots);
+  const float* src = part + ((size_t)q * nslots + k0) * count + i;
+  float s = 0.f;
+  for (int k = k0; k < k1; ++k, src += count) s += *src;
+  tmp[((size_t)q * gridDim.y + c) * count + i] = s;
+}
+
 int red_finish(const RedQ& r, hipStream_t st) {
   if (!r.part) return MIA_OK;
-  hipLaunchKernelGGL(red_finish_kernel, dim3((r.count + 255) / 256, 3), dim3(256), 0, st, r.part,
-                     r.dst[0], r.dst[1], r.dst[2], r.nslots, r.count);
+  const int nch = red_nchunks(r.nslots);
+  if (nch == 1) {
+    hipLaunchKernelGGL(red_finish_kernel, dim3((r.count + 255) / 256, 3), dim3(256), 0, st,
+                       r.part, r.dst[0], r.dst[1], r.dst[2], r.nslots, r.count);
+    return check_launch("red_finish");
+  }
+  float* tmp = r.part + (size_t)3 * r.nslots * r.count;
+  hipLaunchKernelGGL(red_chunk_kernel, dim3((r.count + 255) / 256, nch, 3), dim3(256), 0, st,
+                     r.part, tmp, r.dst[0] != nullptr, r.dst[1] != nullptr, r.dst[2] != nullptr,
+                     r.nslots, r.count);
+  int rc = check_launch("red_chunk");
+  if (rc != MIA_OK) return rc;
+  hipLaunchKernelGGL(red_finish_kernel, dim3((r.count + 255) / 256, 3), dim3(256), 0, st, tmp,
+                     r.dst[0], r.dst[1], r.dst[2], nch, r.count);
   return check_launch("red_finish");
 }
 
@@ -118,7 +156,8 @@ extern "C" int64_t mia_conv_workspace_size(int N, int H_out, int W_out, int Cout
   if (!has_sums || N <= 0 || H_out <= 0 || W_out <= 0 || Cout <= 0) return 0;
   const int64_t hw = (int64_t)H_out * W_out;
   const int64_t slots = hw % 256 == 0 ? hw / 16 + 2 : hw + 2;
-  return (int64_t)3 * slots * N * Cout * (int64_t)sizeof(float);
+  const int64_t chunks = slots <= 2 * RED_CHUNK ? 0 : (slots + RED_CHUNK - 1) / RED_CHUNK;
+  return (int64_t)3 * (slots + chunks) * N * Cout * (int64_t)sizeof(float);
 }
 
 // pointwise reductions: one slot per block of ≥ 16 pixels (bias_act / torgb: 16 pixel passes of
@@ -126,7 +165,8 @@ extern "C" int64_t mia_conv_workspace_size(int N, int H_out, int W_out, int Cout
 extern "C" int64_t mia_reduction_workspace_size(int N, int HW, int C) {
   if (N <= 0 || HW <= 0 || C <= 0) return 0;
   const int64_t slots = std::max<int64_t>(1024, HW);
-  return (int64_t)3 * slots * N * C * (int64_t)sizeof(float);
+  const int64_t chunks = (slots + RED_CHUNK - 1) / RED_CHUNK;
+  return (int64_t)3 * (slots + chunks) * N * C * (int64_t)sizeof(float);
 }
 
 extern "C" int mia_reserve_reduction_scratch(int64_t bytes, void* stream) {

@@ -830,14 +830,16 @@ def _thin_e4e_input_layer(cuda, dtype, N, H, W):
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("N,H,W", [(2, 32, 48), (3, 16, 16), (4, 256, 256)])
 @pytest.mark.parametrize("mode", ["modconv", "dgrad_sdot", "plain", "acc"])
-@pytest.mark.parametrize("thin", ["1", "0"])
-def test_conv_thin32_layers(cuda, tune, dtype, N, H, W, mode, thin):
-    """32 → 32-channel layers (StyleGAN2 1024² StyledConvs) on the weights-in-VGPR thin kernel
-    (conv_thin.hip conv_thin32_kernel; MIA_CONV_THIN32=0 = the implicit-GEMM tile): modulated
-    forward with demod / noise / bias / lrelu·√2, the input gradient with the style-gradient sdot
-    (partials kept per image run, flushed on image change: 4 × 256² exercises long runs), plain
-    and accumulating, against torch fp64."""
-    tune("MIA_CONV_THIN32", thin)
+@pytest.mark.parametrize("path", ["wres32", "thin32", "generic"])
+def test_conv_thin32_layers(cuda, tune, dtype, N, H, W, mode, path):
+    """32 → 32-channel layers (StyleGAN2 1024² StyledConvs) on the LDS-halo weights-resident
+    kernel (conv_wres.hip conv_wres32_kernel, the default), the global-gather kernel
+    (conv_thin.hip conv_thin32_kernel: MIA_CONV_WRES32=0) and the implicit-GEMM tile (both 0):
+    modulated forward with demod / noise / bias / lrelu·√2, the input gradient with the
+    style-gradient sdot (4 × 256² exercises long persistent runs across images), plain and
+    accumulating, against torch fp64."""
+    tune("MIA_CONV_WRES32", path == "wres32")
+    tune("MIA_CONV_THIN32", path != "generic")
     C = 32
     g = torch.Generator().manual_seed(N * 31 + H + W + len(mode))
     x = torch.randn(N, C, H, W, generator=g)
@@ -877,6 +879,78 @@ def test_conv_thin32_layers(cuda, tune, dtype, N, H, W, mode, thin):
     assert rel_err(nchw(y), ref) < 2 * TOL[dtype]
     if sd is not None:
         assert rel_err(sd, sd_ref) < 2 * TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,H,W", [(2, 32, 48), (3, 16, 16), (5, 64, 32)])
+@pytest.mark.parametrize("mode", ["mod", "mod_lrelu_in", "sdot", "sdot_acc", "sdot_bab",
+                                  "sdot_acc_bab", "plain", "acc"])
+def test_conv_wres32_matches_thin32(cuda, tune, dtype, N, H, W, mode):
+    """The LDS-halo 32-channel kernel (conv_wres32_kernel) against the global-gather one
+    (conv_thin32_kernel): same weights in VGPRs, same modulate<T> rounding of act(x)·s (once per
+    halo in LDS vs per fragment read), the same 9 MFMAs per fragment in tap order and the same
+    epilogue source, so the outputs agree to the epilogue's last rounding; the sdot / q sums are
+    the same terms in a different order (per-patch LDS pre-reduction + ordered slots vs per-wave
+    runs): ≤ 1e-5 relative. 5 × 64×32 puts patch runs across image boundaries; plus the 'mod'
+    forward against fp64 on the same rounded operands."""
+    g = torch.Generator().manual_seed(N * 7 + H + W + len(mode) + (dtype == torch.bfloat16))
+    C = 32
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
+    y0 = torch.randn(N, C, H, W, generator=g)
+    b = torch.randn(C, generator=g) * 0.1
+    a = torch.randn(N, C, H, W, generator=g)
+    s = torch.rand(N, C, generator=g) + 0.5
+    d = torch.rand(N, C, generator=g) + 0.5
+    noise = torch.randn(H * W, generator=g)
+    red = mode.startswith("sdot")
+
+    def run():
+        y = nhwc(y0, dtype).to(cuda)
+        sd = torch.zeros(N * C, device=cuda) if red else None
+        q = torch.zeros(N * C, device=cuda) if "bab" in mode else None
+        kw = {}
+        if mode.startswith("mod"):
+            kw = dict(in_scale=s.to(cuda), out_scale=d.to(cuda), noise=noise.to(cuda),
+                      noise_w=0.3, bias=b.to(cuda), act_out=ops.ACT_LRELU_S2)
+            if mode == "mod_lrelu_in":
+                kw["act_in"] = ops.ACT_LRELU_S2
+        elif red:
+            kw = dict(out_scale=s.to(cuda), aux_x=nhwc(a, dtype).to(cuda), sdot=sd,
+                      accumulate="acc" in mode)
+            if q is not None:
+                kw["bab"] = dict(demod=d.to(cuda), noise=noise.to(cuda), noise_w=0.3,
+                                 bias=b.to(cuda), q=q)
+        elif mode == "acc":
+            kw = dict(accumulate=True)
+        ops.conv3x3(nhwc(x, dtype).to(cuda), layouts.fwd_matrix(w, dtype).to(cuda), y, cout=C,
+                    **kw)
+        torch.cuda.synchronize()
+        return y.clone(), sd, q
+
+    tune("MIA_CONV_WRES32", 1)
+    y_w, sd_w, q_w = run()
+    tune("MIA_CONV_WRES32", 0)
+    y_t, sd_t, q_t = run()
+    # the compiler may contract the last fp32 multiply / add of an epilogue chain differently in
+    # the two kernels' schedules (fp16: fused into the conversion, v_fma_mix*; one rounding
+    # instead of two) for a few elements: ≤ 1 ulp of T there (measured ≤ 10 of 10⁵ elements;
+    # most modes bit-identical)
+    ulp = torch.finfo(dtype).eps * y_t.float().abs().clamp_min(2.0 ** -14)
+    dd = (y_w.float() - y_t.float()).abs()
+    assert (dd <= ulp).all(), (mode, dd.max().item())
+    assert (dd > 0).float().mean().item() < 1e-3, mode
+    for u, v in ((sd_w, sd_t), (q_w, q_t)):
+        if u is not None:
+            assert ((u - v).abs().max() / v.abs().max()).item() < 1e-5
+    if mode == "mod":
+        xm = (x.to(dtype).double() * s.to(dtype).double().view(N, C, 1, 1)).to(dtype).double()
+        pre = F.conv2d(xm, w.to(dtype).double(), padding=1) * d.double().view(N, C, 1, 1) \
+            + 0.3 * noise.double().view(1, 1, H, W) + b.double().view(1, C, 1, 1)
+        ref = torch.where(pre > 0, pre, 0.2 * pre) * math.sqrt(2)
+        got = y_w.permute(0, 3, 1, 2).double().cpu()
+        tol = 2e-2 if dtype == torch.float16 else 1e-1
+        assert ((got - ref).abs().max() / ref.abs().max()).item() < tol
 
 
 @pytest.mark.parametrize("off,nbytes", [(0, 4096), (0, 4100), (4, 64), (1, 33), (16, 1 << 20),

@@ -34,7 +34,10 @@ SHAPES = [
     ("dgrad+tap 256² 64→64", 256, 64, 64, "tap"),
     ("dgrad 128² 128→64", 128, 128, 64, "plain"),
     ("mod 1024² 32→32", 1024, 32, 32, "mod"),
+    ("mod 512² 64→64", 512, 64, 64, "mod"),
+    ("dgrad+sdot 512² 64→64", 512, 64, 64, "sdot"),
     ("dgrad+sdot 1024² 32→32", 1024, 32, 32, "sdot"),
+    ("dgrad+bab 1024² 32→32", 1024, 32, 32, "bab"),
     ("up 128²→256² 256→128", 128, 256, 128, "up"),
     ("up 64²→128² 512→256", 64, 512, 256, "up"),
     ("up 32²→64² 512→512", 32, 512, 512, "up"),
@@ -143,6 +146,14 @@ def run(name, H, Cin, Cout, mode, N, iters, dtype, dev):
         kw = dict(out_scale=torch.rand(N, Cout, device=dev, generator=g) + 0.5,
                   aux_x=torch.randn(N, H, H, Cout, device=dev, generator=g).to(dtype),
                   sdot=torch.zeros(N, Cout, device=dev))
+    elif mode == "bab":  # StyledConv input gradient + the layer below's bias-act backward
+        kw = dict(out_scale=torch.rand(N, Cout, device=dev, generator=g) + 0.5,
+                  aux_x=torch.randn(N, H, H, Cout, device=dev, generator=g).to(dtype),
+                  sdot=torch.zeros(N, Cout, device=dev),
+                  bab=dict(demod=torch.rand(N, Cout, device=dev, generator=g) + 0.5,
+                           noise=torch.randn(H * H, device=dev, generator=g), noise_w=0.1,
+                           bias=torch.randn(Cout, device=dev, generator=g),
+                           q=torch.zeros(N, Cout, device=dev)))
     elif mode == "tap":
         a = torch.randn(N, H, H, Cout, device=dev, generator=g).relu().to(dtype)
         kw = dict(tap_a=a, tap_t=torch.randn(N, H, H, Cout, device=dev, generator=g).to(dtype), tap_coef=0.3, mask_a=a)

@@ -187,9 +187,13 @@ static int run_gemm_groups(const mia_gemm_group* groups, int ngroups, hipStream_
   return MIA_OK;
 }
 
-// demod[n][co] = rsqrt(scale2·Σ_ci s²·wsq[co][ci] + 1e-8); one thread per (n, co).
-__global__ void style_demod_kernel(const float* __restrict__ s, const float* __restrict__ wsq,
-                                   float* __restrict__ demod, int Cin, int Cout, float scale2) {
+// demod[n][co] = rsqrt(scale2·Σ_ci s²·wsq[co][ci] + 1e-8). One wave per (n, co): its lanes read
+// the weight row coalesced (ci = lane + 64·k, summed in k order), then a fixed butterfly
+// (wave_sum); 4 output channels per block share the block's s² row in LDS.
+__global__ __launch_bounds__(256) void style_demod_kernel(const float* __restrict__ s,
+                                                          const float* __restrict__ wsq,
+                                                          float* __restrict__ demod, int Cin,
+                                                          int Cout, float scale2) {
   extern __shared__ float s2[];
   const int n = blockIdx.y;
   for (int i = threadIdx.x; i < Cin; i += blockDim.x) {
@@ -197,30 +201,45 @@ __global__ void style_demod_kernel(const float* __restrict__ s, const float* __r
     s2[i] = v * v;
   }
   __syncthreads();
-  const int co = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63, co = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (co >= Cout) return;
   const float* w = wsq + (size_t)co * Cin;
   float acc = 0.f;
-  for (int ci = 0; ci < Cin; ++ci) acc += s2[ci] * w[ci];
-  demod[(size_t)n * Cout + co] = rsqrtf(scale2 * acc + 1e-8f);
+  for (int ci = lane; ci < Cin; ci += 64) acc += s2[ci] * w[ci];
+  acc = wave_sum(acc);
+  if (lane == 0) demod[(size_t)n * Cout + co] = rsqrtf(scale2 * acc + 1e-8f);
 }
 
-// gs[n][ci] += −scale2·s[n][ci]·Σ_co q[n][co]·demod[n][co]²·wsq[co][ci]
-__global__ void demod_bwd_kernel(const float* __restrict__ q, const float* __restrict__ demod,
-                                 const float* __restrict__ wsq, const float* __restrict__ s,
-                                 float* __restrict__ gs, int Cin, int Cout, float scale2) {
-  extern __shared__ float r[];
+// gs[n][ci] += −scale2·s[n][ci]·Σ_co q[n][co]·demod[n][co]²·wsq[co][ci]. A block owns 64 input
+// channels of one image; its 4 waves sum a quarter of the output channels each (rows coalesced
+// over ci), then the quarters are added in order: a fixed order, 4× the parallelism and a quarter
+// of the serial chain of one thread per (n, ci).
+__global__ __launch_bounds__(256) void demod_bwd_kernel(const float* __restrict__ q,
+                                                        const float* __restrict__ demod,
+                                                        const float* __restrict__ wsq,
+                                                        const float* __restrict__ s,
+                                                        float* __restrict__ gs, int Cin, int Cout,
+                                                        float scale2) {
+  extern __shared__ float r[];  // [Cout] q·demod², then [4][64] partial sums
+  float* const part = r + Cout;
   const int n = blockIdx.y;
   for (int i = threadIdx.x; i < Cout; i += blockDim.x) {
     const float d = demod[(size_t)n * Cout + i];
     r[i] = q[(size_t)n * Cout + i] * d * d;
   }
   __syncthreads();
-  const int ci = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ci >= Cin) return;
+  const int lane = threadIdx.x & 63, qtr = threadIdx.x >> 6;
+  const int ci = blockIdx.x * 64 + lane;
+  const int per = (Cout + 3) / 4, c0 = qtr * per, c1 = min(c0 + per, Cout);
   float acc = 0.f;
-  for (int co = 0; co < Cout; ++co) acc += r[co] * wsq[(size_t)co * Cin + ci];
-  gs[(size_t)n * Cin + ci] += -scale2 * s[(size_t)n * Cin + ci] * acc;
+  if (ci < Cin)
+    for (int co = c0; co < c1; ++co) acc += r[co] * wsq[(size_t)co * Cin + ci];
+  part[qtr * 64 + lane] = acc;
+  __syncthreads();
+  if (qtr == 0 && ci < Cin) {
+    const float t = ((part[lane] + part[64 + lane]) + part[128 + lane]) + part[192 + lane];
+    gs[(size_t)n * Cin + ci] += -scale2 * s[(size_t)n * Cin + ci] * t;
+  }
 }
 
 }  // namespace mia
@@ -250,7 +269,7 @@ extern "C" int mia_gemm_f32_grouped(const mia_gemm_group* groups, int ngroups, v
 extern "C" int mia_style_demod(const float* s, const float* wsq, float* demod, int N, int Cin,
                                int Cout, float scale2, void* stream) {
   MIA_CHECK_ARG(s && wsq && demod && N > 0 && Cin > 0 && Cout > 0, "bad args");
-  dim3 grid((Cout + 255) / 256, N);
+  dim3 grid((Cout + 3) / 4, N);
   hipLaunchKernelGGL(style_demod_kernel, grid, dim3(256), Cin * sizeof(float), (hipStream_t)stream,
                      s, wsq, demod, Cin, Cout, scale2);
   return check_launch("style_demod");
@@ -259,8 +278,9 @@ extern "C" int mia_style_demod(const float* s, const float* wsq, float* demod, i
 extern "C" int mia_demod_bwd(const float* q, const float* demod, const float* wsq, const float* s,
                              float* gs, int N, int Cin, int Cout, float scale2, void* stream) {
   MIA_CHECK_ARG(q && demod && wsq && s && gs && N > 0, "bad args");
-  dim3 grid((Cin + 255) / 256, N);
-  hipLaunchKernelGGL(demod_bwd_kernel, grid, dim3(256), Cout * sizeof(float), (hipStream_t)stream,
+  dim3 grid((Cin + 63) / 64, N);
+  hipLaunchKernelGGL(demod_bwd_kernel, grid, dim3(256), (Cout + 256) * sizeof(float),
+                     (hipStream_t)stream,
                      q, demod, wsq, s, gs, Cin, Cout, scale2);
   return check_launch("demod_bwd");
 }

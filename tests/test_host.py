@@ -80,6 +80,25 @@ def test_library_exports_every_header_symbol():
     assert lib.mia_conv_kpad(8, 1) == 128  # host-only helper
 
 
+def test_kernel_variant_switch_table():
+    """mia_set_tuning / mia_get_tuning (host-only, no GPU): the measured-best defaults, a set value
+    read back, and an unknown name rejected with the library's error (include/miattack.h)."""
+    from gfa_amd import _lib
+    defaults = {"MIA_CONV_HALO": 1, "MIA_CONV_X6": 1, "MIA_HALO_EPI": 1, "MIA_CONV_WRES32": 1,
+                "MIA_HALO_C64": 2, "MIA_EPI_PRERED": 1}
+    for name, v in defaults.items():
+        if os.environ.get(name) is None:
+            assert _lib.get_tuning(name) == v, name
+    old = _lib.set_tuning("MIA_CONV_WRES32", 0)
+    try:
+        assert _lib.get_tuning("MIA_CONV_WRES32") == 0
+    finally:
+        _lib.set_tuning("MIA_CONV_WRES32", old)
+    assert _lib.get_tuning("MIA_CONV_WRES32") == old
+    with pytest.raises(_lib.MiaError, match="unknown tuning switch"):
+        _lib.set_tuning("MIA_NO_SUCH_SWITCH", 1)
+
+
 @pytest.mark.parametrize("cname,pyname", [("mia_conv_args", "ConvArgs"),
                                           ("mia_conv_group", "ConvGroup"),
                                           ("mia_conv_batch", "ConvBatch"),

@@ -399,7 +399,27 @@ static int launch_bn(ConvK& k, hipStream_t st) {
   // has ≥ 2 waves of them. Default 128x128: measured faster on every StyleGAN2/VGG shape of the
   // 256² attack step (2 blocks/CU hide each other's DMA waits better than 1 deeper ring).
   const int force = tune(T_CONV_TILE);
-  if (k.a.Cout <= 64) return launch_tile<T, Tile128x64, PRO, SMALLC>(k, st);
+  if (k.a.Cout <= 64) {
+    // the 64-column tile with the specialised register epilogue for the same feature masks as
+    // the 128-column tile below (the 512² StyledConv input gradients and the up-conv adjoints of
+    // the 1024² generator: the LDS-staged generic epilogue with its sums cost ≈ as much as the
+    // tile's short K loop)
+    if constexpr (!PRO) {
+      using namespace epi;
+      switch (reg_epi_mask(k, sizeof(T))) {
+        case OSC | SDOT: return launch_tile<T, Tile128x64, PRO, SMALLC, OSC | SDOT>(k, st);
+        case OSC | SDOT | ACC:
+          return launch_tile<T, Tile128x64, PRO, SMALLC, OSC | SDOT | ACC>(k, st);
+        case OSC | SDOT | BAB:
+          return launch_tile<T, Tile128x64, PRO, SMALLC, OSC | SDOT | BAB>(k, st);
+        case OSC | SDOT | ACC | BAB:
+          return launch_tile<T, Tile128x64, PRO, SMALLC, OSC | SDOT | ACC | BAB>(k, st);
+        case BIAS | PRELU: return launch_tile<T, Tile128x64, PRO, SMALLC, BIAS | PRELU>(k, st);
+        default: break;
+      }
+    }
+    return launch_tile<T, Tile128x64, PRO, SMALLC>(k, st);
+  }
   // Launches with fewer 128x128 tiles than 2 per CU (the e4e style heads at 8²…1² outputs,
   // K = 9·512) run one block per CU and serialise each wave's LDS reads, MFMAs and the step
   // barrier; 64x64 tiles put 4× the blocks (and waves) on the chip. T_CONV_SMALLTILE = the

@@ -538,11 +538,11 @@ bool conv_halo_eligible(const ConvK& k, int dtype) {
   const mia_conv_args& a = k.a;
   const ConvGroup& G = k.g[0];
   const int bk = dtype == MIA_F32 ? 32 : 64;
-  // Cout = 64 (T_HALO_C64: 0 never, 1 always, 2 = the bf16 modulated forward only): measured
-  // +39 % for the bf16 512² StyledConv forward (the generic tile's per-fragment bf16 modulation),
-  // −2 % fp16, −50 % for the input gradient with the sdot sums (r03_wres32_ab.log)
-  const int c64s = tune(T_HALO_C64);
-  const bool c64 = c64s == 1 || (c64s == 2 && dtype == MIA_BF16 && a.in_scale != nullptr);
+  // Cout = 64 on the 64-channel halo tile (T_HALO_C64: 1 = the 2-byte types, default; 0 = never):
+  // with its specialised epilogues and unrolled taps it beats the generic 64-column tile on every
+  // attack shape (512² StyledConv forward bf16 2.69 → 1.39 ms, fp16 1.85 → 1.34, input gradient
+  // + sdot 1.53 → 1.42, 128² 128 → 64 gradient 0.58 → 0.46; profiles/r03_halo_c64_ab.txt)
+  const bool c64 = tune(T_HALO_C64) != 0 && dtype != MIA_F32;
   return k.ng == 1 && k.stride == 1 && G.kh == 3 && G.kw == 3 && G.pad_y == 1 && G.pad_x == 1 &&
          G.ho == a.H && G.wo == a.W && G.ay == 1 && G.ax == 1 && G.by == 0 && G.bx == 0 &&
          !a.shuffle_out && a.H % 16 == 0 && a.W % 16 == 0 && a.Cin % bk == 0 &&
@@ -572,9 +572,9 @@ int launch_conv_halo(ConvK& k, int dtype, hipStream_t st) {
       return pro ? launch_halo_tile<T, Small32, true, false>(k, st)
                  : launch_halo_tile<T, Small32, false, false>(k, st);
     }
-    if (k.a.Cout <= 64)
-      return pro ? launch_halo_tile<T, Small64, true, false>(k, st)
-                 : launch_halo_tile<T, Small64, false, false>(k, st);
+    if (k.a.Cout <= 64)  // (specialised epilogues + unrolled taps, as the 128-channel tile)
+      return pro ? launch_halo_tile<T, Small64, true, true>(k, st)
+                 : launch_halo_tile<T, Small64, false, true>(k, st);
     return pro ? launch_halo_tile<T, Small, true, true>(k, st)
                : launch_halo_tile<T, Small, false, true>(k, st);
   });

@@ -84,7 +84,7 @@ enum TuneKey {
   T_UPCONV_HALO,     // 0: the up-conv forward as 4 sub-pixel phase GEMMs
   T_EPI_PRERED,      // 0: no LDS pre-reduction of the channel sums in the register epilogues
   T_CONV_WRES32,     // 0: the 32 → 32 layers on the global-gather kernel (conv_thin32)
-  T_HALO_C64,        // Cout = 64 on the 64-channel halo tile: 0 never, 1 always, 2 bf16 modulated fwd
+  T_HALO_C64,        // Cout = 64 (2-byte types) on the 64-channel halo tile: 1 (default), 0 never
   T_NKEYS
 };
 int tune(TuneKey key);

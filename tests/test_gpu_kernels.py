@@ -1076,7 +1076,7 @@ def test_x6_halo_variants_bitwise(cuda, tune, C, H, W, mode):
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("C,H,W", [(128, 32, 16), (256, 16, 32)])
+@pytest.mark.parametrize("C,H,W", [(128, 32, 16), (256, 16, 32), (64, 32, 32)])
 @pytest.mark.parametrize("mode", ["plain", "bias_relu", "mask", "tap", "mod", "sdot_bab"])
 def test_halo_lowp_unrolled_bitwise(cuda, tune, dtype, C, H, W, mode):
     """fp16 / bf16 halo kernel (conv_halo.hip): the specialised-epilogue launches run the taps
@@ -1085,6 +1085,8 @@ def test_halo_lowp_unrolled_bitwise(cuda, tune, dtype, C, H, W, mode):
     bit-identical; both within the dtype's tolerance of fp64. 'mod' = the StyledConv forward
     (modulated input, halo modulated once in LDS; demod, noise, bias, LeakyReLU·√2)."""
     g = torch.Generator().manual_seed(C + H + W + len(mode) + (dtype == torch.bfloat16))
+    if C == 64:  # the 64-channel halo tile for every 64-channel launch (default: bf16 forward)
+        tune("MIA_HALO_C64", 1)
     N = 2
     x = torch.randn(N, C, H, W, generator=g)
     w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)

@@ -85,7 +85,7 @@ def test_kernel_variant_switch_table():
     read back, and an unknown name rejected with the library's error (include/miattack.h)."""
     from gfa_amd import _lib
     defaults = {"MIA_CONV_HALO": 1, "MIA_CONV_X6": 1, "MIA_HALO_EPI": 1, "MIA_CONV_WRES32": 1,
-                "MIA_HALO_C64": 2, "MIA_EPI_PRERED": 1}
+                "MIA_HALO_C64": 1, "MIA_EPI_PRERED": 1}
     for name, v in defaults.items():
         if os.environ.get(name) is None:
             assert _lib.get_tuning(name) == v, name

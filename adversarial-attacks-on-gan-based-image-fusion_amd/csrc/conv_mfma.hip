@@ -32,6 +32,7 @@
 // spans. The epilogue stages the fp32 tile through LDS and then works on 8-channel vectors
 // (16-byte loads of every aux operand, 16-byte stores).
 #include "conv_common.h"
+#include <cstdio>
 #include "halo_epilogue.h"
 
 namespace mia {
@@ -359,6 +360,12 @@ static int launch_tile(ConvK& k, hipStream_t st) {
   RedQ r;
   int rc = conv_red_begin(k, r, nslots, st);
   if (rc != MIA_OK) return rc;
+#ifdef MIA_DEBUG_LAUNCH  // diagnostic builds only (make variant): which tile / epilogue a launch takes
+  fprintf(stderr, "MIA_LAUNCH conv_kernel bytes=%d BM=%d BN=%d PRO=%d SMALLC=%d EPI=%d X6B=%d "
+                  "mask=%d N=%d H=%d W=%d Cin=%d Cout=%d stride=%d ng=%d ho=%d wo=%d\n",
+          (int)sizeof(T), TL::BM, TL::BN, (int)PRO, (int)SMALLC, EPI, (int)X6B, epi_mask(k), k.a.N,
+          k.a.H, k.a.W, k.a.Cin, k.a.Cout, k.stride, k.ng, k.g[0].ho, k.g[0].wo);
+#endif
   hipLaunchKernelGGL(fn, dim3(blk), dim3(TL::NT), lds, st, k);
   rc = check_launch("conv");
   return rc != MIA_OK ? rc : red_finish(r, st);
@@ -385,6 +392,9 @@ static int reg_epi_mask(const ConvK& k, int bytes) {
   switch (f) {
     case OSC | SDOT: case OSC | SDOT | ACC: case OSC | SDOT | BAB: case OSC | SDOT | ACC | BAB:
     case BIAS | PRELU:
+    // the e4e encoder's stride-2 body convs and 1×1 shortcuts (folded BN: bias) and the FPN
+    // laterals accumulating onto the up-sampled map
+    case BIAS: case ACC: case BIAS | ACC:
       return f;
     default:
       return -1;
@@ -415,6 +425,9 @@ static int launch_bn(ConvK& k, hipStream_t st) {
         case OSC | SDOT | ACC | BAB:
           return launch_tile<T, Tile128x64, PRO, SMALLC, OSC | SDOT | ACC | BAB>(k, st);
         case BIAS | PRELU: return launch_tile<T, Tile128x64, PRO, SMALLC, BIAS | PRELU>(k, st);
+        case BIAS: return launch_tile<T, Tile128x64, PRO, SMALLC, BIAS>(k, st);
+        case ACC: return launch_tile<T, Tile128x64, PRO, SMALLC, ACC>(k, st);
+        case BIAS | ACC: return launch_tile<T, Tile128x64, PRO, SMALLC, BIAS | ACC>(k, st);
         default: break;
       }
     }
@@ -440,6 +453,9 @@ static int launch_bn(ConvK& k, hipStream_t st) {
       case OSC | SDOT | ACC | BAB:
         return launch_tile<T, Tile128x128, PRO, SMALLC, OSC | SDOT | ACC | BAB>(k, st);
       case BIAS | PRELU: return launch_tile<T, Tile128x128, PRO, SMALLC, BIAS | PRELU>(k, st);
+      case BIAS: return launch_tile<T, Tile128x128, PRO, SMALLC, BIAS>(k, st);
+      case ACC: return launch_tile<T, Tile128x128, PRO, SMALLC, ACC>(k, st);
+      case BIAS | ACC: return launch_tile<T, Tile128x128, PRO, SMALLC, BIAS | ACC>(k, st);
       default: break;
     }
   }
@@ -480,6 +496,9 @@ static int launch_conv(ConvK& k, hipStream_t st) {
         case OSC | SDOT | ACC | BAB:
           return launch_tile<T, Tile128x128, false, false, OSC | SDOT | ACC | BAB, true>(k, st);
         case BIAS | PRELU: return launch_tile<T, Tile128x128, false, false, BIAS | PRELU, true>(k, st);
+        case BIAS: return launch_tile<T, Tile128x128, false, false, BIAS, true>(k, st);
+        case ACC: return launch_tile<T, Tile128x128, false, false, ACC, true>(k, st);
+        case BIAS | ACC: return launch_tile<T, Tile128x128, false, false, BIAS | ACC, true>(k, st);
         default: break;
       }
       return launch_tile<T, Tile128x128, false, false, -2, true>(k, st);

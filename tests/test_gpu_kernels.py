@@ -683,6 +683,49 @@ def test_upconv_halo_fwd(cuda, tune, dtype, N, cin, cout, R, lrelu_in, x6):
     assert rel_err(t1.float(), t2.float()) < 2 * TOL[dtype]
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("C", [64, 128])
+@pytest.mark.parametrize("mode", ["bias", "acc", "bias_acc"])
+def test_generic_tile_register_epilogues_stride2(cuda, tune, dtype, C, mode):
+    """The generic tile's specialised register epilogues for the e4e stride-2 body convs / 1×1
+    shortcuts (folded BN: bias) and the FPN laterals (accumulate, bias + accumulate): 64-column
+    tile at C = 64, 128-column (fp32: X6B split-once B) at C = 128, against fp64 torch, and against
+    the LDS-staged generic epilogue (MIA_CONV_REGEPI=0) of the same tile."""
+    g = torch.Generator().manual_seed(C + len(mode) + (7 if dtype == torch.float16 else 0))
+    N, H = 2, 32
+    ho = H // 2
+    x = torch.randn(N, C, H, H, generator=g)
+    w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
+    b = torch.randn(C, generator=g) * 0.1
+    y0 = torch.randn(N, C, ho, ho, generator=g)
+    xq, wq = x.to(dtype).double(), w.to(dtype).double()
+    kp = ops.conv2d_kpad(9, C, dtype)
+    wm = torch.zeros(C, kp)
+    wm[:, :9 * C] = w.permute(0, 2, 3, 1).reshape(C, 9 * C)
+    grp = [dict(w=wm.to(dtype).to(cuda), kh=3, kw=3, pad=(1, 1), ho=ho, wo=ho)]
+    ref = F.conv2d(xq, wq, stride=2, padding=1)
+    kw = {}
+    if "bias" in mode:
+        ref = ref + b.double().view(1, C, 1, 1)
+        kw["bias"] = b.to(cuda)
+    if "acc" in mode:
+        ref = ref + y0.to(dtype).double()
+        kw["accumulate"] = True
+
+    def run():
+        y = nhwc(y0, dtype).to(cuda)
+        ops.conv2d(nhwc(x, dtype).to(cuda), grp, y, (ho, ho), cout=C, stride=2, **kw)
+        torch.cuda.synchronize()
+        return nchw(y)
+    y_reg = run()
+    tune("MIA_CONV_REGEPI", 0)
+    y_lds = run()
+    tol = 2e-5 if dtype == torch.float32 else 2 * TOL[dtype]
+    assert rel_err(y_reg, ref) < tol
+    assert rel_err(y_lds, ref) < tol
+    assert rel_err(y_reg, y_lds.double()) < tol
+
+
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("N,H,W,C", [(2, 192, 192, 64), (1, 16, 16, 64), (3, 16, 48, 64),
                                      (2, 32, 16, 128)])

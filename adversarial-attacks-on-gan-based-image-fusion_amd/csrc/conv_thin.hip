@@ -449,11 +449,16 @@ __global__ __launch_bounds__(256) void conv_thin_in_f32_kernel(
 // in VGPRs; the segment's 4 pixels × 4 output channels are reduced over the 16 lanes by DPP.
 // Real output channels ≥ 4 (never the case for an RGB image) take a slower path with the weights
 // as wave-uniform scalar loads, one pixel per lane.
-template <bool ACC>
+// LDSW (T_THIN_F32 ≥ 1): the 144 weights a lane needs are read from LDS per tap instead of held in
+// VGPRs (209 → ~80 VGPRs: 2 → 6 waves per SIMD to cover the 2.1 GB gradient read); LDS layout
+// [tap][e][q][co], so the 16 lanes of a group read 256 contiguous bytes (no bank conflict). Same
+// FMA order either way (bit-identical).
+template <bool ACC, bool LDSW>
 __global__ __launch_bounds__(256) void conv_thin_out_f32_kernel(
     const float* __restrict__ g, const float* __restrict__ w, int kpad, float* __restrict__ y,
     int N, int H, int W) {
   constexpr int CIN = 64, COUT = 8, K = 9 * CIN;
+  __shared__ __attribute__((aligned(16))) float wl[LDSW ? 9 * 4 * 16 * 4 : 4];
   __shared__ int cmask_s;
   const int tid = threadIdx.x;
   if (tid == 0) cmask_s = 0;
@@ -497,13 +502,21 @@ __global__ __launch_bounds__(256) void conv_thin_out_f32_kernel(
     return;
   }
   const int q = tid & 15;
-  float wv[9][4][4];  // [tap][input channel 4q + e][output channel]
+  float wv[LDSW ? 1 : 9][4][4];  // [tap][input channel 4q + e][output channel]
+  if constexpr (LDSW) {
+    for (int i = tid; i < 9 * 4 * 16 * 4; i += 256) {  // i = ((t·4 + e)·16 + q')·4 + co
+      const int co = i & 3, qq = (i >> 2) & 15, te = i >> 6, t = te >> 2, e = te & 3;
+      wl[i] = w[(size_t)co * kpad + t * CIN + 4 * qq + e];
+    }
+    __syncthreads();
+  } else {
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+    for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
+      for (int e = 0; e < 4; ++e)
 #pragma unroll
-      for (int co = 0; co < 4; ++co) wv[t][e][co] = w[(size_t)co * kpad + t * CIN + 4 * q + e];
+        for (int co = 0; co < 4; ++co) wv[t][e][co] = w[(size_t)co * kpad + t * CIN + 4 * q + e];
+  }
   const int64_t nseg = (int64_t)N * H * (W / 4);
   for (int64_t seg = (int64_t)blockIdx.x * 16 + (tid >> 4); seg < nseg;
        seg += (int64_t)gridDim.x * 16) {
@@ -527,14 +540,29 @@ __global__ __launch_bounds__(256) void conv_thin_out_f32_kernel(
                    : f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
-      for (int tx = 0; tx < 3; ++tx)
+      for (int tx = 0; tx < 3; ++tx) {
+        f32x4 wt[4];  // this tap's weights [e][co]
+        if constexpr (LDSW) {
+          // an opaque lane offset per tap keeps the reads inside the segment loop (hoisted out of
+          // it they would be the 144 VGPRs again)
+          int off = (((3 * ty + tx) * 4) * 16 + q) * 4;
+          asm volatile("" : "+v"(off));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) wt[e] = *(const f32x4*)(wl + off + e * 64);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            wt[e] = f32x4{wv[3 * ty + tx][e][0], wv[3 * ty + tx][e][1], wv[3 * ty + tx][e][2],
+                          wv[3 * ty + tx][e][3]};
+        }
 #pragma unroll
         for (int p = 0; p < 4; ++p)
 #pragma unroll
           for (int e = 0; e < 4; ++e)
 #pragma unroll
             for (int co = 0; co < 4; ++co)
-              acc[p][co] = fmaf(gr[p + tx][e], wv[3 * ty + tx][e][co], acc[p][co]);
+              acc[p][co] = fmaf(gr[p + tx][e], wt[e][co], acc[p][co]);
+      }
     }
     // lanes 2p, 2p + 1 of the group write pixel p's channels 0–3 / 4–7 (zero, or unchanged)
     f32x4 o = {0.f, 0.f, 0.f, 0.f};
@@ -648,18 +676,34 @@ int launch_conv_thin(ConvK& k, int dtype, hipStream_t st) {
   const int grid = grid_for((int64_t)a.N * a.H * (a.W / 16));  // ≤ 8 waves per SIMD
   if (dtype == MIA_F32) {  // the fp32 VALU kernels (one pixel per thread / per 16 threads)
     const int64_t npix = (int64_t)a.N * a.H * a.W;
+    // T_THIN_F32: 0 = the round-2 launches (8 waves per CU, gradient weights in VGPRs); 1 =
+    // 16 waves per CU for the forward (112 VGPRs: 4 per SIMD fit), LDS weights + 20 waves per CU (82 VGPRs: 5 per SIMD)
+    // for the gradient
+    const int mode = tune(T_THIN_F32);
+    const int wpc_in = mode ? 16 : 8, wpc_out = mode ? 20 : 8;
+    const int grid_out = grid_for(npix / 16, wpc_out);
     if (a.Cin == 8) {
-      hipLaunchKernelGGL(conv_thin_in_f32_kernel, dim3(grid_for(npix / 16, 8)), dim3(256), 0, st,
+      hipLaunchKernelGGL(conv_thin_in_f32_kernel, dim3(grid_for(npix / 16, wpc_in)), dim3(256), 0, st,
                          (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, a.bias,
                          a.act_out, a.act_slope, (float*)a.y, a.N, a.H, a.W);
     } else if (a.accumulate) {
-      hipLaunchKernelGGL(conv_thin_out_f32_kernel<true>, dim3(grid_for(npix / 16, 8)), dim3(256), 0,
-                         st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
-                         a.N, a.H, a.W);
+      if (mode)
+        hipLaunchKernelGGL((conv_thin_out_f32_kernel<true, true>), dim3(grid_out), dim3(256), 0, st,
+                           (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
+                           a.N, a.H, a.W);
+      else
+        hipLaunchKernelGGL((conv_thin_out_f32_kernel<true, false>), dim3(grid_out), dim3(256), 0,
+                           st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
+                           a.N, a.H, a.W);
     } else {
-      hipLaunchKernelGGL(conv_thin_out_f32_kernel<false>, dim3(grid_for(npix / 16, 8)), dim3(256), 0,
-                         st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
-                         a.N, a.H, a.W);
+      if (mode)
+        hipLaunchKernelGGL((conv_thin_out_f32_kernel<false, true>), dim3(grid_out), dim3(256), 0,
+                           st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
+                           a.N, a.H, a.W);
+      else
+        hipLaunchKernelGGL((conv_thin_out_f32_kernel<false, false>), dim3(grid_out), dim3(256), 0,
+                           st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
+                           a.N, a.H, a.W);
     }
     return check_launch("conv_thin_f32");
   }

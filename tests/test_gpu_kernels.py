@@ -645,6 +645,36 @@ def test_conv_thin_vgg_input_layer(cuda, tune, dtype, N, H, W, thin, e4e):
     assert rel_err(nchw(gx), gx_ref) < 2 * TOL[dtype]
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 17, 16), (9, 256, 256)])
+def test_conv_thin_f32_launch_modes_bitwise(cuda, tune, N, H, W):
+    """The fp32 VALU thin kernels' launch modes (MIA_THIN_F32: 1 = 16 / 20 waves per CU with the
+    gradient weights in LDS, 0 = the round-2 launches) run the same FMAs in the same order: the
+    forward, the plain gradient and the accumulating gradient are bit-identical."""
+    g = torch.Generator().manual_seed(7 * N + H + W)
+    x = torch.zeros(N, 8, H, W)
+    x[:, :3] = torch.rand(N, 3, H, W, generator=g) * 2 - 1
+    w = torch.randn(64, 3, 3, 3, generator=g) / math.sqrt(27)
+    b = torch.randn(64, generator=g) * 0.1
+    gout = torch.randn(N, 64, H, W, generator=g)
+    base = torch.randn(N, H, W, 8, generator=g).to(cuda)
+    xin, gin = nhwc(x, torch.float32).to(cuda), nhwc(gout, torch.float32).to(cuda)
+    wf = layouts.fwd_matrix(w, torch.float32, cin_pad=8).to(cuda)
+    wd = layouts.dgrad_matrix(w, torch.float32, cin_pad=8).to(cuda)
+    outs = []
+    for mode in ("0", "1"):
+        tune("MIA_THIN_F32", mode)
+        y = torch.empty(N, H, W, 64, device=cuda)
+        ops.conv3x3(xin, wf, y, cout=64, bias=b.to(cuda), act_out=ops.ACT_RELU)
+        gx = torch.empty(N, H, W, 8, device=cuda)
+        ops.conv3x3(gin, wd, gx, cout=8)
+        ga = base.clone()
+        ops.conv3x3(gin, wd, ga, cout=8, accumulate=True)
+        torch.cuda.synchronize()
+        outs.append((y, gx, ga))
+    for a, b_ in zip(*outs):
+        assert torch.equal(a, b_)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("N,cin,cout,R", [(2, 64, 64, 16), (1, 128, 192, 32), (2, 256, 128, 16),
                                           (1, 64, 64, 8), (2, 64, 32, 32), (1, 128, 96, 16)])

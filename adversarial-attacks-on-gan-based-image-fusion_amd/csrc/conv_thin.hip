@@ -361,7 +361,9 @@ __device__ __forceinline__ int64_t thin_seg_origin(int64_t seg, int H, int W, in
 // weights are transposed into LDS as [k][64] (one 16-B read per (tap, channel) serves the
 // segment's 4 pixels × 4 channels). CM: the real input channels as a compile-time mask (0x07, the
 // RGB image), or 0xff with the runtime mask cmask.
-template <int CM>
+// HOIST (T_THIN_F32 = 2): the segment's 3 × 6 input pixels are all loaded before the first FMA
+// (one exposed load latency per segment instead of one per tap row); same FMA order.
+template <int CM, bool HOIST>
 __device__ __forceinline__ void thin_in_f32_body(const float* __restrict__ x,
                                                  const float* __restrict__ wl, int cmask,
                                                  const f32x4 bs, const f32x4 sl, int act,
@@ -375,6 +377,21 @@ __device__ __forceinline__ void thin_in_f32_body(const float* __restrict__ x,
     int n, yy, x0;
     const int64_t pix0 = thin_seg_origin(seg, H, W, n, yy, x0);
     f32x4 acc[4] = {bs, bs, bs, bs};
+    f32x4 xh[HOIST ? 3 : 1][6];
+    if constexpr (HOIST) {
+#pragma unroll
+      for (int ty = 0; ty < 3; ++ty) {
+        const int sy = yy + ty - 1;
+        const bool oky = sy >= 0 && sy < H;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          const int sx = x0 + c - 1;
+          const bool ok = oky && sx >= 0 && sx < W;
+          xh[ty][c] = ok ? *(const f32x4*)(x + ((size_t)(n * H + sy) * W + sx) * CIN)
+                         : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
 #pragma unroll
     for (int ty = 0; ty < 3; ++ty) {
       const int sy = yy + ty - 1;
@@ -382,11 +399,15 @@ __device__ __forceinline__ void thin_in_f32_body(const float* __restrict__ x,
       f32x4 xa[6], xb[6];
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
-        const int sx = x0 + c - 1;
-        const bool ok = sx >= 0 && sx < W;
-        const float* xp = x + ((size_t)(n * H + sy) * W + (ok ? sx : 0)) * CIN;
-        xa[c] = ok ? *(const f32x4*)xp : f32x4{0.f, 0.f, 0.f, 0.f};
-        if constexpr (CM >> 4) xb[c] = ok && hi4 ? *(const f32x4*)(xp + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (HOIST) {
+          xa[c] = xh[ty][c];
+        } else {
+          const int sx = x0 + c - 1;
+          const bool ok = sx >= 0 && sx < W;
+          const float* xp = x + ((size_t)(n * H + sy) * W + (ok ? sx : 0)) * CIN;
+          xa[c] = ok ? *(const f32x4*)xp : f32x4{0.f, 0.f, 0.f, 0.f};
+          if constexpr (CM >> 4) xb[c] = ok && hi4 ? *(const f32x4*)(xp + 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
       }
 #pragma unroll
       for (int tx = 0; tx < 3; ++tx)
@@ -416,7 +437,8 @@ __device__ __forceinline__ void thin_in_f32_body(const float* __restrict__ x,
   }
 }
 
-__global__ __launch_bounds__(256) void conv_thin_in_f32_kernel(
+template <bool HOIST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv_thin_in_f32_kernel(
     const float* __restrict__ x, const float* __restrict__ w, int kpad,
     const float* __restrict__ bias, int act, const float* __restrict__ slope,
     float* __restrict__ y, int N, int H, int W) {
@@ -440,8 +462,11 @@ __global__ __launch_bounds__(256) void conv_thin_in_f32_kernel(
   f32x4 bs = {0.f, 0.f, 0.f, 0.f}, sl = {0.f, 0.f, 0.f, 0.f};
   if (bias) bs = *(const f32x4*)(bias + c0);
   if (act == MIA_ACT_PRELU) sl = *(const f32x4*)(slope + c0);
-  if (cmask == 0x07) thin_in_f32_body<0x07>(x, wl, cmask, bs, sl, act, y, N, H, W);
-  else thin_in_f32_body<0xff>(x, wl, cmask, bs, sl, act, y, N, H, W);
+  if (cmask == 0x07) {
+    thin_in_f32_body<0x07, HOIST>(x, wl, cmask, bs, sl, act, y, N, H, W);
+  } else {
+    thin_in_f32_body<0xff, false>(x, wl, cmask, bs, sl, act, y, N, H, W);
+  }
 }
 
 // input gradient, Cin = 64 → 8 output channels (store or accumulate). Lane q of a group holds
@@ -678,14 +703,20 @@ int launch_conv_thin(ConvK& k, int dtype, hipStream_t st) {
     const int64_t npix = (int64_t)a.N * a.H * a.W;
     // T_THIN_F32: 0 = the round-2 launches (8 waves per CU, gradient weights in VGPRs); 1 =
     // 16 waves per CU for the forward (112 VGPRs: 4 per SIMD fit), LDS weights + 20 waves per CU (82 VGPRs: 5 per SIMD)
-    // for the gradient
+    // for the gradient; 2 = mode 1 with the forward's loads hoisted (thin_in_f32_body HOIST, held
+    // to 128 VGPRs: 16 waves per CU)
     const int mode = tune(T_THIN_F32);
     const int wpc_in = mode ? 16 : 8, wpc_out = mode ? 20 : 8;
     const int grid_out = grid_for(npix / 16, wpc_out);
     if (a.Cin == 8) {
-      hipLaunchKernelGGL(conv_thin_in_f32_kernel, dim3(grid_for(npix / 16, wpc_in)), dim3(256), 0, st,
-                         (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, a.bias,
-                         a.act_out, a.act_slope, (float*)a.y, a.N, a.H, a.W);
+      if (mode == 2)
+        hipLaunchKernelGGL(conv_thin_in_f32_kernel<true>, dim3(grid_for(npix / 16, 16)), dim3(256),
+                           0, st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, a.bias,
+                           a.act_out, a.act_slope, (float*)a.y, a.N, a.H, a.W);
+      else
+        hipLaunchKernelGGL(conv_thin_in_f32_kernel<false>, dim3(grid_for(npix / 16, wpc_in)),
+                           dim3(256), 0, st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad,
+                           a.bias, a.act_out, a.act_slope, (float*)a.y, a.N, a.H, a.W);
     } else if (a.accumulate) {
       if (mode)
         hipLaunchKernelGGL((conv_thin_out_f32_kernel<true, true>), dim3(grid_out), dim3(256), 0, st,

@@ -647,9 +647,10 @@ def test_conv_thin_vgg_input_layer(cuda, tune, dtype, N, H, W, thin, e4e):
 
 @pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 17, 16), (9, 256, 256)])
 def test_conv_thin_f32_launch_modes_bitwise(cuda, tune, N, H, W):
-    """The fp32 VALU thin kernels' launch modes (MIA_THIN_F32: 1 = 16 / 20 waves per CU with the
-    gradient weights in LDS, 0 = the round-2 launches) run the same FMAs in the same order: the
-    forward, the plain gradient and the accumulating gradient are bit-identical."""
+    """The fp32 VALU thin kernels' launch modes (MIA_THIN_F32: 2 = mode 1 with the forward's input
+    loads hoisted, 1 = 16 / 20 waves per CU with the gradient weights in LDS, 0 = the round-2
+    launches) run the same FMAs in the same order: the forward, the plain gradient and the
+    accumulating gradient are bit-identical."""
     g = torch.Generator().manual_seed(7 * N + H + W)
     x = torch.zeros(N, 8, H, W)
     x[:, :3] = torch.rand(N, 3, H, W, generator=g) * 2 - 1
@@ -661,7 +662,7 @@ def test_conv_thin_f32_launch_modes_bitwise(cuda, tune, N, H, W):
     wf = layouts.fwd_matrix(w, torch.float32, cin_pad=8).to(cuda)
     wd = layouts.dgrad_matrix(w, torch.float32, cin_pad=8).to(cuda)
     outs = []
-    for mode in ("0", "1"):
+    for mode in ("0", "1", "2"):
         tune("MIA_THIN_F32", mode)
         y = torch.empty(N, H, W, 64, device=cuda)
         ops.conv3x3(xin, wf, y, cout=64, bias=b.to(cuda), act_out=ops.ACT_RELU)
@@ -671,8 +672,9 @@ def test_conv_thin_f32_launch_modes_bitwise(cuda, tune, N, H, W):
         ops.conv3x3(gin, wd, ga, cout=8, accumulate=True)
         torch.cuda.synchronize()
         outs.append((y, gx, ga))
-    for a, b_ in zip(*outs):
-        assert torch.equal(a, b_)
+    for other in outs[1:]:
+        for a, b_ in zip(outs[0], other):
+            assert torch.equal(a, b_)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])

@@ -30,6 +30,10 @@ SHAPES = [
     ("dgrad+tap 64² 256→256", 64, 256, 256, "tap"),
     ("thin vgg1_1 256² 8→64", 256, 8, 64, "vgg"),
     ("thin dgrad 256² 64→8", 256, 64, 8, "plain"),
+    # the attack's thin layers: an RGB image padded to 8 channels (3 real, zero weights elsewhere)
+    ("thin rgb vgg1_1 256² 8→64", 256, 8, 64, "rgb"),
+    ("thin rgb dgrad 256² 64→8", 256, 64, 8, "rgb"),
+    ("thin rgb dgrad+acc 256² 64→8", 256, 64, 8, "rgbacc"),
     ("vgg 256² 64→64", 256, 64, 64, "vgg"),
     ("dgrad+tap 256² 64→64", 256, 64, 64, "tap"),
     ("dgrad 128² 128→64", 128, 128, 64, "plain"),
@@ -142,6 +146,14 @@ def run(name, H, Cin, Cout, mode, N, iters, dtype, dev):
                   bias=torch.randn(Cout, device=dev, generator=g), act_out=ops.ACT_LRELU_S2)
     elif mode == "vgg":
         kw = dict(bias=torch.randn(Cout, device=dev, generator=g), act_out=ops.ACT_RELU)
+    elif mode in ("rgb", "rgbacc"):
+        if Cin == 8:  # forward: K = tap·8 + ci, channels ≥ 3 padded
+            w.view(Cout, -1)[:, :72].view(Cout, 9, 8)[:, :, 3:] = 0
+            x[..., 3:] = 0
+            kw = dict(bias=torch.randn(Cout, device=dev, generator=g), act_out=ops.ACT_RELU)
+        else:  # input gradient: output channels ≥ 3 padded
+            w[3:] = 0
+            kw = dict(accumulate=mode == "rgbacc")
     elif mode == "sdot":
         kw = dict(out_scale=torch.rand(N, Cout, device=dev, generator=g) + 0.5,
                   aux_x=torch.randn(N, H, H, Cout, device=dev, generator=g).to(dtype),

@@ -481,7 +481,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 template <bool ACC, bool LDSW>
 __global__ __launch_bounds__(256) void conv_thin_out_f32_kernel(
     const float* __restrict__ g, const float* __restrict__ w, int kpad, float* __restrict__ y,
-    int N, int H, int W) {
+    int N, int H, int W, int gen_blocks) {
   constexpr int CIN = 64, COUT = 8, K = 9 * CIN;
   __shared__ __attribute__((aligned(16))) float wl[LDSW ? 9 * 4 * 16 * 4 : 4];
   __shared__ int cmask_s;
@@ -498,8 +498,11 @@ __global__ __launch_bounds__(256) void conv_thin_out_f32_kernel(
   const int cmask = __builtin_amdgcn_readfirstlane(cmask_s);
   if (cmask >> 4) {  // general path
     const int64_t npix = (int64_t)N * H * W;
+    // one pixel per thread, each reading whole 256-B records: past gen_blocks blocks the extra
+    // waves only thrash L1 / TA (mode-1 grid: 3.5x slower), so the rest of the grid exits
+    if ((int)blockIdx.x >= gen_blocks) return;
     for (int64_t pix = (int64_t)blockIdx.x * 256 + tid; pix < npix;
-         pix += (int64_t)gridDim.x * 256) {
+         pix += (int64_t)gen_blocks * 256) {
       const int n = (int)(pix / ((int64_t)H * W));
       const int rem = (int)(pix - (int64_t)n * H * W);
       const int yy = rem / W, xx = rem - (rem / W) * W;
@@ -708,6 +711,7 @@ int launch_conv_thin(ConvK& k, int dtype, hipStream_t st) {
     const int mode = tune(T_THIN_F32);
     const int wpc_in = mode ? 16 : 8, wpc_out = mode ? 20 : 8;
     const int grid_out = grid_for(npix / 16, wpc_out);
+    const int gen_blocks = std::min(grid_out, grid_for(npix / 16, 8));  // the general path's grid
     if (a.Cin == 8) {
       if (mode == 2)
         hipLaunchKernelGGL(conv_thin_in_f32_kernel<true>, dim3(grid_for(npix / 16, 16)), dim3(256),
@@ -721,20 +725,20 @@ int launch_conv_thin(ConvK& k, int dtype, hipStream_t st) {
       if (mode)
         hipLaunchKernelGGL((conv_thin_out_f32_kernel<true, true>), dim3(grid_out), dim3(256), 0, st,
                            (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
-                           a.N, a.H, a.W);
+                           a.N, a.H, a.W, gen_blocks);
       else
         hipLaunchKernelGGL((conv_thin_out_f32_kernel<true, false>), dim3(grid_out), dim3(256), 0,
                            st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
-                           a.N, a.H, a.W);
+                           a.N, a.H, a.W, gen_blocks);
     } else {
       if (mode)
         hipLaunchKernelGGL((conv_thin_out_f32_kernel<false, true>), dim3(grid_out), dim3(256), 0,
                            st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
-                           a.N, a.H, a.W);
+                           a.N, a.H, a.W, gen_blocks);
       else
         hipLaunchKernelGGL((conv_thin_out_f32_kernel<false, false>), dim3(grid_out), dim3(256), 0,
                            st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
-                           a.N, a.H, a.W);
+                           a.N, a.H, a.W, gen_blocks);
     }
     return check_launch("conv_thin_f32");
   }

@@ -646,15 +646,17 @@ def test_conv_thin_vgg_input_layer(cuda, tune, dtype, N, H, W, thin, e4e):
 
 
 @pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 17, 16), (9, 256, 256)])
-def test_conv_thin_f32_launch_modes_bitwise(cuda, tune, N, H, W):
+@pytest.mark.parametrize("creal", [3, 8])
+def test_conv_thin_f32_launch_modes_bitwise(cuda, tune, N, H, W, creal):
     """The fp32 VALU thin kernels' launch modes (MIA_THIN_F32: 2 = mode 1 with the forward's input
     loads hoisted, 1 = 16 / 20 waves per CU with the gradient weights in LDS, 0 = the round-2
     launches) run the same FMAs in the same order: the forward, the plain gradient and the
-    accumulating gradient are bit-identical."""
+    accumulating gradient are bit-identical. creal = 8: every padded channel real (the general
+    gradient path, one pixel per thread)."""
     g = torch.Generator().manual_seed(7 * N + H + W)
     x = torch.zeros(N, 8, H, W)
-    x[:, :3] = torch.rand(N, 3, H, W, generator=g) * 2 - 1
-    w = torch.randn(64, 3, 3, 3, generator=g) / math.sqrt(27)
+    x[:, :creal] = torch.rand(N, creal, H, W, generator=g) * 2 - 1
+    w = torch.randn(64, creal, 3, 3, generator=g) / math.sqrt(9 * creal)
     b = torch.randn(64, generator=g) * 0.1
     gout = torch.randn(N, 64, H, W, generator=g)
     base = torch.randn(N, H, W, 8, generator=g).to(cuda)

@@ -15,6 +15,8 @@
 //     (v_permlane16_swap) so every lane writes 8 consecutive channels with one 16-B store;
 //   * the gradient kernel stages each input pixel once per wave work item in LDS (9 taps read it);
 //   * waves stride over the pixel groups / work items.
+#include <type_traits>
+
 #include "conv_common.h"
 #include "halo_epilogue.h"
 
@@ -478,7 +480,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 // VGPRs (209 → ~80 VGPRs: 2 → 6 waves per SIMD to cover the 2.1 GB gradient read); LDS layout
 // [tap][e][q][co], so the 16 lanes of a group read 256 contiguous bytes (no bank conflict). Same
 // FMA order either way (bit-identical).
-template <bool ACC, bool LDSW>
+// STRIP (T_THIN_F32 = 3, with LDSW): sliding-window row strips (below); the grid-strided
+// 4-pixel segments re-read each input row for 3 output rows from L2 / HBM (rocprof: 5.5 GB
+// fetched per 2.15 GB gradient).
+constexpr int THIN_STRIP = 16;
+template <bool ACC, bool LDSW, bool STRIP = false>
 __global__ __launch_bounds__(256) void conv_thin_out_f32_kernel(
     const float* __restrict__ g, const float* __restrict__ w, int kpad, float* __restrict__ y,
     int N, int H, int W, int gen_blocks) {
@@ -544,6 +550,92 @@ __global__ __launch_bounds__(256) void conv_thin_out_f32_kernel(
       for (int e = 0; e < 4; ++e)
 #pragma unroll
         for (int co = 0; co < 4; ++co) wv[t][e][co] = w[(size_t)co * kpad + t * CIN + 4 * q + e];
+  }
+  if constexpr (STRIP) {
+    // a 16-lane group walks THIN_STRIP output rows of one 4-pixel column segment with a sliding
+    // window of 3 input rows in VGPRs: one new input row (6 pixel records) per output row instead
+    // of 3. The 16 groups of a block take 16 adjacent segments of the same strip. Per output
+    // pixel the FMAs run in the same order as the segment loop below (bit-identical).
+    const int spr = W / 4, nsy = (H + THIN_STRIP - 1) / THIN_STRIP;
+    const int64_t nitems = (int64_t)N * nsy * spr;
+    auto load_row = [&](int n, int sy, int x0, f32x4 (&dst)[6]) __attribute__((always_inline)) {
+      const bool oky = sy >= 0 && sy < H;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const int sx = x0 + c - 1;
+        const bool ok = oky && sx >= 0 && sx < W;
+        dst[c] = ok ? *(const f32x4*)(g + ((size_t)(n * H + sy) * W + sx) * CIN + 4 * q)
+                    : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    };
+    // NCO = 3 when output channel 3 is padding too (cmask 0x07, an RGB image): its FMAs are
+    // skipped and it stores +0, what the four-channel form computes from zero weights
+    auto strip = [&](auto nco_c) __attribute__((always_inline)) {
+    constexpr int NCO = decltype(nco_c)::value;
+    for (int64_t it = (int64_t)blockIdx.x * 16 + (tid >> 4); it < nitems;
+         it += (int64_t)gridDim.x * 16) {
+      const int xs = (int)(it % spr);
+      const int64_t r = it / spr;
+      const int n = (int)(r / nsy), y0 = (int)(r - (int64_t)n * nsy) * THIN_STRIP;
+      const int x0 = xs * 4, y1 = min(y0 + THIN_STRIP, H);
+      f32x4 win[3][6];
+      load_row(n, y0 - 1, x0, win[0]);
+      load_row(n, y0, x0, win[1]);
+      for (int yy = y0; yy < y1; ++yy) {
+        load_row(n, yy + 1, x0, win[2]);
+        float acc[4][4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+          for (int co = 0; co < 4; ++co) acc[p][co] = 0.f;
+#pragma unroll
+        for (int ty = 0; ty < 3; ++ty) {
+          const int sy = yy + ty - 1;
+          if (sy < 0 || sy >= H) continue;
+#pragma unroll
+          for (int tx = 0; tx < 3; ++tx) {
+            f32x4 wt[4];
+            int off = (((3 * ty + tx) * 4) * 16 + q) * 4;
+            asm volatile("" : "+v"(off));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) wt[e] = *(const f32x4*)(wl + off + e * 64);
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+#pragma unroll
+                for (int co = 0; co < NCO; ++co)
+                  acc[p][co] = fmaf(win[ty][p + tx][e], wt[e][co], acc[p][co]);
+          }
+        }
+        f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+          for (int co = 0; co < NCO; ++co) {
+            const float sm = row16_sum(acc[p][co]);
+            if (q == 2 * p) o[co] = sm;
+          }
+        if (q < 8) {
+          float* yp = y + ((size_t)(n * H + yy) * W + x0 + (q >> 1)) * COUT + 4 * (q & 1);
+          if constexpr (ACC) {
+            const f32x4 a = *(const f32x4*)yp;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] += a[e];
+          }
+          *(f32x4*)yp = o;
+        }
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          win[0][c] = win[1][c];
+          win[1][c] = win[2][c];
+        }
+      }
+    }
+    };
+    if (cmask == 0x07) strip(std::integral_constant<int, 3>{});
+    else strip(std::integral_constant<int, 4>{});
+    return;
   }
   const int64_t nseg = (int64_t)N * H * (W / 4);
   for (int64_t seg = (int64_t)blockIdx.x * 16 + (tid >> 4); seg < nseg;
@@ -707,13 +799,13 @@ int launch_conv_thin(ConvK& k, int dtype, hipStream_t st) {
     // T_THIN_F32: 0 = the round-2 launches (8 waves per CU, gradient weights in VGPRs); 1 =
     // 16 waves per CU for the forward (112 VGPRs: 4 per SIMD fit), LDS weights + 20 waves per CU (82 VGPRs: 5 per SIMD)
     // for the gradient; 2 = mode 1 with the forward's loads hoisted (thin_in_f32_body HOIST, held
-    // to 128 VGPRs: 16 waves per CU)
+    // to 128 VGPRs: 16 waves per CU); 3 = mode 2 with the gradient's sliding-window row strips
     const int mode = tune(T_THIN_F32);
     const int wpc_in = mode ? 16 : 8, wpc_out = mode ? 20 : 8;
-    const int grid_out = grid_for(npix / 16, wpc_out);
+    const int grid_out = grid_for(npix / 16, mode == 3 ? 12 : wpc_out);  // 3: 144 VGPRs
     const int gen_blocks = std::min(grid_out, grid_for(npix / 16, 8));  // the general path's grid
     if (a.Cin == 8) {
-      if (mode == 2)
+      if (mode >= 2)
         hipLaunchKernelGGL(conv_thin_in_f32_kernel<true>, dim3(grid_for(npix / 16, 16)), dim3(256),
                            0, st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, a.bias,
                            a.act_out, a.act_slope, (float*)a.y, a.N, a.H, a.W);
@@ -722,7 +814,11 @@ int launch_conv_thin(ConvK& k, int dtype, hipStream_t st) {
                            dim3(256), 0, st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad,
                            a.bias, a.act_out, a.act_slope, (float*)a.y, a.N, a.H, a.W);
     } else if (a.accumulate) {
-      if (mode)
+      if (mode == 3)
+        hipLaunchKernelGGL((conv_thin_out_f32_kernel<true, true, true>), dim3(grid_out), dim3(256),
+                           0, st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad,
+                           (float*)a.y, a.N, a.H, a.W, gen_blocks);
+      else if (mode)
         hipLaunchKernelGGL((conv_thin_out_f32_kernel<true, true>), dim3(grid_out), dim3(256), 0, st,
                            (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
                            a.N, a.H, a.W, gen_blocks);
@@ -731,7 +827,11 @@ int launch_conv_thin(ConvK& k, int dtype, hipStream_t st) {
                            st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
                            a.N, a.H, a.W, gen_blocks);
     } else {
-      if (mode)
+      if (mode == 3)
+        hipLaunchKernelGGL((conv_thin_out_f32_kernel<false, true, true>), dim3(grid_out), dim3(256),
+                           0, st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad,
+                           (float*)a.y, a.N, a.H, a.W, gen_blocks);
+      else if (mode)
         hipLaunchKernelGGL((conv_thin_out_f32_kernel<false, true>), dim3(grid_out), dim3(256), 0,
                            st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
                            a.N, a.H, a.W, gen_blocks);

@@ -85,8 +85,9 @@ enum TuneKey {
   T_EPI_PRERED,      // 0: no LDS pre-reduction of the channel sums in the register epilogues
   T_CONV_WRES32,     // 0: the 32 → 32 layers on the global-gather kernel (conv_thin32)
   T_HALO_C64,        // Cout = 64 (2-byte types) on the 64-channel halo tile: 1 (default), 0 never
-  T_THIN_F32,        // fp32 thin layers: 2 (default) hoisted forward loads, 1 more waves + LDS
-                     // gradient weights, 0 round 2 (profiles/r03_thin_f32_ab.txt)
+  T_THIN_F32,        // fp32 thin layers: 3 (default) + sliding-window gradient strips, 2 hoisted
+                     // forward loads, 1 more waves + LDS gradient weights, 0 round 2
+                     // (profiles/r03_thin_f32_ab.txt)
   T_NKEYS
 };
 int tune(TuneKey key);

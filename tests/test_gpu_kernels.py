@@ -648,7 +648,8 @@ def test_conv_thin_vgg_input_layer(cuda, tune, dtype, N, H, W, thin, e4e):
 @pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 17, 16), (9, 256, 256)])
 @pytest.mark.parametrize("creal", [3, 8])
 def test_conv_thin_f32_launch_modes_bitwise(cuda, tune, N, H, W, creal):
-    """The fp32 VALU thin kernels' launch modes (MIA_THIN_F32: 2 = mode 1 with the forward's input
+    """The fp32 VALU thin kernels' launch modes (MIA_THIN_F32: 3 = mode 2 with the gradient's
+    sliding-window row strips, 2 = mode 1 with the forward's input
     loads hoisted, 1 = 16 / 20 waves per CU with the gradient weights in LDS, 0 = the round-2
     launches) run the same FMAs in the same order: the forward, the plain gradient and the
     accumulating gradient are bit-identical. creal = 8: every padded channel real (the general
@@ -664,7 +665,7 @@ def test_conv_thin_f32_launch_modes_bitwise(cuda, tune, N, H, W, creal):
     wf = layouts.fwd_matrix(w, torch.float32, cin_pad=8).to(cuda)
     wd = layouts.dgrad_matrix(w, torch.float32, cin_pad=8).to(cuda)
     outs = []
-    for mode in ("0", "1", "2"):
+    for mode in ("0", "1", "2", "3"):
         tune("MIA_THIN_F32", mode)
         y = torch.empty(N, H, W, 64, device=cuda)
         ops.conv3x3(xin, wf, y, cout=64, bias=b.to(cuda), act_out=ops.ACT_RELU)

@@ -88,7 +88,33 @@ def parse(argv=None):
                     help="e4e = Encoder4Editing(50,'ir_se'), the reference's net.encoder "
                          "(code/utils/model_utils.py:24; default); linear = the SURVEY.md §7 "
                          "stand-in (rounds before the e4e encoder existed)")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: gloo process group on host tensors — only with --engine-factory "
+                         "(tests of the multi-rank leg); the product bench runs on cuda")
+    ap.add_argument("--engine-factory", default=None, help=argparse.SUPPRESS)
     return ap.parse_args(argv)
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_workers(n, argv):
+    """`--gpus N` without a launcher: start the N one-process-per-GPU ranks as ONE child
+    (`python -m torch.distributed.run --nproc-per-node N … bench.py <same args>`) and return its
+    exit code. This process touches no GPU (no HIP call before or after), so nothing is exec'd
+    from an initialised process; the ranks' rank 0 prints the JSON line on the shared stdout."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           os.path.abspath(__file__), *argv]
+    log(f"spawning {n} ranks: {' '.join(cmd[1:6])} …")
+    return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
 
 
 def encoder_weights(kind, size):
@@ -218,12 +244,15 @@ def run_leg(args, dtype, steps, warmup, dev, world, rank, roofline, make_engine=
     gathered = []
 
     def one_step():
+        # world > 1: the fp16 loss-scale decision is taken job-wide (pgd.rescale_consensus), as
+        # in dist.attack_distributed, so no rank is left alone in the all-gather
+        grp = dist.group.WORLD if world > 1 else None
         if args.norm == "l2_cw":
             adv = eng.run_cw(x0, tgt, args.pgd_steps, c=1e-4, lr=0.01,
-                             early_stop=not args.cw_fixed)
+                             early_stop=not args.cw_fixed, group=grp)
             cw_runs.append(eng.cw_steps_run)
         else:
-            adv = eng.run(x0, tgt, args.pgd_steps, eps, alpha)
+            adv = eng.run(x0, tgt, args.pgd_steps, eps, alpha, group=grp)
         if world > 1:
             gathered[:] = [gather_shards(adv, n_total)]
         return adv
@@ -365,30 +394,46 @@ def headline_record(args, r, world, dist_world):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` (no launcher): this process becomes the launcher
+        sys.exit(spawn_workers(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("launch N>1 with torch.distributed.run (one process per GPU)")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (one process per GPU)")
+    make_engine = build_engine
+    if args.engine_factory:
+        import importlib
+        mod, fn = args.engine_factory.split(":")
+        make_engine = getattr(importlib.import_module(mod), fn)
+    elif args.device != "cuda":
+        raise SystemExit("--device cpu needs --engine-factory: the attack engine is HIP-only")
+    if args.device == "cuda":
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    else:
+        dev = torch.device("cpu")
     dist_world = 1
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if dev.type == "cuda":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
         dist_world = dist.get_world_size()
     S = args.size
     r = run_leg(args, args.dtype, args.steps, args.warmup, dev, world, rank,
-                not args.no_roofline)
+                not args.no_roofline, make_engine=make_engine)
     out = headline_record(args, r, world, dist_world)
     if "conv_busy_ms" in r:
         out["roofline"] = roofline_record(args, args.dtype, r)
     if world == 1 and args.lowp != "none" and args.lowp != args.dtype:
         gc.collect()
-        torch.cuda.empty_cache()
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
         lw = max(1, min(args.warmup, 1))
         rl = run_leg(args, args.lowp, args.lowp_steps, lw, dev, world, rank,
-                     not args.no_roofline)
+                     not args.no_roofline, make_engine=make_engine)
         sub = {"note": "reduced-precision run of the same workload; NOT the headline value",
                "dtype": DT_NAME[args.lowp], "value": rl["n_total"] * args.lowp_steps
                / rl["elapsed"], "unit": "attacked images/s", "steps": args.lowp_steps,

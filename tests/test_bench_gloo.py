@@ -2,11 +2,11 @@
 barrier + max-over-ranks clock, the per-step all-gather of the shards (gather_shards, the RCCL
 all_gather_into_tensor on the GPU node) and the JSON record's whole-job fields — the path the
 driver's 8-GPU run takes (BASELINE config #4), which no GPU run of this builder exercises."""
+import json
 import os
 import socket
+import subprocess
 import sys
-import time
-import types
 
 import pytest
 import torch
@@ -24,32 +24,19 @@ def _free_port():
     return p
 
 
-class _StubEngine:
-    """CPU stand-in for pgd.AttackEngine: an elementwise 'attack' with a rank-dependent delay
-    (so the max over ranks is visible) and the flop attributes bench.py reports."""
-
-    def __init__(self, rank):
-        self.rank = rank
-        self.G = types.SimpleNamespace(flops_fwd_per_image=10.0)
-        self.V = types.SimpleNamespace(flops_fwd_per_image=1.0)
-        self.E = types.SimpleNamespace(flops_fwd_per_image=3.0)
-
-    def run(self, x0, t, steps, eps, alpha):
-        time.sleep(0.05 * (1 + self.rank))
-        return torch.clamp(x0 + 2 * eps * torch.sign(t - x0), -1.0, 1.0)
-
-
 def _worker(rank, world, port, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
                       RANK=str(rank))
     sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
     import bench
+    from bench_stub import StubEngine
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         args = bench.parse(["--gpus", str(world), "--steps", "2", "--warmup", "1", "--batch", "3",
                             "--size", "16", "--no-roofline", "--no-cpu-baseline"])
         r = bench.run_leg(args, "fp32", args.steps, args.warmup, torch.device("cpu"), world, rank,
-                          False, make_engine=lambda a, d, dev: _StubEngine(rank))
+                          False, make_engine=lambda a, d, dev: StubEngine(rank))
         out = bench.headline_record(args, r, world, dist.get_world_size())
         out_q.put((rank, out, r["elapsed"]))
     finally:
@@ -78,3 +65,36 @@ def test_bench_multi_rank_leg_gloo_world2():
         assert out["value"] == pytest.approx(6 * 2 / el0)
         assert out["scaling"] == "weak" and out["steps"] == 2 and out["warmup"] == 1
         assert c["algorithmic_gflop_per_image_step"] == pytest.approx((2 * 10 + 4 * 1 + 6) / 1e9)
+
+
+def test_bench_self_spawns_ranks_gloo_world2():
+    """`python bench.py --gpus 2` with no launcher starts the two ranks itself (one
+    torch.distributed.run child; the parent touches no GPU) and exactly ONE JSON line reaches
+    stdout, from rank 0, with the whole-job fields of a world-2 run — the command form the
+    driver's N>1 bench may use."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(ROOT, "tests"), ROOT,
+                                         env.get("PYTHONPATH", "")])
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+           "--engine-factory", "bench_stub:make_engine", "--steps", "2", "--warmup", "1",
+           "--batch", "3", "--size", "16", "--no-roofline", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=240, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    c = out["config"]
+    assert out["n_gpus"] == 2 and c["dist_world_size"] == 2 and c["parallelism"] == "dp2"
+    assert c["global_batch"] == 6 and c["gathered_output_ok"] is True
+    assert out["value"] == pytest.approx(6 * 2 / (out["ms_per_step"] * 2 / 1e3))
+
+
+def test_bench_rejects_world_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240,
+                       cwd=ROOT)
+    assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr

@@ -441,8 +441,9 @@ static int launch_bn(ConvK& k, hipStream_t st) {
   for (int g = 0; g < k.ng; ++g) tiles += (k.g[g].m + 127) / 128;
   tiles *= (k.a.Cout + 127) / 128;
   const int64_t small_below = tune(T_CONV_SMALLTILE);
-  // (2-byte types only: in fp32, the reference-precision path, a small image keeps one tile per
-  // image row block, so its sdot / csum sums stay single-atomic and run-to-run deterministic)
+  // (2-byte types only: fp32's small launches — the e4e style heads — have pre-split weights and
+  // take the X6B 128×128 tile in launch_conv before reaching here; the 64×64 tile has no
+  // pre-split-B form, and on the on-the-fly split it would double the split VALU per MFMA)
   if (sizeof(T) == 2 && tiles < small_below) return launch_tile<T, Tile64x64, PRO, SMALLC>(k, st);
   if constexpr (!SMALLC && !PRO) {
     using namespace epi;

@@ -457,10 +457,9 @@ __device__ __forceinline__ void halo_epilogue_f(
     if (lds_red) {
       // the waves of one channel range meet here; the first wave row sums them (in wave order)
       // and stores one partial per channel for the block (nwm× fewer partials). LDS-only
-      // hand-off: lgkmcnt(0) + s_barrier, no memory fence (a fence would also wait for a
-      // persistent caller's halo DMA in flight)
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-      __builtin_amdgcn_s_barrier();
+      // hand-off: lgkmcnt(0) + s_barrier + a compiler barrier, no memory fence (a fence would
+      // also wait for a persistent caller's halo DMA in flight)
+      lds_handoff();
       if (wm == 0 && px == 0) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) {

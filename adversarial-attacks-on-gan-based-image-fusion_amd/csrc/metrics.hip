@@ -9,7 +9,9 @@
 // The images are NCHW fp32 at the API (the fused / attacked images in [-1, 1]). HBM-bound: every
 // block stages the (32+6)² gray window of the reference and of its image in LDS (one read of the
 // 3 channels each), forms the five window moments by separable row/column sums, and reduces S in
-// fp64 into the per-image sum; a second launch divides by the pixel count.
+// fp64 into its own slot of the per-image tile partials (work[n][tile]); a second launch sums an
+// image's slots in tile order and divides by the pixel count — no atomics, so an image's SSIM is
+// bit-identical run to run and independent of the other images of the call.
 #include "mia_common.h"
 
 namespace mia {
@@ -25,7 +27,7 @@ __device__ __forceinline__ float gray_at(const float* img, int64_t plane, int id
 __global__ __launch_bounds__(256) void ssim_tile_kernel(const float* __restrict__ ref,
                                                         const float* __restrict__ imgs, int H,
                                                         int W, float c1, float c2,
-                                                        double* __restrict__ sums) {
+                                                        double* __restrict__ part) {
   __shared__ float gx[SS_W][SS_W + 1], gy[SS_W][SS_W + 1];
   // row sums over the 7 columns of a window, 5 moments, for the 38 rows × 32 columns
   __shared__ float rs[5][SS_W][SS_T + 1];
@@ -90,18 +92,37 @@ __global__ __launch_bounds__(256) void ssim_tile_kernel(const float* __restrict_
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if ((tid & 63) == 0) red[tid >> 6] = acc;
   __syncthreads();
-  if (tid == 0) atomicAdd(&sums[n], red[0] + red[1] + red[2] + red[3]);
+  const int ntiles = gridDim.x * gridDim.y;
+  if (tid == 0)
+    part[(int64_t)n * ntiles + blockIdx.y * gridDim.x + blockIdx.x] =
+        ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-__global__ void ssim_finish_kernel(const double* __restrict__ sums, float* __restrict__ out, int N,
-                                   double count) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n < N) out[n] = (float)(sums[n] / count);
+// one wave per image: lane l sums tiles l, l+64, … in order, then a fixed butterfly
+__global__ __launch_bounds__(64) void ssim_finish_kernel(const double* __restrict__ part,
+                                                         float* __restrict__ out, int ntiles,
+                                                         double count) {
+  const int n = blockIdx.x, l = threadIdx.x;
+  const double* p = part + (int64_t)n * ntiles;
+  double s = 0.0;
+  for (int k = l; k < ntiles; k += 64) s += p[k];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (l == 0) out[n] = (float)(s / count);
 }
 
 }  // namespace mia
 
 using namespace mia;
+
+static inline int64_t ssim_tiles(int H, int W) {
+  return (int64_t)((W - 2 * SS_R + SS_T - 1) / SS_T) * ((H - 2 * SS_R + SS_T - 1) / SS_T);
+}
+
+extern "C" int64_t mia_ssim_workspace_size(int N, int H, int W) {
+  if (N <= 0 || H < 7 || W < 7) return 0;
+  return (int64_t)N * ssim_tiles(H, W) * (int64_t)sizeof(double);
+}
 
 extern "C" int mia_ssim(const float* ref, const float* imgs, int N, int H, int W, float data_range,
                         double* work, float* ssim_out, void* stream) {
@@ -109,8 +130,6 @@ extern "C" int mia_ssim(const float* ref, const float* imgs, int N, int H, int W
   MIA_CHECK_ARG(H >= 7 && W >= 7, "images smaller than the 7×7 window");
   MIA_CHECK_ARG(data_range > 0.f, "data_range must be > 0");
   hipStream_t st = (hipStream_t)stream;
-  if (hipMemsetAsync(work, 0, sizeof(double) * N, st) != hipSuccess)
-    return set_error("mia_ssim: memset failed");
   const float c1 = (0.01f * data_range) * (0.01f * data_range);
   const float c2 = (0.03f * data_range) * (0.03f * data_range);
   const int iw = W - 2 * SS_R, ih = H - 2 * SS_R;
@@ -118,7 +137,7 @@ extern "C" int mia_ssim(const float* ref, const float* imgs, int N, int H, int W
   hipLaunchKernelGGL(ssim_tile_kernel, grid, dim3(256), 0, st, ref, imgs, H, W, c1, c2, work);
   const int rc = check_launch("ssim_tile_kernel");
   if (rc != MIA_OK) return rc;
-  hipLaunchKernelGGL(ssim_finish_kernel, dim3((N + 255) / 256), dim3(256), 0, st, work, ssim_out,
-                     N, (double)iw * ih);
+  hipLaunchKernelGGL(ssim_finish_kernel, dim3(N), dim3(64), 0, st, work, ssim_out,
+                     (int)ssim_tiles(H, W), (double)iw * ih);
   return check_launch("ssim_finish_kernel");
 }

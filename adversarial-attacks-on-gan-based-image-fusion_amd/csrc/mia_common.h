@@ -44,6 +44,15 @@ __device__ __forceinline__ float lrelu_s2_inv_grad(float pre) {
 // lgkmcnt wait per step, serialised per value).
 #define MIA_DPP(v, ctrl) \
   __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, (v)), (ctrl), 0xf, 0xf, false))
+// LDS-only hand-off between the waves of a block: this wave's LDS accesses retired
+// (lgkmcnt(0)) and the block barrier, WITHOUT the vector-memory fence of __syncthreads() (which
+// would also wait for global loads / LDS-DMA in flight). The asm's "memory" clobber makes it a
+// compiler barrier too: no LDS store is sunk below it and no LDS load hoisted above it
+// (__builtin_amdgcn_s_waitcnt / s_barrier alone do not order the compiler's memory accesses).
+__device__ __forceinline__ void lds_handoff() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ float row16_sum(float v) {
   v += MIA_DPP(v, 0xB1);   // quad_perm [1,0,3,2]: lane ^ 1
   v += MIA_DPP(v, 0x4E);   // quad_perm [2,3,0,1]: lane ^ 2

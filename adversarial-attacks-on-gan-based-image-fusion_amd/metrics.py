@@ -29,7 +29,7 @@ def ssim(ref, imgs, data_range=2.0):
     N, C, H, W = imgs.shape
     if C != 3 or tuple(ref.shape) != (3, H, W):
         raise ValueError("ssim: RGB images of one size expected")
-    work = torch.empty(N, dtype=torch.float64, device=imgs.device)
+    work = torch.empty(ops.ssim_workspace_numel(N, H, W), dtype=torch.float64, device=imgs.device)
     out = torch.empty(N, dtype=torch.float32, device=imgs.device)
     ops.ssim(ref, imgs, data_range, work, out)
     return out

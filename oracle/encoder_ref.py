@@ -21,6 +21,8 @@ import math
 import torch
 import torch.nn.functional as F
 
+from . import forcing
+
 BN_EPS = 1e-5
 # Teacher-forced activation masks (tests only): {key: bool tensor (NCHW)}. Under forced_masks the
 # positive set of a PReLU / LeakyReLU is taken from the given mask instead of the sign of its own
@@ -51,6 +53,7 @@ def _leaky(x, slope, key):
     if m is None:
         return F.prelu(x, slope) if torch.is_tensor(slope) else F.leaky_relu(x, slope)
     s = slope.view(1, -1, 1, 1) if torch.is_tensor(slope) else slope
+    forcing.relu_site("e4e." + key, m, x)
     return torch.where(m.to(x.device), x, s * x)
 E4E_STAGES = [(64, 64, 3), (64, 128, 4), (128, 256, 14), (256, 512, 3)]  # helpers.get_blocks(50)
 COARSE, MIDDLE = 3, 7

@@ -20,6 +20,8 @@ import math
 import torch
 import torch.nn.functional as F
 
+from . import forcing
+
 BLUR_1D = [1.0, 3.0, 3.0, 1.0]
 
 
@@ -107,6 +109,7 @@ def styled_conv(p, prefix, x, w, noise, upsample=False, s=None):
     b = p[prefix + ".activate.bias"].to(x.dtype)
     pre = out + b.view(1, -1, 1, 1)
     if _FORCED is not None and prefix in _FORCED:
+        forcing.relu_site("g." + prefix, _FORCED[prefix], pre)
         return torch.where(_FORCED[prefix], pre, 0.2 * pre) * math.sqrt(2.0)
     return F.leaky_relu(pre, 0.2) * math.sqrt(2.0)
 

@@ -9,6 +9,8 @@ Restates ``code/vgg.py``:
 import torch
 import torch.nn.functional as F
 
+from . import forcing
+
 LAYERS = ["conv1_1", "conv1_2", "conv2_1", "conv2_2", "conv3_1", "conv3_2", "conv3_3",
           "conv4_1", "conv4_2"]
 
@@ -52,11 +54,13 @@ def vgg_forward(params, image):
         w, b = params[name]
         y = F.conv2d(x, w.to(x.dtype), b.to(x.dtype), padding=1)
         if forced is not None:
+            forcing.relu_site("vgg." + name, forced[name], y)
             return torch.where(forced[name], y, torch.zeros_like(y))
         return F.relu(y)
 
     def pool(name, x, ceil_mode=False):
         if forced is not None:  # the forced window maxima: a sum over each window of x·one-hot
+            forcing.pool_site("vgg." + name, forced[name], x, ceil_mode)
             xm = torch.where(forced[name], x, torch.zeros_like(x))
             return F.avg_pool2d(xm, 2, 2, ceil_mode=ceil_mode, divisor_override=1)
         return F.max_pool2d(x, 2, 2, ceil_mode=ceil_mode)

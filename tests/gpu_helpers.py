@@ -115,19 +115,50 @@ class capture_vgg:
         self.V.forward = self._fwd
 
 
+# Forced-branch bound (oracle/forcing.py): every site where the device's branch disagrees with the
+# fp64 oracle's own decision must be a near-tie — |pre| ≤ FLIP_TOL[dtype]·max|pre| of its layer
+# (pools: max − x[forced] ≤ FLIP_TOL·max|x|) — and such sites at most FLIP_FRAC of all sites.
+# fp32: the split arithmetic's ≈ 1e-6 relative activation error (test_fp32_arithmetic_is_fp32_
+# accurate) compounded through the e4e / generator / VGG depth stays well inside 1e-5.
+FLIP_TOL = {torch.float32: 1e-5}
+FLIP_FRAC = 1e-4
+
+
 class forced_all:
     """Oracle context following every branch of the device's most recent gradient pass: e4e
     PReLU / LeakyReLU / SE ReLU, generator LeakyReLU, VGG ReLU and pool argmax (both VGG passes,
-    captured with capture_vgg). ``n``: the first n images only."""
+    captured with capture_vgg). ``n``: the first n images only. ``.audit`` records, per forced
+    site, the branches that disagree with the oracle's own fp64 decision (oracle/forcing.py);
+    ``check()`` bounds them."""
 
     def __init__(self, eng, vgg_cap, n=None):
-        from oracle import encoder_ref, stylegan2_ref, vgg_ref
+        from oracle import encoder_ref, forcing, stylegan2_ref, vgg_ref
         em = e4e_masks(eng.E)
         if n is not None:
             em = {k: v[:n] for k, v in em.items()}
-        self.ctx = [encoder_ref.forced_masks(em),
+        self.audit = forcing.audit()
+        self.dtype = eng.dtype
+        self.ctx = [self.audit, encoder_ref.forced_masks(em),
                     stylegan2_ref.forced_masks(g_masks(eng.G, eng.ws, n)),
                     vgg_ref.forced_masks(vgg_cap.masks[-2:])]
+
+    def report(self):
+        flips, sites, worst, key = self.audit.summary()
+        return (f"forced flips: {flips} of {sites} sites, max |pre| at a flip "
+                f"{worst:.2e} of its layer's max" + (f" ({key})" if key else ""))
+
+    def check(self, tol=None, frac=FLIP_FRAC):
+        """Assert every forced disagreement is a near-tie and that they are rare; returns
+        report()."""
+        tol = FLIP_TOL.get(self.dtype, 1e-5) if tol is None else tol
+        flips, sites, worst, key = self.audit.summary()
+        assert sites > 0, "no forced site was evaluated"
+        bad = [r for r in self.audit.records if r["flips"] and r["rel_gap"] > tol]
+        assert not bad, ("forced branches that are not near-ties: "
+                         + ", ".join(f"{r['key']}: {r['flips']} flips, gap {r['rel_gap']:.2e}"
+                                     for r in bad[:8]))
+        assert flips <= frac * sites, self.report()
+        return self.report()
 
     def __enter__(self):
         for c in self.ctx:

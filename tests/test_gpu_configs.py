@@ -63,8 +63,10 @@ def test_cfg2_pgd10_batch32_fp32(cuda):
         g = eng.full_gradient(x.to(cuda))[:1].cpu().double()
     p64 = to64(params)
     refs = attack_ref.Refs(*p64, x0[:1].double(), t[:1].double(), size)
-    with forced_all(eng, cap, n=1):
+    fa = forced_all(eng, cap, n=1)
+    with fa:
         _, gr = attack_ref.loss_grad(*p64, x[:1].double(), refs, size)
+    print("cfg2 image 0 " + fa.check())
     nrm, mx, agree = grad_stats(g, gr)
     print(f"cfg2 image-0 gradient vs oracle: norm {nrm:.2e} max {mx:.2e} agree {agree:.5f}")
     assert nrm < 1e-4 and agree > 0.9999  # every branch forced: fp32 arithmetic (9.3e-6)

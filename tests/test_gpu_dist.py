@@ -56,4 +56,4 @@ def test_attack_distributed_nccl_world1_equals_attack(cuda, nccl_world1, dtype):
     want = attack(net, x0, 8 / 255, 3, target=t, random_start=True, seed=5, alpha=2 / 255)
     torch.cuda.synchronize()
     assert got.shape == x0.shape and torch.equal(got, want)
-    assert ((got - x0).abs() <= 8 / 255 + 1e-6).all()
+    assert ((got - x0).abs() <= 16 / 255 + 1e-6).all()  # ε in [0,1] units on [-1,1] images

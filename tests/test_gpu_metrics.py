@@ -26,6 +26,11 @@ def test_ssim_kernel_matches_oracle(cuda, N, H, W):
         want = metrics_ref.cal_ssmi(ref.numpy(), imgs[i].numpy())
         assert abs(got[i].item() - want) < 2e-5, (i, got[i].item(), want)
     assert abs(got[0].item() - 1.0) < 1e-5
+    # ordered per-tile partials (no atomics): bit-identical reruns, and an image's SSIM does not
+    # depend on the other images of the call
+    assert torch.equal(metrics.ssim(ref.to(cuda), imgs.to(cuda)).cpu(), got)
+    alone = metrics.ssim(ref.to(cuda), imgs[N - 1:].to(cuda)).cpu()
+    assert torch.equal(alone, got[N - 1:])
 
 
 def test_cal_ssmi_and_cal_result(cuda):

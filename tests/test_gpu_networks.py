@@ -50,6 +50,9 @@ def test_vgg_taps_and_grad_vs_reference_golden(cuda, golden, dtype, tol):
         taps_t = [v.clone() for v in VGGNet.taps(at)]
         a = net.forward(xin, ws, "x")
         taps = VGGNet.taps(a)
+        if dtype == torch.float32 and not full:
+            from gpu_helpers import vgg_masks
+            dev_masks = vgg_masks(a)  # the device forward's ReLU / pool branches
         for name, tp in zip(["conv1_1", "conv1_2", "conv3_2", "conv4_2"], taps):
             got = tp.permute(0, 3, 1, 2).double().cpu()
             assert tuple(got.shape) == tuple(golden[f"{tag}/{name}/shape"])
@@ -79,10 +82,45 @@ def test_vgg_taps_and_grad_vs_reference_golden(cuda, golden, dtype, tol):
             # 36²: no ReLU / pool branch within rounding of a tie here — fp32 arithmetic only
             # (measured norm 3.6e-6, max 4.5e-6)
             assert nrm < 1e-5 and rel_err(got, ref) < 2e-5, (tag, "grad", nrm)
+        elif dtype == torch.float32:
+            # 256²: the fixture (torch CPU fp32) and the device sum in different orders, so ReLU /
+            # pool decisions within rounding of a tie go different ways (measured: norm 1.1e-3,
+            # max 9.4e-3 on stable pixels). Separate the two effects with the fp64 oracle on the
+            # same inputs: free (the fixture's branches but at ties) and forced onto the device
+            # run's branches (every forced disagreement a near-tie, forced_all's bound). The
+            # device equals the forced oracle to fp32 arithmetic, and deviates from the fixture
+            # by no more than the branch flips alone do (forced vs free fp64) + 1e-4 of max.
+            from oracle import forcing
+            vp = {k: (w.double(), b.double())
+                  for k, (w, b) in vgg_ref.load_positional(sd).items()}
+            with torch.no_grad():
+                tt = vgg_ref.vgg_forward(vp, t.double())
+            _, g_free = vgg_ref.tap_mse_grad(vp, x.double(), tt)
+            with forcing.audit() as au, vgg_ref.forced_masks([dev_masks]):
+                _, g_forced = vgg_ref.tap_mse_grad(vp, x.double(), tt)
+            flips, sites, worst, key = au.summary()
+            bad = [r["key"] for r in au.records if r["flips"] and r["rel_gap"] > 1e-5]
+            assert not bad and flips <= 1e-4 * sites, (flips, sites, worst, key)
+            g_full = gx[..., :3].permute(0, 3, 1, 2).double().cpu()
+            f_nrm = ((g_full - g_forced).norm() / g_forced.norm()).item()
+            f_mx = rel_err(g_full, g_forced)
+            scale = ref.abs().max()
+            tie = (g_forced[:, :, ::5, ::7] - g_free[:, :, ::5, ::7]).abs() / scale
+            dev = (got - ref).abs() / scale
+            untouched = tie <= 1e-6
+            st_un = dev[stable & untouched].max().item()
+            print(f"VGG golden 256²: forced flips {flips} of {sites} (max gap {worst:.2e}, "
+                  f"{key}); device vs forced fp64 oracle norm {f_nrm:.2e} max {f_mx:.2e}; vs "
+                  f"fixture max {dev.max():.2e} = branch flips {tie.max():.2e} + arithmetic; "
+                  f"{untouched.double().mean():.3f} of pixels untouched by flips, max there "
+                  f"{st_un:.2e}")
+            assert f_nrm < 1e-5 and f_mx < 2e-5, (f_nrm, f_mx)
+            assert (dev <= tie + 1e-4).all(), (dev - tie).max().item()
+            assert st_un <= 1e-4, st_un  # stable pixels no flip reaches: fp32 arithmetic only
+            assert nrm < 30 * tol and rel_err(got, ref) < 100 * tol, (tag, "grad", nrm)
         else:
-            # 256² (and bf16): ReLU masks of pre-activations within rounding of 0 flip between
-            # the two summation orders (fp32 s256 measured: norm 1.1e-3, max 9.4e-3); the
-            # arithmetic is pinned mask-for-mask in test_gpu_parity / test_gpu_networks
+            # bf16: ReLU masks of pre-activations within rounding of 0 flip between the two
+            # summation orders; the arithmetic is pinned mask-for-mask in test_gpu_parity
             assert nrm < 30 * tol and rel_err(got, ref) < 100 * tol, (tag, "grad", nrm)
         assert gx[..., 3:].abs().max().item() == 0.0
 

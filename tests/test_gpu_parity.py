@@ -6,7 +6,9 @@
 * mask-for-mask against the fp64 oracle: every branch of the oracle — e4e PReLU / LeakyReLU / SE
   ReLU, generator LeakyReLU, VGG ReLU and pool argmax of both VGG passes — is forced to the device
   run's (gpu_helpers.forced_all), which removes the flips of activations within rounding of a
-  tie; the remaining difference is fp32 arithmetic: measured 7.5e-6 in norm, bound 1e-4;
+  tie; the remaining difference is fp32 arithmetic: measured 7.5e-6 in norm, bound 1e-4. The
+  forcing is itself bounded: every forced branch that disagrees with the oracle's own fp64
+  decision must be a near-tie (|pre| ≤ 1e-5 of its layer's max) and such sites ≤ 1e-4 of all;
 * teacher-forced PGD steps: from the device's own iterate, the device update equals the oracle's
   projection (interpolation.py:92-94) of the oracle's mask-forced gradient BIT-EXACTLY on every
   sign-stable pixel.
@@ -112,8 +114,13 @@ def test_adam_mode_matches_reference_optimize_vgg(cuda, objg):
 
 
 def _forced_oracle_grad(eng, cap, params64, refs, x, size):
-    with forced_all(eng, cap):
-        return attack_ref.loss_grad(*params64, x.double(), refs, size)
+    """The fp64 oracle gradient on the device run's branches; every forced branch that disagrees
+    with the oracle's own must be a near-tie (gpu_helpers.forced_all.check)."""
+    fa = forced_all(eng, cap)
+    with fa:
+        out = attack_ref.loss_grad(*params64, x.double(), refs, size)
+    print(fa.check())
+    return out
 
 
 def test_e4e_attack_gradient_mask_for_mask(cuda):

@@ -271,6 +271,41 @@ def test_forced_branches_reproduce_the_free_forward():
     img = stylegan2_ref.synthesis(gp, lat, 32)
     with stylegan2_ref.forced_masks({}):  # no entry: the free branch
         assert torch.equal(img, stylegan2_ref.synthesis(gp, lat, 32))
+    # the flip audit (oracle/forcing.py): the oracle's own branches disagree nowhere ...
+    from oracle import forcing
+    with forcing.audit() as au, vgg_ref.forced_masks([masks]):
+        vgg_ref.vgg_forward(vp, x)
+    flips, sites, worst, _ = au.summary()
+    assert flips == 0 and worst == 0.0 and sites > 0
+    # ... a flipped decision at a clearly positive pre-activation and a moved pool argmax are
+    # reported with their gap (not near-ties: a device bug the forcing must not absorb)
+    w, b = vp["conv1_1"]
+    pre = torch.nn.functional.conv2d(x, w, b, padding=1)
+    i = int(pre.abs().flatten().argmax())
+    bad = dict(masks)
+    m = masks["conv1_1"].clone().flatten()
+    m[i] = ~m[i]
+    bad["conv1_1"] = m.view_as(masks["conv1_1"])
+    with forcing.audit() as au, vgg_ref.forced_masks([bad]):
+        vgg_ref.vgg_forward(vp, x)
+    rec = {r["key"]: r for r in au.records}
+    assert rec["vgg.conv1_1"]["flips"] == 1 and rec["vgg.conv1_1"]["rel_gap"] == 1.0
+    # (downstream layers now disagree too: their masks came from the unflipped forward)
+    assert rec["vgg.conv2_1"]["flips"] > 0
+    # a pool window whose one-hot is moved off its maximum: exactly that window, gap > 0
+    c12 = torch.relu(torch.nn.functional.conv2d(torch.relu(pre), *vp["conv1_2"], padding=1))
+    win = torch.nn.functional.max_pool2d(c12, 2, 2)
+    n0, ch, r, c = np.unravel_index(int(win.flatten().argmax()), tuple(win.shape))
+    bad = dict(masks)
+    p1 = masks["pool1"].clone()
+    w4 = p1[n0, ch, 2 * r:2 * r + 2, 2 * c:2 * c + 2]
+    p1[n0, ch, 2 * r:2 * r + 2, 2 * c:2 * c + 2] = w4.flip(0).flip(1)
+    bad["pool1"] = p1
+    with forcing.audit() as au, vgg_ref.forced_masks([bad]):
+        vgg_ref.vgg_forward(vp, x)
+    rec = {r["key"]: r for r in au.records}
+    assert rec["vgg.conv1_2"]["flips"] == 0
+    assert rec["vgg.pool1"]["flips"] == 1 and rec["vgg.pool1"]["rel_gap"] > 0
 
 
 # ---- the patch attack / patch_white_box / partial fusion pinned to the reference's own code ------

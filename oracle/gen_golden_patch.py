@@ -4,8 +4,9 @@
     python oracle/gen_golden_patch.py     # writes tests/golden/{patch,fusion}_golden.npz
 
 Like ``gen_golden_objective.py``, each function is taken out of its reference file with ``ast``
-and executed unchanged under ``oracle/refexec.py``'s restricted builtins, with the oracle's
-networks (fp64) where the reference fills in un-vendored modules:
+and executed unchanged through ``oracle/refexec.py`` — NOT a sandbox: a manual step in the build
+container (``MIA_EXEC_REFERENCE=1``) — with the oracle's networks (fp64) where the reference fills
+in un-vendored modules:
 
 * ``attack`` — ``code/attack/patch/adversarial_patch.py:94-160`` (the patch optimisation:
   ``patch -= ∇loss`` with loss = −MSE(E(x0'), E(x')), composite + clamp to the batch's
@@ -69,15 +70,15 @@ def gen_patch():
     gp, vp, ep = networks("e4e")
     img, patch, mask, tgt = (t.double() for t in patch_inputs())
     P = PATCH
-    with tempfile.TemporaryDirectory() as sandbox:
-        ns = refexec.execute(PATCH_FILE, ["attack"], sandbox, Variable=torch.autograd.Variable)
+    with tempfile.TemporaryDirectory() as workdir:
+        ns = refexec.execute(PATCH_FILE, ["attack"], workdir, Variable=torch.autograd.Variable)
         args = types.SimpleNamespace(max_count=P["max_count"], save_img=False)
         p = patch.clone()
         adv, m, p_out, rec = ns["attack"](
             img, p, mask, _Generator(gp), lambda x: encoder_ref.apply(ep, x, SIZE),
-            lambda x: tuple(vgg_ref.vgg_forward(vp, x)), "cpu", args, tgt, sandbox, 0, 0)
+            lambda x: tuple(vgg_ref.vgg_forward(vp, x)), "cpu", args, tgt, workdir, 0, 0)
         losses = [float(s.split(":")[1])
-                  for s in open(os.path.join(sandbox, "w_loss.txt")).read().split()]
+                  for s in open(os.path.join(workdir, "w_loss.txt")).read().split()]
     assert len(losses) == P["max_count"]
     probes = projections(SIZE, P["n"])
     ys, xs = slice(P["y0"], P["y0"] + P["side"]), slice(P["x0"], P["x0"] + P["side"])
@@ -96,8 +97,8 @@ def gen_patch():
     wb_mask[:, :, 10:30, 20:44] = 1.0
     wb_mask[:, :, 30:34, 20:44] = 0.5  # a soft edge
     wb_patch = (torch.rand(1, 3, WB_SIZE, WB_SIZE, generator=g) * 2.4 - 1.2) * (wb_mask > 0)
-    with tempfile.TemporaryDirectory() as sandbox:
-        ns = refexec.execute(MAIN2_FILE, ["patch_white_box"], sandbox)
+    with tempfile.TemporaryDirectory() as workdir:
+        ns = refexec.execute(MAIN2_FILE, ["patch_white_box"], workdir)
         wb = ns["patch_white_box"](inputs, wb_mask, wb_patch)
     out.update({"wb/inputs": inputs.numpy(), "wb/mask": wb_mask.numpy(),
                 "wb/patch": wb_patch.numpy(), "wb/out": wb.numpy()})
@@ -123,13 +124,13 @@ def gen_fusion():
     gp = {k: v.double() for k, v in make_generator_weights(SIZE, seed=0).items()}
     W, Wa = (t.double() for t in fusion_latents())
     M = FUSION["m"]
-    with tempfile.TemporaryDirectory() as sandbox:
+    with tempfile.TemporaryDirectory() as workdir:
         ns = refexec.execute(INTERP_FILE, ["interpolation", "partial_adv_fusion_arithmetic"],
-                             sandbox, batch_idx=0, drawer=_OracleDrawer(gp),
+                             workdir, batch_idx=0, drawer=_OracleDrawer(gp),
                              args=types.SimpleNamespace(save_img=False))
         inputs = torch.zeros(M, 3, 8, 8)
         with torch.no_grad():
-            fused = ns["partial_adv_fusion_arithmetic"](sandbox, inputs, inputs + 1, W, Wa)
+            fused = ns["partial_adv_fusion_arithmetic"](workdir, inputs, inputs + 1, W, Wa)
     assert tuple(fused.shape) == (M + 1, 3, SIZE, SIZE)
     probes = projections(SIZE, M + 1)
     out = {"fused/slice": fused[SLICE].numpy(), "fused/proj": _proj(fused, probes),

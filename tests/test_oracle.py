@@ -371,3 +371,25 @@ def test_oracle_partial_fusion_matches_reference():
     assert _rel(fused[gi.SLICE].numpy(), fg["fused/slice"]) < 1e-12
     probes = gi.projections(gi.SIZE, M + 1)
     assert _rel([float((q * fused).sum()) for q in probes], fg["fused/proj"]) < 1e-12
+
+
+def test_reference_sources_unchanged():
+    """The reference functions the golden fixtures were generated from still have the AST they
+    had then (oracle/ref_sources.py: parsed, never executed). Build container only: the GPU box
+    has no /root/reference."""
+    import json
+    from oracle import ref_sources
+    if not os.path.isdir(ref_sources.REF):
+        pytest.skip("no /root/reference here")
+    with open(os.path.join(GOLDEN, "reference_sources.json")) as fh:
+        want = json.load(fh)
+    assert ref_sources.compute() == want
+
+
+def test_refexec_refuses_without_explicit_opt_in(monkeypatch):
+    """oracle/refexec runs reference code with full privileges (it is not a sandbox): it refuses
+    unless the golden-generation opt-in is set, so no test or product path can run it."""
+    from oracle import refexec
+    monkeypatch.delenv("MIA_EXEC_REFERENCE", raising=False)
+    with pytest.raises(PermissionError):
+        refexec.execute(__file__, ["seeded"], "/tmp")

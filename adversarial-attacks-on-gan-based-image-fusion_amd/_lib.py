@@ -84,6 +84,8 @@ SIGNATURES = {
     "mia_get_tuning": (c_int, [ctypes.c_char_p, ctypes.POINTER(c_int)]),
     "mia_conv_kpad": (c_int, [c_int, c_int]),
     "mia_conv3x3": (c_int, [ctypes.POINTER(ConvArgs), c_int, P]),
+    "mia_modulate_weights": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
+    "mia_conv3x3_wmod": (c_int, [ctypes.POINTER(ConvArgs), c_int64, c_int, P]),
     "mia_modconv_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P, P,
                                 c_float, P, c_int, c_int, P]),
     "mia_modconv_bwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, c_int, P, P,

@@ -23,6 +23,14 @@ struct ConvGroup {
 };
 constexpr int MIA_MAX_GROUPS = 16;
 
+// N·H·W as the int of ConvGroup::m, saturated: the product is formed before the argument checks
+// (which reject anything ≥ 2^31), so it must not overflow on its way there (signed-overflow UB,
+// found by the host sanitizer build, tools/asan/host_abi_check.cpp)
+inline int pixels_clamped(int n, int h, int w) {
+  const int64_t m = (int64_t)n * h * w;
+  return m < 0 ? -1 : (m > 0x7fffffff ? 0x7fffffff : (int)m);
+}
+
 struct ConvK {
   mia_conv_args a;  // x, y, N, H/W = INPUT dims, Cin, Cout and the epilogue fields
   int stride, HT, WT, ystride, cout_mod, log2cin, n_first_max, ng, nblk, nbn;
@@ -36,6 +44,9 @@ struct ConvK {
   float* red_part;
   int red_nslots, red_count;     // slots per output; outputs per quantity (N·Cout)
   int red_px;                    // LDS-staged epilogue: one slot per output pixel (small images)
+  int64_t wn;                    // elements between the images' weight matrices (0: one shared
+                                 // [Cout][Kpad]; > 0: per-image modulated weights, mia_conv3x3_wmod,
+                                 // the 2-byte halo kernel only)
   ConvGroup g[MIA_MAX_GROUPS];
 };
 

@@ -94,9 +94,11 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
   constexpr int HPIECES = TL::HPIECES, BWAVES = TL::BWAVES, HWAVES = TL::HWAVES;
   constexpr int HPS = TL::H_PER_STEP;
 
-  // AUXP: the StyledConv forward (modulated input; demod, noise, bias, lrelu) prefetches its
-  // epilogue operands into the free halo buffer during the last channel block
-  constexpr bool AUXP = PRO && EPI == (epi::OSC | epi::NOISE | epi::BIAS | epi::LRELU) &&
+  // AUXP: the StyledConv forward (demod, noise, bias, lrelu — modulated input, or per-image
+  // modulated weights without the demod) prefetches its epilogue operands into the free halo
+  // buffer during the last channel block
+  constexpr bool AUXP = ((PRO && EPI == (epi::OSC | epi::NOISE | epi::BIAS | epi::LRELU)) ||
+                         (!PRO && EPI == (epi::NOISE | epi::BIAS | epi::LRELU))) &&
                         TL::NHBUF == 2 && TL::BN == 128 && TL::FM <= 4;
   constexpr int AUX_OFF = 4096;  // past the LDS pre-reduction rows (3 × WM × BN floats)
   static_assert(!AUXP || (AUX_OFF + 2048 <= TL::HBUF && 3 * TL::WM * TL::BN * 4 <= AUX_OFF &&
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
   const int n = mt / (ptx * pty);
 
   const T* __restrict__ X = (const T*)p.x;
-  const T* __restrict__ Wt = (const T*)G.w;
+  const T* __restrict__ Wt = (const T*)G.w + (size_t)n * k.wn;  // per-image weights (wmod)
   const T* zero = (const T*)g_zero16;
   const bool bwave = wid < BWAVES;  // wave-uniform role
   const int hw = wid - BWAVES;      // H-wave index
@@ -255,8 +257,9 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
       const int l = lane & 31;
       const float* a0;
       if (lane < 32) {  // demod (out_scale) | noise rows
-        a0 = n0 + 4 * l < Cout ? p.out_scale + (size_t)n * k.cout_mod + n0 + 4 * l
-                               : (const float*)g_zero16;
+        a0 = (EPI & epi::OSC) && n0 + 4 * l < Cout
+                 ? p.out_scale + (size_t)n * k.cout_mod + n0 + 4 * l
+                 : (const float*)g_zero16;
       } else {          // bias
         a0 = n0 + 4 * l < Cout ? p.bias + n0 + 4 * l : (const float*)g_zero16;
       }
@@ -508,6 +511,8 @@ static int launch_halo_tile(ConvK& k, hipStream_t st) {
           return launch_halo_tile_<T, TL, PRO, OSC | NOISE | BIAS | LRELU>(k, st);
       } else switch (f) {  // the other launches of the attack step (vgg.py, stylegan2.py)
         case 0: return launch_halo_tile_<T, TL, PRO, 0>(k, st);
+        // the StyledConv forward on per-image modulated + demodulated weights (mia_conv3x3_wmod)
+        case NOISE | BIAS | LRELU: return launch_halo_tile_<T, TL, PRO, NOISE | BIAS | LRELU>(k, st);
         case BIAS | RELU: return launch_halo_tile_<T, TL, PRO, BIAS | RELU>(k, st);
         case MASK: return launch_halo_tile_<T, TL, PRO, MASK>(k, st);
         case TAP: return launch_halo_tile_<T, TL, PRO, TAP>(k, st);
@@ -581,7 +586,98 @@ int launch_conv_halo(ConvK& k, int dtype, hipStream_t st) {
   return MIA_OK;
 }
 
+// Per-image modulated + demodulated weights of a StyledConv (rosinality ModulatedConv2d's
+// weight path, the form the reference's generator computes: w' = w·s[n][ci]·demod[n][co]), for
+// the 2-byte halo kernel at high resolution: the activations enter the MFMAs unmodulated, so the
+// kernel has no per-channel-block modulation pass over the halo in LDS and no demod in the
+// epilogue. One thread per 16-B vector of a weight row; rows [n][co] of the [N][Cout][Kpad] out.
+template <typename T>
+__global__ __launch_bounds__(256) void modulate_weights_kernel(const T* __restrict__ w,
+                                                               const float* __restrict__ s,
+                                                               const float* __restrict__ d,
+                                                               T* __restrict__ out, int Cout,
+                                                               int Cin, int K, int Kpad,
+                                                               int64_t nvec) {
+  typedef typename Vec<T>::type VT;
+  constexpr int VEC = Vec<T>::N;
+  const int vpr = Kpad / VEC;  // vectors per row
+  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec;
+       v += (int64_t)gridDim.x * 256) {
+    const int64_t row = v / vpr;  // n·Cout + co
+    const int kv = (int)(v - row * vpr) * VEC;
+    const int n = (int)(row / Cout), co = (int)(row - (int64_t)n * Cout);
+    const VT wv = *(const VT*)(w + (size_t)co * Kpad + kv);
+    const float dm = d ? d[row] : 1.f;
+    const float* sn = s + (size_t)n * Cin;
+    VT o;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const int kk = kv + e;
+      o[e] = kk < K ? from_f<T>(to_f(wv[e]) * sn[kk & (Cin - 1)] * dm) : from_f<T>(0.f);
+    }
+    *(VT*)(out + (size_t)row * Kpad + kv) = o;
+  }
+}
+
 }  // namespace mia
+
+using namespace mia;
+
+extern "C" int mia_modulate_weights(const void* w, const float* in_scale, const float* out_scale,
+                                    void* w_mod, int N, int Cout, int Cin, int Kpad, int dtype,
+                                    void* stream) {
+  MIA_CHECK_ARG(w && in_scale && w_mod && N > 0 && Cout > 0, "bad args");
+  MIA_CHECK_ARG(dtype == MIA_F16 || dtype == MIA_BF16, "2-byte dtypes only");
+  MIA_CHECK_ARG(Cin >= 8 && (Cin & (Cin - 1)) == 0, "Cin must be a power of two >= 8");
+  MIA_CHECK_ARG(Kpad == mia_conv_kpad(Cin, dtype), "Kpad must be mia_conv_kpad()");
+  const int64_t nvec = (int64_t)N * Cout * (Kpad / 8);
+  const int grid = (int)std::min<int64_t>((nvec + 255) / 256, 8192);
+  hipStream_t st = (hipStream_t)stream;
+  MIA_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL(modulate_weights_kernel<T>, dim3(grid), dim3(256), 0, st, (const T*)w,
+                       in_scale, out_scale, (T*)w_mod, Cout, Cin, 9 * Cin, Kpad, nvec);
+  });
+  return check_launch("modulate_weights");
+}
+
+// mia_conv3x3 on per-image weights: args->w = [N][Cout][Kpad] (mia_modulate_weights), the images'
+// matrices w_nstride elements apart; no in_scale (the modulation is in the weights).
+extern "C" int mia_conv3x3_wmod(const mia_conv_args* args, int64_t w_nstride, int dtype,
+                                void* stream) {
+  MIA_CHECK_ARG(args != nullptr, "null args");
+  const mia_conv_args& a = *args;
+  MIA_CHECK_ARG(dtype == MIA_F16 || dtype == MIA_BF16, "2-byte dtypes only");
+  MIA_CHECK_ARG(w_nstride >= (int64_t)a.Cout * a.Kpad, "w_nstride < Cout·Kpad");
+  MIA_CHECK_ARG(a.in_scale == nullptr && a.act_in == MIA_ACT_NONE && !a.shuffle_out,
+                "per-image weights: no in_scale / act_in / shuffle_out");
+  MIA_CHECK_ARG(a.Cout > 64 && a.Cin <= 2048, "per-image weights: the 128-channel halo tile");
+  ConvK k = {};
+  k.a = a;
+  k.stride = 1;
+  k.ng = 1;
+  ConvGroup& G = k.g[0];
+  G.w = a.w;
+  G.kpad = a.Kpad;
+  G.kh = G.kw = 3;
+  G.pad_y = G.pad_x = 1;
+  G.ho = a.H;
+  G.wo = a.W;
+  G.ay = G.ax = 1;
+  G.m = pixels_clamped(a.N, a.H, a.W);
+  k.HT = a.H;
+  k.WT = a.W;
+  k.cout_mod = a.Cout;
+  k.ystride = a.y_cstride > 0 ? a.y_cstride : a.Cout;
+  k.wn = w_nstride;
+  MIA_CHECK_ARG(k.ystride >= k.cout_mod, "y_cstride < Cout");
+  MIA_CHECK_ARG(a.x && a.w && a.y && a.N > 0 && a.Cin % 64 == 0 && a.Cout % 8 == 0,
+                "bad conv args");
+  MIA_CHECK_ARG(a.Kpad == mia_conv_kpad(a.Cin, dtype), "Kpad must be mia_conv_kpad()");
+  MIA_CHECK_ARG((int64_t)a.N * a.H * a.W * a.Cin < (1LL << 31), "input too large");
+  MIA_CHECK_ARG(conv_halo_eligible(k, dtype), "per-image weights need the halo kernel's shapes "
+                                              "(H, W multiples of 16)");
+  return launch_conv_halo(k, dtype, (hipStream_t)stream);
+}
 
 #ifdef MIA_HALO_TIMING
 extern "C" int mia_debug_halo_timing(unsigned long long* out, int reset) {

@@ -611,7 +611,7 @@ extern "C" int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream) {
   G.ho = a.H;
   G.wo = a.W;
   G.ay = G.ax = 1;
-  G.m = a.N * a.H * a.W;
+  G.m = pixels_clamped(a.N, a.H, a.W);
   k.HT = a.shuffle_out ? 2 * a.H : a.H;
   k.WT = a.shuffle_out ? 2 * a.W : a.W;
   k.cout_mod = a.shuffle_out ? a.Cout / 4 : a.Cout;
@@ -678,7 +678,7 @@ static int conv2d_impl(const mia_conv_args* args, int stride, const mia_conv_gro
     G.by = s.by;
     G.ax = s.ax;
     G.bx = s.bx;
-    G.m = a.N * s.ho * s.wo;
+    G.m = pixels_clamped(a.N, s.ho, s.wo);
     if (batch) {
       G.n_in = batch[g].n_in;
       G.n_out = batch[g].n_out;
@@ -721,7 +721,7 @@ extern "C" int mia_upconv_fwd(const void* x, const void* const* w_phase, void* t
     G.ay = G.ax = 2;
     G.by = py;
     G.bx = px;
-    G.m = N * G.ho * G.wo;
+    G.m = pixels_clamped(N, G.ho, G.wo);
   }
   return run_conv(k, dtype, (hipStream_t)stream);
 }
@@ -778,7 +778,7 @@ extern "C" int mia_upconv_fwd_halo_split(const void* x, const void* const* w_pha
       G.pad_y = G.kh - 1; G.pad_x = (G.kw - 1) - R;
       G.by = py; G.bx = 2 * R + px;
     }
-    G.m = N * G.ho * G.wo;
+    G.m = pixels_clamped(N, G.ho, G.wo);
   }
   return run_conv(k, dtype, (hipStream_t)stream);
 }
@@ -837,7 +837,7 @@ static int upconv_dgrad_impl(const mia_conv_args& a, const void* w_t, int N, int
   G.pad_y = G.pad_x = 0;
   G.ho = G.wo = R;
   G.ay = G.ax = 1;
-  G.m = N * R * R;
+  G.m = pixels_clamped(N, R, R);
   k.HT = k.WT = R;
   k.cout_mod = Cin;
   k.ystride = Cin;

@@ -139,6 +139,50 @@ def conv3x3(x, w, y, *, cout, act_in=ACT_NONE, in_scale=None, out_scale=None, bi
     return y
 
 
+def conv3x3_modw(x, w, y, w_mod, *, cout, in_scale, out_scale=None, bias=None, noise=None,
+                 noise_w=0.0, act_out=ACT_NONE, flops=None):
+    """The StyledConv forward on per-image weights (fp16 / bf16): mia_modulate_weights writes
+    w_mod[n] = w·in_scale[n]·out_scale[n] (the modulation and demodulation folded into the
+    weights), then mia_conv3x3_wmod convolves the unmodulated x. Same result as
+    conv3x3(x, w, y, in_scale=…, out_scale=…) up to where the one rounding to T happens.
+    Profiled as ONE conv call (the weight pass included)."""
+    N, H, W, Cin = x.shape
+    T = x.dtype
+    if T not in (torch.float16, torch.bfloat16):
+        raise ValueError("per-image weights: fp16 / bf16 only")
+    kpad = conv_kpad(Cin, T)
+    _need(w, (cout, kpad), T, "w")
+    _need(w_mod, (N, cout, kpad), T, "w_mod")
+    _need(y, (N, H, W, cout), T, "y")
+    f32 = torch.float32
+    _numel_ok(in_scale, N * Cin, f32, "in_scale")
+    _numel_ok(out_scale, N * cout, f32, "out_scale")
+    _numel_ok(bias, cout, f32, "bias")
+    _numel_ok(noise, H * W, f32, "noise")
+    if in_scale is None:
+        raise ValueError("in_scale (the style) is required")
+    a = ConvArgs()
+    a.x, a.w, a.y = ptr(x), ptr(w_mod), ptr(y)
+    a.N, a.H, a.W, a.Cin, a.Cout, a.Kpad = N, H, W, Cin, cout, kpad
+    a.y_cstride = cout
+    a.act_in = ACT_NONE
+    a.bias, a.noise = ptr(bias), ptr(noise)
+    a.noise_w = float(noise_w)
+    a.act_out = act_out
+    prof = PROFILE
+    if prof is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    call("mia_modulate_weights", ptr(w), ptr(in_scale), ptr(out_scale), ptr(w_mod), N, cout, Cin,
+         kpad, dt(T), stream())
+    call("mia_conv3x3_wmod", ctypes.byref(a), cout * kpad, dt(T), stream())
+    if prof is not None:
+        e1.record()
+        prof.append((e0, e1, flops if flops is not None else 2 * N * H * W * 9 * Cin * cout))
+        _tag(f"conv3x3 {H}x{W} {Cin}->{cout} mod wmod")
+    return y
+
+
 def _prof_call(name, flops, *args):
     prof = PROFILE
     if prof is not None:

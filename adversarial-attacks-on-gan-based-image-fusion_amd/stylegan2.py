@@ -27,6 +27,13 @@ from .ops import ACT_LRELU_S2, ACT_NONE
 from .weights import STYLE_DIM, generator_layout, n_latent_for
 
 UP_K = list(layouts.BLUR_F)  # separable ToRGB skip up-sampler (Upsample(blur_kernel), factor 2)
+# fp16 / bf16 StyledConv forwards at resolution ≥ WMOD_MIN_RES run on per-image modulated +
+# demodulated weights (ops.conv3x3_modw: rosinality's own weight path) instead of modulating the
+# input halo in LDS once per channel block: at 128² / 256² an image's weight matrix is read by
+# ≥ 128 patch blocks of one XCD (L2-resident), and the halo kernel drops its modulation pass and
+# the demod in its epilogue. Below it (≤ 32 patches per image, 512 channels) the per-image
+# matrices would not stay in L2. 0 disables (A/B: MIA_G_WMOD_RES).
+WMOD_MIN_RES = int(__import__("os").environ.get("MIA_G_WMOD_RES", "128"))
 
 
 class SynthesisNet:
@@ -186,6 +193,13 @@ class SynthesisNet:
                                w_up=L.get("wup"))
                 ops.upconv_blur_fwd(t, pre, L["_d"], L["noise"], L["noise_w"], L["bias"],
                                     act_out=ACT_LRELU_S2)
+            elif (not L["up"] and T != torch.float32 and WMOD_MIN_RES
+                  and r >= WMOD_MIN_RES and r % 16 == 0 and cout > 64):
+                wm = ws.get(f"g.wmod{i}", (N,) + tuple(L["wf"].shape), T)
+                ops.conv3x3_modw(x, L["wf"], pre, wm, cout=cout, in_scale=L["_s"],
+                                 out_scale=L["_d"], noise=L["noise"], noise_w=L["noise_w"],
+                                 bias=L["bias"], act_out=ACT_LRELU_S2,
+                                 flops=self._alg_flops(L, N))
             else:
                 ops.conv3x3(x, L["wf"], pre, cout=4 * cout if L["up"] else cout,
                             in_scale=L["_s"], out_scale=L["_d"], noise=L["noise"],

@@ -139,6 +139,17 @@ typedef struct mia_conv_args {
 
 int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream);
 
+/* StyledConv forward on per-image weights (fp16 / bf16; the StyleGAN2 modulated_conv2d of
+ * attack_main2.py:619-621, rosinality ModulatedConv2d's own weight path): mia_modulate_weights
+ * writes w_mod[n][co][k] = w[co][k]·in_scale[n][ci(k)]·out_scale[n][co] (out_scale may be NULL),
+ * k = tap·Cin + ci < 9·Cin, 0 in the Kpad padding; mia_conv3x3_wmod then runs mia_conv3x3 with
+ * args->w = w_mod, the images' matrices w_nstride elements apart, and no in_scale / out_scale
+ * (folded into the weights). Halo-kernel shapes only (H, W multiples of 16, Cout > 64). */
+int mia_modulate_weights(const void* w, const float* in_scale, const float* out_scale,
+                         void* w_mod, int N, int Cout, int Cin, int Kpad, int dtype,
+                         void* stream);
+int mia_conv3x3_wmod(const mia_conv_args* args, int64_t w_nstride, int dtype, void* stream);
+
 /*
  * General form of the same implicit-GEMM conv: 1..4 problems ("groups") over one input x
  * (args->H × args->W) that share the epilogue, each with its own weights [Cout][Kpad]

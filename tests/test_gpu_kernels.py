@@ -165,6 +165,52 @@ def test_modconv_fwd(cuda, dtype, up):
     assert rel_err(nchw(y), ref) < 2 * TOL[dtype]
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,cin,cout,R", [(3, 128, 128, 32), (2, 256, 256, 16), (2, 64, 128, 48)])
+def test_modconv_fwd_per_image_weights(cuda, dtype, N, cin, cout, R):
+    """The StyledConv forward on per-image modulated + demodulated weights (mia_modulate_weights
+    + mia_conv3x3_wmod, the fp16 / bf16 synthesis at ≥ 128²) against the fp64 oracle's
+    per-sample modulated_conv2d (rosinality's weight path) and the halo kernel's LDS-modulated
+    form of the same layer; the epilogue (noise, bias, lrelu·√2) as the generator stores it."""
+    p, wlat, x, noise, bias = _modconv_setup(13, N, cin, cout, R)
+    noise = noise[..., :R, :R].contiguous()
+    xa = F.leaky_relu(x.double(), 0.2) * math.sqrt(2)  # the stored activation of the layer below
+    pre = stylegan2_ref.modulated_conv2d({k: v.double() for k, v in p.items()}, "m", xa,
+                                         wlat.double(), demodulate=True)
+    ref = F.leaky_relu(pre + 0.1 * noise.double() + bias.double().view(1, -1, 1, 1),
+                       0.2) * math.sqrt(2)
+    scale = 1.0 / math.sqrt(cin * 9)
+    ws = p["m.weight"][0].double() * scale
+    s = F.linear(wlat.double(), p["m.modulation.weight"].double() / math.sqrt(512),
+                 p["m.modulation.bias"].double()).float().to(cuda)
+    wsq = (ws ** 2).sum((2, 3)).float().to(cuda)
+    demod = torch.empty(N, cout, device=cuda)
+    ops.style_demod(s, wsq, demod)
+    wf = layouts.fwd_matrix(ws, dtype).to(cuda)
+    xd = nhwc(xa, dtype).to(cuda)
+    kw = dict(cout=cout, in_scale=s, out_scale=demod, noise=noise.reshape(-1).to(cuda),
+              noise_w=0.1, bias=bias.to(cuda), act_out=ops.ACT_LRELU_S2)
+    y = torch.empty(N, R, R, cout, dtype=dtype, device=cuda)
+    wm = torch.empty((N,) + tuple(wf.shape), dtype=dtype, device=cuda)
+    ops.conv3x3_modw(xd, wf, y, wm, **kw)
+    y_lds = torch.empty_like(y)
+    ops.conv3x3(xd, wf, y_lds, **kw)
+    torch.cuda.synchronize()
+    # the weights themselves: (w·s)·demod in fp32, rounded once to the dtype; 0 in the padding
+    K = 9 * cin
+    wref = torch.zeros(wm.shape, dtype=torch.float32, device=cuda)
+    wref[:, :, :K] = wf[:, :K].float()[None] * s.repeat(1, 9)[:, None, :] * demod[:, :, None]
+    assert torch.equal(wm, wref.to(dtype))
+    e_w, e_lds = rel_err(nchw(y), ref), rel_err(nchw(y_lds), ref)
+    print(f"per-image weights {dtype} {N}x{R}² {cin}->{cout}: rel err {e_w:.2e} "
+          f"(LDS-modulated {e_lds:.2e})")
+    assert e_w < 2 * TOL[dtype] and e_w < 2 * e_lds + 1e-3
+    with pytest.raises(_lib.MiaError):  # not a halo-kernel shape: refused, no fallback
+        ops.conv3x3_modw(xd[:, :R - 8, :R - 8].contiguous(), wf,
+                         torch.empty(N, R - 8, R - 8, cout, dtype=dtype, device=cuda), wm,
+                         **dict(kw, noise=None))
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("up", [False, True])
 @pytest.mark.parametrize("store_act", [False, True])

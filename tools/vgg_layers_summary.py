@@ -53,9 +53,23 @@ def dispatches(path, kind):
 AUX = {"dconv4_2": 1, "dconv3_3": 1, "dconv3_2": 1, "dconv3_1": 2, "dconv2_2": 1, "dconv1_2": 2}
 
 
+# pools: (input channels, input side); the 2×2 window's input gradient at pool1 carries the fused
+# conv1_2 tap-MSE term (maxpool2_bwd<…, true>: reads the tap and its target)
+POOLS = {"pool1": (64, 256, True), "pool2": (128, 128, False), "pool3": (256, 64, False)}
+
+
 def work(label, N, esize):
     """(algorithmic FLOP, algorithmic HBM bytes: inputs read once + outputs written once)."""
     base = label.lstrip("d")
+    if base in POOLS:
+        c, r, tap = POOLS[base]
+        ro = -(-r // 2)
+        big, small = N * r * r * c * esize, N * ro * ro * c * esize
+        if label.startswith("d"):  # read x (+ tap target) and g_out, write g_in
+            return 0, big * (3 if tap else 2) + small
+        return 0, big + small
+    if label == "tap4_2":  # read the tap and its target, write the gradient (32², 512 ch)
+        return 0, 3 * N * 32 * 32 * 512 * esize
     if base not in CONVS:
         return 0, None
     cin, cout, r = CONVS[base]
@@ -82,14 +96,16 @@ def main():
     wr = dispatches(a.write, "pmc")
     mf = dispatches(a.mfma, "pmc") if a.mfma else [{}] * len(LABELS)
     assert len(tr) == len(fe) == len(wr) == len(LABELS), (len(tr), len(fe), len(wr))
-    rows, tot_ns, tot_b = [], 0, 0.0
+    rows, tot_ns, tot_b, tot_alg = [], 0, 0.0, 0.0
     lines = [f"# VGG16 cascade per layer ({a.dtype}, {a.batch} images at 256²: code/vgg.py:44-64 "
              f"forward + the tap-MSE input gradient)", "",
              "rocprofv3 kernel trace + separate FETCH_SIZE / WRITE_SIZE passes (FETCH_SIZE ×2, "
              "gfx950 correction); last rep of tools/vgg_cascade.py. GB/s = PMC HBM bytes ÷ "
-             "dispatch duration; alg. MB = inputs read once + outputs written once.", "",
-             "| layer | kernel | µs | TFLOP/s | HBM MB (PMC) | alg. MB | HBM GB/s | MFMA busy |",
-             "|---|---|---|---|---|---|---|---|"]
+             "dispatch duration; alg. MB = inputs read once + outputs written once; PMC/alg = "
+             "the wasted-traffic ratio (re-reads of halos / weights beyond one pass).", "",
+             "| layer | kernel | µs | TFLOP/s | HBM MB (PMC) | alg. MB | PMC/alg | HBM GB/s | "
+             "MFMA busy |",
+             "|---|---|---|---|---|---|---|---|---|"]
     for lab, (name, ns), f, w, m in zip(LABELS, tr, fe, wr, mf):
         hb = 2.0 * f.get("FETCH_SIZE", 0.0) * 1024 + w.get("WRITE_SIZE", 0.0) * 1024
         fl, alg = work(lab, a.batch, es)
@@ -103,14 +119,19 @@ def main():
         rows.append(r)
         tot_ns += ns
         tot_b += hb
+        tot_alg += alg or 0.0
         lines.append(f"| {lab} | `{kn}` | {ns / 1e3:.1f} | "
                      f"{'' if not fl else f'{fl / ns / 1e3:.1f}'} | {hb / 1e6:.1f} | "
-                     f"{'' if not alg else f'{alg / 1e6:.1f}'} | {hb / ns:.0f} | "
+                     f"{'' if not alg else f'{alg / 1e6:.1f}'} | "
+                     f"{'' if not alg else f'{hb / alg:.2f}'} | {hb / ns:.0f} | "
                      f"{'' if busy is None else f'{busy:.2f}'} |")
-    lines += ["", f"cascade: {tot_ns / 1e3:.0f} µs, {tot_b / 1e6:.0f} MB HBM, "
-              f"{tot_b / tot_ns:.0f} GB/s average"]
+    lines += ["", f"cascade: {tot_ns / 1e3:.0f} µs, {tot_b / 1e6:.0f} MB HBM (PMC) vs "
+              f"{tot_alg / 1e6:.0f} MB algorithmic = {tot_b / tot_alg:.2f}× wasted-traffic ratio; "
+              f"{tot_b / tot_ns:.0f} GB/s average (PMC bytes), "
+              f"{tot_alg / tot_ns:.0f} GB/s algorithmic"]
     open(a.out + ".md", "w").write("\n".join(lines) + "\n")
-    json.dump({"layers": rows, "total_us": tot_ns / 1e3, "total_hbm_mb": tot_b / 1e6},
+    json.dump({"layers": rows, "total_us": tot_ns / 1e3, "total_hbm_mb": tot_b / 1e6,
+               "total_alg_mb": tot_alg / 1e6},
               open(a.out + ".json", "w"), indent=1)
     print("\n".join(lines))
 

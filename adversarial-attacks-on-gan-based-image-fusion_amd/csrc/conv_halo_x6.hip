@@ -48,8 +48,11 @@ __device__ unsigned long long g_x6_stamps[4][16];
 #endif
 
 // BN_ = 128: 4 row waves × 2 column waves of 4 × 4 fragments; BN_ = 64 (the 64-channel layers):
-// 8 row waves of 2 × 4 fragments.
-template <int BN_>
+// 8 row waves of 2 × 4 fragments. TPS_ taps per K-step (round 4, the 64-column tile of the
+// unrolled loop: 2): a stage holds the pre-split weights of TPS taps, so a K-step carries the
+// 128-column tile's MFMA count (96 per wave) and weight DMA pieces (6 per B-wave) and the per-step
+// barrier, wait and DMA issue are paid half as often (9 taps = 5 steps per channel block).
+template <int BN_, int TPS_ = 1>
 struct HaloX6 {
   static constexpr int PH = 16, PW = 16, NW = 8, NT = 64 * NW;
   static constexpr int WN = BN_ == 128 ? 2 : 1, WM = NW / WN, FM = 16 / WM, FN = 4;
@@ -58,12 +61,15 @@ struct HaloX6 {
   static constexpr int HPIECES = (HROWS + 7) / 8;                 // 1-KB pieces of 8 rows
   static constexpr int HBUF = HPIECES * 1024;
   static constexpr int LROWB = 64, LBUF = HROWS * LROWB;          // lo: 32 × bf16 per pixel
-  static constexpr int BHM = BN * ROWB, BL = BN * LROWB, BSTAGE = BHM + BL;
+  static constexpr int TPS = TPS_, NG = (9 + TPS - 1) / TPS;  // taps per K-step, steps per block
+  static constexpr int BHM = BN * ROWB, BL = BN * LROWB, BSTAGE1 = BHM + BL;  // one tap
+  static constexpr int BSTAGE = TPS * BSTAGE1;
   static constexpr int BWAVES = 4, HWAVES = 4;
   static constexpr int B_HM_INS = BN / 8 / BWAVES;   // [hi|mid] pieces (8 rows) per B-wave
   static constexpr int B_L_INS = BN / 16 / BWAVES;   // lo pieces (16 rows of 64 B) per B-wave
   static constexpr int H_INS = (HPIECES + HWAVES - 1) / HWAVES;
-  static constexpr int H_PER_STEP = (H_INS + 3) / 4;  // next block's halo issued over taps 0–3
+  static constexpr int HSTEPS = (4 + TPS - 1) / TPS;    // next block's halo issued over taps 0–3
+  static constexpr int H_PER_STEP = (H_INS + HSTEPS - 1) / HSTEPS;
   static constexpr int EROWS = 128, ES = BN + 4;      // shared LDS epilogue staging
   static constexpr int LDS = 2 * HBUF + LBUF + 2 * BSTAGE;
   static_assert(WM * FM * 16 == BM && WN * FN * 16 == BN, "");
@@ -71,10 +77,12 @@ struct HaloX6 {
   static_assert(LDS <= 160 * 1024, "");
 };
 
-template <int BN_, bool PRO, int EPI, bool EARLY, bool PRIO, bool UNR>
+template <int BN_, bool PRO, int EPI, bool EARLY, bool PRIO, bool UNR, int TPS = 1>
 __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const ConvK k) {
   static_assert(!UNR || (EARLY && PRIO && EPI != -2), "UNR: the EARLY + PRIO schedule, D[ch][px]");
-  typedef HaloX6<BN_> TL;
+  static_assert(UNR || TPS == 1, "several taps per K-step: the unrolled loop only");
+  typedef HaloX6<BN_, TPS> TL;
+  constexpr int NG = TL::NG;
   constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, NT = TL::NT, BN = TL::BN, BK = TL::BK;
   constexpr int HSIDE = TL::HSIDE, HROWS = TL::HROWS, HPIECES = TL::HPIECES, HBUF = TL::HBUF;
   constexpr int H_INS = TL::H_INS, HPS = TL::H_PER_STEP, HWAVES = TL::HWAVES;
@@ -139,26 +147,32 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
         src[j] = (const char*)(X + ((size_t)(n * H + y) * W + x) * Cin + ((lane & 7) ^ fsw(hr)) * 4);
     }
   }
-  const int ncb = Cin / BK, nk = 9 * ncb;
+  const int ncb = Cin / BK, nk = NG * ncb;
 
-  auto issue_b = [&](int s, int st) {  // B-wave: its weight pieces of K-step s = (cb, tap)
-    const int cb = s / 9, t = s - (s / 9) * 9;
-    const int koff = t * Cin + cb * BK;  // k offset (elements) of the step in a weight row
-    char* dst = bring + st * BSTAGE;
+  auto issue_b = [&](int s, int st) {  // B-wave: its weight pieces of K-step s = (cb, taps)
+    const int cb = s / NG, tg = s - (s / NG) * NG;
 #pragma unroll
-    for (int j = 0; j < B_HM_INS; ++j) {
-      const char* a = EPI >= 0 ? src[j] + (size_t)koff * 4 : src[j] ? src[j] + (size_t)koff * 4 : zero;
-      __builtin_amdgcn_global_load_lds((gptr_t)a, (lptr_t)(dst + (wid * B_HM_INS + j) * 1024), 16,
-                                       0, 0);
-    }
+    for (int tt = 0; tt < TPS; ++tt) {
+      const int t = tg * TPS + tt;
+      if (TPS > 1 && t >= 9) break;        // the block's last step holds 9 mod TPS taps
+      const int koff = t * Cin + cb * BK;  // k offset (elements) of the tap in a weight row
+      char* dst = bring + st * BSTAGE + tt * TL::BSTAGE1;
 #pragma unroll
-    for (int j = 0; j < B_L_INS; ++j) {
-      const char* a = EPI >= 0                ? src[B_HM_INS + j] + (size_t)koff * 2
-                      : src[B_HM_INS + j] ? src[B_HM_INS + j] + (size_t)koff * 2
-                                          : zero;
-      __builtin_amdgcn_global_load_lds((gptr_t)a,
-                                       (lptr_t)(dst + TL::BHM + (wid * B_L_INS + j) * 1024), 16, 0,
-                                       0);
+      for (int j = 0; j < B_HM_INS; ++j) {
+        const char* a = EPI >= 0 ? src[j] + (size_t)koff * 4
+                                 : src[j] ? src[j] + (size_t)koff * 4 : zero;
+        __builtin_amdgcn_global_load_lds((gptr_t)a, (lptr_t)(dst + (wid * B_HM_INS + j) * 1024),
+                                         16, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < B_L_INS; ++j) {
+        const char* a = EPI >= 0                ? src[B_HM_INS + j] + (size_t)koff * 2
+                        : src[B_HM_INS + j] ? src[B_HM_INS + j] + (size_t)koff * 2
+                                            : zero;
+        __builtin_amdgcn_global_load_lds((gptr_t)a,
+                                         (lptr_t)(dst + TL::BHM + (wid * B_L_INS + j) * 1024), 16,
+                                         0, 0);
+      }
     }
   };
   auto issue_h = [&](int cb, int j, int buf) {  // H-wave: its halo piece j of channel block cb
@@ -236,58 +250,64 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
     int st = 0;
     for (int cb = 0; cb < ncb; ++cb) {
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int s = cb * 9 + t;
-        // opaque per tap: keeps (table ^ half) and (buffer + table) from being hoisted out of the
-        // unrolled taps as 54 more live registers
+      for (int tg = 0; tg < NG; ++tg) {
+        const int s = cb * NG + tg;
+        // opaque per step: keeps (table ^ half) and (buffer + table) from being hoisted out of
+        // the unrolled taps as 54 more live registers
         int hoff = (cb & 1) * HBUF, x1 = 64, x2 = 32;
         asm volatile("" : "+s"(hoff), "+s"(x1), "+s"(x2));
         const char* ha = hbuf + hoff;
-        const int dy = t / 3, dx = t % 3;
-        const char* sb = bring + st * BSTAGE;
+        const char* sb0 = bring + st * BSTAGE;
         if (bwave && s + 1 < nk) issue_b(s + 1, st ^ 1);
-        if (!bwave && cb + 1 < ncb && t < (H_INS + HPS - 1) / HPS) {
+        if (!bwave && cb + 1 < ncb && tg < (H_INS + HPS - 1) / HPS) {
 #pragma unroll
           for (int q = 0; q < HPS; ++q) {
-            const int j = t * HPS + q;
+            const int j = tg * HPS + q;
             if (j < H_INS && j < my_pieces) issue_h(cb + 1, j, (cb + 1) & 1);
           }
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int ch = h * 4 + fq;
-          u32x4 ahm[FM], bhm[FN];
-          u32x2 al[FM], blo[FN];
+        for (int tt = 0; tt < TPS; ++tt) {
+          const int t = tg * TPS + tt;
+          if (t >= 9) break;
+          const int dy = t / 3, dx = t % 3;
+          const char* sb = sb0 + tt * TL::BSTAGE1;
 #pragma unroll
-          for (int i = 0; i < FM; ++i) {
-            ahm[i] = *(const u32x4*)(ha + (h ? oh[i + dy][dx] ^ x1 : oh[i + dy][dx]));
-            al[i] = *(const u32x2*)(lbuf + (h ? ol[i + dy][dx] ^ x2 : ol[i + dy][dx]));
+          for (int h = 0; h < 2; ++h) {
+            const int ch = h * 4 + fq;
+            u32x4 ahm[FM], bhm[FN];
+            u32x2 al[FM], blo[FN];
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+              ahm[i] = *(const u32x4*)(ha + (h ? oh[i + dy][dx] ^ x1 : oh[i + dy][dx]));
+              al[i] = *(const u32x2*)(lbuf + (h ? ol[i + dy][dx] ^ x2 : ol[i + dy][dx]));
+            }
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+              const int row = wn * FN * 16 + 16 * j + frow;
+              bhm[j] = *(const u32x4*)(sb + row * ROWB + ((ch ^ fsw(row)) << 4));
+              blo[j] = *(const u32x2*)(sb + TL::BHM + row * TL::LROWB + ((ch ^ lsw(row)) << 3));
+            }
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+              for (int j = 0; j < FN; ++j)
+                acc[i][j] = mfma_x6(bhm[j], blo[j], ahm[i], al[i], acc[i][j]);  // D[ch][px]
+            __builtin_amdgcn_s_setprio(0);
           }
-#pragma unroll
-          for (int j = 0; j < FN; ++j) {
-            const int row = wn * FN * 16 + 16 * j + frow;
-            bhm[j] = *(const u32x4*)(sb + row * ROWB + ((ch ^ fsw(row)) << 4));
-            blo[j] = *(const u32x2*)(sb + TL::BHM + row * TL::LROWB + ((ch ^ lsw(row)) << 3));
-          }
-          __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-          for (int i = 0; i < FM; ++i)
-#pragma unroll
-            for (int j = 0; j < FN; ++j)
-              acc[i][j] = mfma_x6(bhm[j], blo[j], ahm[i], al[i], acc[i][j]);  // D[ch][px]
-          __builtin_amdgcn_s_setprio(0);
         }
 #ifdef MIA_STAMPS
         const unsigned long long w0 = __builtin_amdgcn_s_memtime();
 #endif
-        if (bwave || t == 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (bwave || tg == NG - 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
 #ifdef MIA_STAMPS
         st_wb += __builtin_amdgcn_s_memtime() - w0;
 #endif
-        if (t == 8 && cb + 1 < ncb) {
+        if (tg == NG - 1 && cb + 1 < ncb) {
 #ifdef MIA_STAMPS
           const unsigned long long c0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -422,15 +442,16 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
 #endif
 }
 
-template <int BN_, bool PRO, int EPI, bool EARLY, bool PRIO = false, bool UNR = false>
+template <int BN_, bool PRO, int EPI, bool EARLY, bool PRIO = false, bool UNR = false,
+          int TPS = 1>
 static int launch_x6_e(ConvK& k, hipStream_t st) {
-  typedef HaloX6<BN_> TL;
+  typedef HaloX6<BN_, TPS> TL;
   k.nbn = (k.a.Cout + TL::BN - 1) / TL::BN;
   k.nblk = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW) * k.nbn;
   size_t lds = TL::LDS;
   lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
   lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
-  auto fn = conv_halo_x6_kernel<BN_, PRO, EPI, EARLY, PRIO, UNR>;
+  auto fn = conv_halo_x6_kernel<BN_, PRO, EPI, EARLY, PRIO, UNR, TPS>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -457,7 +478,12 @@ static int launch_x6_(ConvK& k, hipStream_t st) {
   // issuing it between the two MFMA halves) + s_setprio(1) around each MFMA block (+1-4 %): the
   // wave in its MFMA phase keeps issue priority over the co-resident wave's LDS reads
   if constexpr (EPI >= 0) {  // + the taps unrolled with lane-constant fragment offsets
-    if (tune(T_X6_UNR) != 0) return launch_x6_e<BN_, PRO, EPI, true, true, true>(k, st);
+    // T_X6_UNR = 2 (default): the 64-column tile takes two taps per K-step (HaloX6 TPS)
+    const int u = tune(T_X6_UNR);
+    if constexpr (BN_ == 64) {
+      if (u == 2) return launch_x6_e<BN_, PRO, EPI, true, true, true, 2>(k, st);
+    }
+    if (u != 0) return launch_x6_e<BN_, PRO, EPI, true, true, true>(k, st);
   }
   return launch_x6_e<BN_, PRO, EPI, true, true>(k, st);  // the rolled loop (T_X6_UNR = 0)
 }

@@ -79,7 +79,8 @@ enum TuneKey {
   T_CONV_HALO,       // 0: the 2-byte stride-1 convs on the generic tile instead of the halo tile
   T_CONV_X6,         // 0: the fp32 convs on the on-the-fly split kernels instead of split-once
   T_HALO_EPI,        // halo tiles' epilogue: 0 LDS-staged, 1 specialised (default), 2 runtime
-  T_X6_UNR,          // 0: the x6 halo kernel's rolled tap loop
+  T_X6_UNR,          // x6 halo kernel: 0 rolled tap loop, 1 unrolled taps, 2 (default) + two
+                     // taps per K-step on the 64-column tile
   T_X6_64AUX,        // 1: the 64-column x6 tile for the tap-pair launches too
   T_CONV_THIN,       // 0: no thin-channel input-layer kernels
   T_CONV_THIN32,     // 0: no 32-channel thin kernel

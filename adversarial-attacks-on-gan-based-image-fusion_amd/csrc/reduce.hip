@@ -29,7 +29,7 @@ struct TuneDef {
   int value;
 };
 TuneDef g_tune[T_NKEYS] = {
-    {"MIA_CONV_HALO", 1}, {"MIA_CONV_X6", 1},       {"MIA_HALO_EPI", 1},    {"MIA_X6_UNR", 1},
+    {"MIA_CONV_HALO", 1}, {"MIA_CONV_X6", 1},       {"MIA_HALO_EPI", 1},    {"MIA_X6_UNR", 2},
     {"MIA_X6_64AUX", 0},  {"MIA_CONV_THIN", 1},     {"MIA_CONV_THIN32", 1}, {"MIA_CONV_WRES", 1},
     {"MIA_CONV_TILE", 0}, {"MIA_CONV_REGEPI", 1},   {"MIA_CONV_SMALLTILE", 512},
     {"MIA_S2DG_X6", 1},   {"MIA_S2DG_HALO", 1},     {"MIA_UPCONV_X6", 1},   {"MIA_UPCONV_HALO", 1},

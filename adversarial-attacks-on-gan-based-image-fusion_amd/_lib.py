@@ -154,6 +154,8 @@ SIGNATURES = {
     "mia_repeat": (c_int, [P, P, c_int64, c_int, P]),
     "mia_memset": (c_int, [P, c_int, c_int64, P]),
     "mia_conv2d_kpad": (c_int, [c_int, c_int, c_int]),
+    "mia_conv2d_planes": (c_int, [ctypes.POINTER(ConvArgs), c_int, ctypes.POINTER(ConvGroup),
+                                  c_int, c_int, c_int, c_int64, c_int, P]),
     "mia_conv2d": (c_int, [ctypes.POINTER(ConvArgs), c_int, ctypes.POINTER(ConvGroup), c_int,
                            c_int, c_int, c_int, P]),
     "mia_conv2d_batched": (c_int, [ctypes.POINTER(ConvArgs), c_int, ctypes.POINTER(ConvGroup),

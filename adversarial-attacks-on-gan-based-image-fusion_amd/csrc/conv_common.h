@@ -44,11 +44,27 @@ struct ConvK {
   float* red_part;
   int red_nslots, red_count;     // slots per output; outputs per quantity (N·Cout)
   int red_px;                    // LDS-staged epilogue: one slot per output pixel (small images)
+  int ysplit;                    // > 0: output channel co goes to plane co / ysplit, channel
+  int64_t yplane;                // co % ysplit; planes yplane elements apart (mia_conv2d_planes)
   int64_t wn;                    // elements between the images' weight matrices (0: one shared
                                  // [Cout][Kpad]; > 0: per-image modulated weights, mia_conv3x3_wmod,
                                  // the 2-byte halo kernel only)
   ConvGroup g[MIA_MAX_GROUPS];
 };
+
+// Output base of a block whose columns start at n0 (all inside one plane: ysplit is a multiple of
+// every tile width): y + plane·yplane − plane·ysplit, so that y + m·ystride + co lands at
+// (plane, m, co − plane·ysplit) with ystride = ysplit.
+template <typename T>
+__device__ __forceinline__ T* y_base(const ConvK& k, int n0) {
+  T* y = (T*)k.a.y;
+  if (k.ysplit > 0 && y) {
+    const int pl = n0 / k.ysplit;
+    y += pl * (k.yplane - k.ysplit);
+  }
+  return y;
+}
+
 
 // the partial of quantity q (0 sdot, 1 bab_q, 2 csum) of contributor `slot` to output i = n·Cout+c
 __device__ __forceinline__ void red_put(const ConvK& k, int q, int slot, int i, float v) {
@@ -353,7 +369,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvK& k, const ConvGroup& G
   const T* TA = (const T*)p.tap_a;
   const T* TT = (const T*)p.tap_t;
   const T* MA = (const T*)p.mask_a;
-  T* __restrict__ Y = (T*)p.y;
+  T* __restrict__ Y = y_base<T>(k, n0);
   float part[8], partq[8], pcs[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) part[e] = partq[e] = pcs[e] = 0.f;

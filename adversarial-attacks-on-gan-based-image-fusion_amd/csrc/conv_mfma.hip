@@ -624,7 +624,7 @@ extern "C" int mia_conv2d_kpad(int taps, int cin, int dtype) { return kpad_for(t
 
 static int conv2d_impl(const mia_conv_args* args, int stride, const mia_conv_group* groups,
                        const mia_conv_batch* batch, int ngroups, int out_h, int out_w, int dtype,
-                       void* stream);
+                       void* stream, int ysplit = 0, int64_t yplane = 0);
 
 extern "C" int mia_conv2d(const mia_conv_args* args, int stride, const mia_conv_group* groups,
                           int ngroups, int out_h, int out_w, int dtype, void* stream) {
@@ -644,9 +644,28 @@ extern "C" int mia_conv2d_batched(const mia_conv_args* args, int stride,
   return conv2d_impl(args, stride, groups, batch, ngroups, out_h, out_w, dtype, stream);
 }
 
+extern "C" int mia_conv2d_planes(const mia_conv_args* args, int stride,
+                                 const mia_conv_group* groups, int out_h, int out_w,
+                                 int plane_channels, int64_t plane_stride, int dtype,
+                                 void* stream) {
+  MIA_CHECK_ARG(args != nullptr && groups != nullptr, "null args");
+  const mia_conv_args& a = *args;
+  MIA_CHECK_ARG(stride == 2, "plane-split output: the stride-2 convs (generic tile) only");
+  MIA_CHECK_ARG(plane_channels > 0 && plane_channels % 128 == 0 && a.Cout % plane_channels == 0,
+                "plane_channels must be a multiple of 128 dividing Cout");
+  MIA_CHECK_ARG(a.y_cstride == 0 || a.y_cstride == plane_channels, "y_cstride = plane_channels");
+  MIA_CHECK_ARG(plane_stride >= (int64_t)a.N * out_h * out_w * plane_channels,
+                "plane_stride < N·out_h·out_w·plane_channels");
+  MIA_CHECK_ARG(a.y && !a.sdot && !a.bab_demod && !a.csum && !a.mask_a && !a.tap_a && !a.aux_x &&
+                    !a.accumulate && !a.out_scale && !a.noise,
+                "plane-split output: bias / act epilogues only");
+  return conv2d_impl(args, stride, groups, nullptr, 1, out_h, out_w, dtype, stream,
+                     plane_channels, plane_stride);
+}
+
 static int conv2d_impl(const mia_conv_args* args, int stride, const mia_conv_group* groups,
                        const mia_conv_batch* batch, int ngroups, int out_h, int out_w, int dtype,
-                       void* stream) {
+                       void* stream, int ysplit, int64_t yplane) {
   MIA_CHECK_ARG(args != nullptr && groups != nullptr, "null args");
   MIA_CHECK_ARG(stride == 1 || stride == 2, "stride 1 or 2");
   MIA_CHECK_ARG(out_h > 0 && out_w > 0, "empty output");
@@ -661,7 +680,10 @@ static int conv2d_impl(const mia_conv_args* args, int stride, const mia_conv_gro
   k.WT = out_w;
   k.cout_mod = a.Cout;
   k.ystride = a.y_cstride > 0 ? a.y_cstride : a.Cout;
-  MIA_CHECK_ARG(k.ystride >= a.Cout, "y_cstride < Cout");
+  k.ysplit = ysplit;
+  k.yplane = yplane;
+  if (ysplit > 0) k.ystride = ysplit;  // each plane holds ysplit channels per pixel
+  MIA_CHECK_ARG(ysplit > 0 || k.ystride >= a.Cout, "y_cstride < Cout");
   for (int g = 0; g < ngroups; ++g) {
     const mia_conv_group& s = groups[g];
     ConvGroup& G = k.g[g];

@@ -34,7 +34,7 @@ __device__ __forceinline__ void halo_epilogue(const ConvK& k, const f32x4 (&acc)
   const T* TA = (const T*)p.tap_a;
   const T* TT = (const T*)p.tap_t;
   const T* MA = (const T*)p.mask_a;
-  T* __restrict__ Y = (T*)p.y;
+  T* __restrict__ Y = y_base<T>(k, n0);
   const bool bab = p.bab_demod != nullptr;
   float osc[FN][4], bia[FN][4], dmv[FN][4], bbv[FN][4], part[FN][4], partq[FN][4];
   float msl[FN][4], asl[FN][4], pcs[FN][4];
@@ -278,7 +278,7 @@ __device__ __forceinline__ void halo_epilogue_f(
   const int H = Hg < 0 ? p.H : Hg, W = Hg < 0 ? p.W : Wg, Cout = p.Cout;
   const int px = lane & 15, lrow = lane >> 4;
   const int cl = n0 + wn * FN * 16 + (lrow << 2);
-  T* __restrict__ Y = (T*)p.y;
+  T* __restrict__ Y = y_base<T>(k, n0);
   const T* AX = (const T*)p.aux_x;
   const T* TA = (const T*)p.tap_a;
   const T* TT = (const T*)p.tap_t;

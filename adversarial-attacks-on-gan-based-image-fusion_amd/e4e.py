@@ -44,6 +44,9 @@ from .weights import (E4E_COARSE, E4E_MIDDLE, E4E_SE_REDUCTION, STYLE_DIM, e4e_s
 
 BN_EPS = 1e-5
 BATCH_MAX = 16  # groups per mia_conv2d_batched launch
+# the style heads' first convs, one launch per FPN source map (mia_conv2d_planes) instead of one
+# per head; 0 = per head (A/B: MIA_E4E_MERGE_HEADS)
+MERGE_HEADS = int(__import__("os").environ.get("MIA_E4E_MERGE_HEADS", "1"))
 
 
 def _bn_fold(p, pre):
@@ -195,6 +198,22 @@ class E4EEncoder:
                     (idx[c:c + 8], torch.cat([self.heads[i]["convs"][0]["wdh"]
                                               for i in idx[c:c + 8]]).contiguous())
                     for c in range(0, len(idx), 8)]
+        # the heads whose first conv reads the same FPN map, as ONE stride-2 conv with their weights
+        # and biases concatenated along Cout; head j's 512 output channels land in its slot of the
+        # stacked level buffer (mia_conv2d_planes; slots of one source are consecutive)
+        self.src_fwd = {}
+        if MERGE_HEADS:
+            for src in ("c3", "p2", "p1"):
+                idx = [i for i, hd in enumerate(self.heads) if hd["src"] == src]
+                if len(idx) < 2:
+                    continue
+                r = self.heads[idx[0]]["res"][0]
+                k0 = self.slot[r][idx[0]]
+                if [self.slot[r][i] for i in idx] != list(range(k0, k0 + len(idx))):
+                    continue
+                self.src_fwd[src] = (idx, k0, r,
+                                     torch.cat([self.heads[i]["convs"][0]["w"] for i in idx]),
+                                     torch.cat([self.heads[i]["convs"][0]["b"] for i in idx]))
         # w = w0 + delta_i: the linear biases of rows i ≥ 1 include style 0's; the backward of
         # style 0 reads the sum of every row (mia_sum_slices)
         b0l = self.heads[0]["lb"]
@@ -314,7 +333,14 @@ class E4EEncoder:
         self._feats = feats
         # style heads: the first conv of each head from its FPN map into the head's slot of the
         # stacked level buffer, then one batched launch per resolution level
+        for src, (idx, k0, r, wcat, bcat) in self.src_fwd.items():
+            ops.conv2d_planes(feats[src], wcat, bcat,
+                              self._level_buf(ws, "a", r, N)[k0 * N:(k0 + len(idx)) * N], (r, r),
+                              planes=len(idx), act_out=ACT_PRELU, act_slope=self.slope_cat)
+        merged = {i for idx, *_ in self.src_fwd.values() for i in idx}
         for i, hd in enumerate(self.heads):
+            if i in merged:
+                continue
             x = feats[hd["src"]]
             cv = hd["convs"][0]
             r = hd["res"][0]

@@ -848,6 +848,43 @@ def conv2d_batched(x, groups, y, out_hw, *, n, cout, stride=1, bias=None, act_ou
     return y
 
 
+def conv2d_planes(x, w, b, y, out_hw, *, planes, act_out=ACT_NONE, act_slope=None, flops=None):
+    """mia_conv2d_planes: one stride-2 pad-1 3×3 conv over x (N,H,W,Cin) with Cout = planes·C
+    (w: [planes·C][Kpad], the heads' matrices concatenated along Cout; b: planes·C), output
+    plane p (channels p·C … p·C+C−1) written to y[p·N:(p+1)·N] of y (planes·N, oh, ow, C)."""
+    N, H, W, Cin = x.shape
+    T = x.dtype
+    oh, ow = out_hw
+    P = int(planes)
+    C = y.shape[-1]
+    cout = P * C
+    _need(y, (P * N, oh, ow, C), T, "y")
+    _need(w, (cout, conv2d_kpad(9, Cin, T)), T, "w")
+    _numel_ok(b, cout, torch.float32, "b")
+    if act_out == ACT_PRELU and (act_slope is None or act_slope.numel() < cout):
+        raise ValueError("ACT_PRELU needs act_slope of Cout entries")
+    wsp = layouts.split_for(w) if T == torch.float32 else None
+    g = _lib.ConvGroup(ptr(w).value, 3, 3, 1, 1, oh, ow, 1, 0, 1, 0,
+                       ptr(wsp).value if wsp is not None else None)
+    a = ConvArgs()
+    a.x, a.y = ptr(x), ptr(y)
+    a.N, a.H, a.W, a.Cin, a.Cout = N, H, W, Cin, cout
+    a.y_cstride = C
+    a.bias = ptr(b)
+    a.act_out, a.act_slope = act_out, ptr(act_slope)
+    prof = PROFILE
+    if prof is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    call("mia_conv2d_planes", ctypes.byref(a), 2, ctypes.byref(g), oh, ow, C, N * oh * ow * C,
+         dt(T), stream())
+    if prof is not None:
+        e1.record()
+        prof.append((e0, e1, flops if flops is not None else 2 * N * oh * ow * 9 * Cin * cout))
+        _tag(f"conv2d_planes {H}x{W} {Cin}->{C} s2 x{P}")
+    return y
+
+
 def se_fwd(csum, w1, w2, u, s, hw):
     N, C = csum.shape
     Cr = w1.shape[0]

@@ -191,6 +191,17 @@ typedef struct mia_conv_group {
 int mia_conv2d_kpad(int taps, int cin, int dtype);
 int mia_conv2d(const mia_conv_args* args, int stride, const mia_conv_group* groups, int ngroups,
                int out_h, int out_w, int dtype, void* stream);
+/* One stride-2 conv whose Cout = P·plane_channels output channels land in P separate planes:
+ * channel co of output pixel (n, y, x) at y[(co / plane_channels)·plane_stride +
+ * ((n·out_h + y)·out_w + x)·plane_channels + co % plane_channels]. The first convs of the e4e
+ * GradualStyleBlocks that read one FPN map (psp_encoders Encoder4Editing.forward: 7 heads on p1,
+ * 4 on p2, 3 on c3; called via net.encoder at attack_main2.py:597,622) as ONE launch with the
+ * heads' weights / biases concatenated along Cout, each head's output in its slot of the stacked
+ * level buffer. plane_channels a multiple of 128; bias / act_out (PReLU: act_slope of Cout)
+ * epilogues only. */
+int mia_conv2d_planes(const mia_conv_args* args, int stride, const mia_conv_group* groups,
+                      int out_h, int out_w, int plane_channels, int64_t plane_stride, int dtype,
+                      void* stream);
 /* Up to 16 INDEPENDENT convs of one geometry family in one launch (the e4e GradualStyleBlock
  * convs of one resolution level across the style heads, psp_encoders GradualStyleBlock.forward,
  * reached through net.encoder at code/attack/attack_main2.py:597,622): group g is a conv with its

@@ -394,3 +394,41 @@ def test_attack_gradient_with_e4e_vs_oracle(cuda):
     L, gr = attack_ref.loss_grad(gp64, vp64, ep64, x.double(), refs, size)
     _grad_close(gd, gr, 3e-2, 0.995)  # mask-flip sensitivity: see _grad_close
     assert rel_err(eng.loss(x.to(cuda)).double(), L) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_style_head_first_convs_merged_per_source(cuda, dtype):
+    """The style heads' first convs as ONE stride-2 launch per FPN source map (mia_conv2d_planes:
+    the heads' weights / biases concatenated along Cout, head j's output in its slot of the level
+    buffer) compute exactly the per-head launches: every head activation and the latents are
+    bit-identical (the same tile and K order per output element); plus a direct check of the
+    plane placement against F.conv2d."""
+    N, S = 2, 256
+    enc = e4e.E4EEncoder(make_e4e_weights(S, seed=1), S, dtype=dtype, device=cuda)
+    assert set(enc.src_fwd) == {"c3", "p2", "p1"}
+    g = torch.Generator().manual_seed(9)
+    x = torch.zeros(N, S, S, CPAD, dtype=dtype)
+    x[..., :3] = (torch.rand(N, S, S, 3, generator=g) * 2 - 1).to(dtype)
+    x = x.to(cuda)
+    ws = Workspace(cuda)
+    lat = enc.forward_nhwc(x, ws).clone()
+    acts = {r: enc._level_buf(ws, "a", r, N).clone() for r in enc.slot}
+    saved, enc.src_fwd = enc.src_fwd, {}
+    lat1 = enc.forward_nhwc(x, ws).clone()
+    for r in enc.slot:
+        assert torch.equal(enc._level_buf(ws, "a", r, N), acts[r]), r
+    assert torch.equal(lat, lat1)
+    # the plane layout itself: 3 planes of 128 channels from one 384-channel conv
+    P, C, H, cin = 3, 128, 16, 64
+    xx = rnd((N, cin, H, H), 31)
+    w = rnd((P * C, cin, 3, 3), 32, math.sqrt(2 / (9 * cin)))
+    b = rnd((P * C,), 33, 0.1)
+    y = torch.full((P * N, H // 2, H // 2, C), float("nan"), dtype=dtype, device=cuda)
+    slope = torch.full((P * C,), 0.01, device=cuda)
+    ops.conv2d_planes(nhwc(xx, dtype, cuda), layouts.fwd_matrix(w, dtype).to(cuda),
+                      b.float().to(cuda), y, (H // 2, H // 2), planes=P, act_out=ops.ACT_PRELU,
+                      act_slope=slope)
+    ref = F.leaky_relu(F.conv2d(xx, w, b, stride=2, padding=1), 0.01)  # (N, P·C, h, w)
+    for p in range(P):
+        assert rel_err(nchw(y[p * N:(p + 1) * N]), ref[:, p * C:(p + 1) * C]) < TOL[dtype]
+    enc.src_fwd = saved

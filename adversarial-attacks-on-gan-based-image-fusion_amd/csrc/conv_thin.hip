@@ -225,7 +225,7 @@ struct Thin32Tile {
 };
 
 // the reductions of image n: the 16 pixel lanes by shuffles, then one partial per channel into the
-// wave's slot for image n (its index among the waves whose runs meet image n)
+// work item's slot of image n (its chunk index: fixed by the image shape, not by N or the grid)
 template <int EPI>
 __device__ __forceinline__ void thin32_flush(const ConvK& k, EpiSums<2>& sums, int n, int slot,
                                              int frow, int fq) {
@@ -247,6 +247,9 @@ __device__ __forceinline__ void thin32_flush(const ConvK& k, EpiSums<2>& sums, i
     }
 }
 
+// 16-pixel groups per work item (= per reduction slot) of the 32-channel kernel
+constexpr int THIN32_CHUNK = 64;
+
 template <typename T, bool PRO, int EPI>
 __global__ __launch_bounds__(256) void conv_thin32_kernel(const ConvK k) {
   typedef typename Vec<T>::type VT;
@@ -266,16 +269,16 @@ __global__ __launch_bounds__(256) void conv_thin32_kernel(const ConvK k) {
     for (int j = 0; j < 2; ++j) wr[t][j] = *(const VT*)(Wt + (size_t)(16 * j + frow) * kpad + t * 32 + fq * 8);
   const bool lrelu_in = p.act_in == MIA_ACT_LRELU_S2;
   const int gpr = W / 16, gpi = H * gpr;
-  const int64_t ngroups = (int64_t)p.N * gpi;
-  // contiguous run of groups per wave (stays inside one image for the reductions)
-  const int64_t per = (ngroups + nwaves - 1) / nwaves;
-  const int64_t g0 = (int64_t)wave * per, g1 = g0 + per < ngroups ? g0 + per : ngroups;
+  // work items: THIN32_CHUNK consecutive 16-pixel groups of ONE image; item (n, c) adds its sums
+  // into slot c of image n. The partition depends on the image's shape only — not on N or on the
+  // grid — so an image's sums do not depend on the other images of the call (mia_common.h RedQ)
+  const int S = (gpi + THIN32_CHUNK - 1) / THIN32_CHUNK;
+  const int64_t nitems = (int64_t)p.N * S;
   EpiSums<TL::FN> sums;
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) sums.part[j][e] = sums.partq[j][e] = sums.pcs[j][e] = 0.f;
-  int cur_n = -1;
   VT sv;
   // the 9 A gathers of group g (issued one group ahead: they land during the previous group's
   // MFMAs and epilogue)
@@ -292,38 +295,34 @@ __global__ __launch_bounds__(256) void conv_thin32_kernel(const ConvK k) {
     }
   };
   VT a_cur[9], a_nxt[9];
-  if (g0 < g1) gather(g0, a_cur);
-  for (int64_t g = g0; g < g1; ++g) {
-    const int n = (int)(g / gpi);
-    const int rem = (int)(g - (int64_t)n * gpi);
-    const int y = rem / gpr, x0 = (rem - y * gpr) * 16;
-    if (g + 1 < g1) gather(g + 1, a_nxt);
-    if (n != cur_n) {
-      if constexpr (RED) {
-        if (cur_n >= 0) thin32_flush<EPI>(k, sums, cur_n, wave - (int)(cur_n * gpi / per), frow, fq);
-      }
-      cur_n = n;
-      if constexpr (PRO) {
-        const float mul = lrelu_in ? SQRT2 : 1.f;
+  for (int64_t it = wave; it < nitems; it += nwaves) {
+    const int n = (int)(it / S), c = (int)(it - (int64_t)n * S);
+    const int64_t g0 = (int64_t)n * gpi + (int64_t)c * THIN32_CHUNK;
+    const int64_t g1 = g0 + min(THIN32_CHUNK, gpi - c * THIN32_CHUNK);
+    if constexpr (PRO) {
+      const float mul = lrelu_in ? SQRT2 : 1.f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) sv[e] = from_f<T>(p.in_scale[(size_t)n * 32 + fq * 8 + e] * mul);
-      }
+      for (int e = 0; e < 8; ++e) sv[e] = from_f<T>(p.in_scale[(size_t)n * 32 + fq * 8 + e] * mul);
     }
-    f32x4 acc[1][2] = {{f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}}};
+    gather(g0, a_cur);
+    for (int64_t g = g0; g < g1; ++g) {
+      const int rem = (int)(g - (int64_t)n * gpi);
+      const int y = rem / gpr, x0 = (rem - y * gpr) * 16;
+      if (g + 1 < g1) gather(g + 1, a_nxt);
+      f32x4 acc[1][2] = {{f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}}};
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      VT a = a_cur[t];
-      if constexpr (PRO) modulate<T>(a, sv, lrelu_in);
+      for (int t = 0; t < 9; ++t) {
+        VT a = a_cur[t];
+        if constexpr (PRO) modulate<T>(a, sv, lrelu_in);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[0][j] = mfma_chunk<T>(wr[t][j], a, acc[0][j]);
+        for (int j = 0; j < 2; ++j) acc[0][j] = mfma_chunk<T>(wr[t][j], a, acc[0][j]);
+      }
+      halo_epilogue_f<T, TL, EPI>(k, acc, n, y, x0, 0, 0, 0, lane, -1, -1, nullptr, nullptr, 1, 0,
+                                  RED ? &sums : nullptr);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) a_cur[t] = a_nxt[t];
     }
-    halo_epilogue_f<T, TL, EPI>(k, acc, n, y, x0, 0, 0, 0, lane, -1, -1, nullptr, nullptr, 1, 0,
-                                RED ? &sums : nullptr);
-#pragma unroll
-    for (int t = 0; t < 9; ++t) a_cur[t] = a_nxt[t];
-  }
-  if constexpr (RED) {
-    if (cur_n >= 0) thin32_flush<EPI>(k, sums, cur_n, wave - (int)(cur_n * gpi / per), frow, fq);
+    if constexpr (RED) thin32_flush<EPI>(k, sums, n, c, frow, fq);
   }
 }
 
@@ -737,13 +736,10 @@ bool conv_thin32_eligible(const ConvK& k, int dtype) {
 
 template <typename T, bool PRO, int F>
 static int launch_thin32_(ConvK& k, int grid, hipStream_t st) {
-  // the waves walk contiguous runs of `per` 16-pixel groups: the waves meeting image n are
-  // wave (n·gpi)/per … , at most gpi/per + 2 of them (slots without a contributor stay 0)
+  // one slot per THIN32_CHUNK-group work item of an image (every slot has its contributor)
   const int64_t gpi = (int64_t)k.a.H * (k.a.W / 16);
-  const int64_t nwaves = (int64_t)grid * 4;
-  const int64_t per = ((int64_t)k.a.N * gpi + nwaves - 1) / nwaves;
   RedQ r;
-  int rc = conv_red_begin(k, r, (int)(gpi / per + 2), st, true);
+  int rc = conv_red_begin(k, r, (int)((gpi + THIN32_CHUNK - 1) / THIN32_CHUNK), st, false);
   if (rc != MIA_OK) return rc;
   hipLaunchKernelGGL((conv_thin32_kernel<T, PRO, F>), dim3(grid), dim3(256), 0, st, k);
   rc = check_launch("conv_thin32");

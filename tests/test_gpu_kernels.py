@@ -1012,6 +1012,40 @@ def test_conv_thin32_layers(cuda, tune, dtype, N, H, W, mode, path):
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("H,W", [(40, 48), (256, 256)])
+def test_conv_thin32_sums_batch_independent(cuda, tune, dtype, H, W):
+    """conv_thin32_kernel (MIA_CONV_WRES32=0): the sdot sums of an image come from work items of
+    a fixed number of 16-pixel groups of that image (slot = chunk index), so they are
+    bit-identical whether the image is attacked alone or in a batch of 5, and run to run
+    (the per-wave partition used to depend on N and the grid)."""
+    tune("MIA_CONV_WRES32", 0)
+    C, N = 32, 5
+    g = torch.Generator().manual_seed(H + W)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
+    s = torch.rand(N, C, generator=g) + 0.5
+    aux = torch.randn(N, C, H, W, generator=g)
+    wf = layouts.fwd_matrix(w, dtype).to(cuda)
+
+    def run(lo, hi):
+        n = hi - lo
+        y = torch.empty(n, H, W, C, dtype=dtype, device=cuda)
+        sd = torch.zeros(n, C, device=cuda)
+        ops.conv3x3(nhwc(x[lo:hi], dtype).to(cuda), wf, y, cout=C, out_scale=s[lo:hi].to(cuda),
+                    aux_x=nhwc(aux[lo:hi], dtype).to(cuda), sdot=sd)
+        torch.cuda.synchronize()
+        return y, sd
+
+    y_all, sd_all = run(0, N)
+    y2, sd2 = run(0, N)
+    assert torch.equal(sd_all, sd2) and torch.equal(y_all, y2)
+    for i in (0, 3, N - 1):
+        y1, sd1 = run(i, i + 1)
+        assert torch.equal(sd1, sd_all[i:i + 1]), i
+        assert torch.equal(y1, y_all[i:i + 1]), i
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("N,H,W", [(2, 32, 48), (3, 16, 16), (5, 64, 32)])
 @pytest.mark.parametrize("mode", ["mod", "mod_lrelu_in", "sdot", "sdot_acc", "sdot_bab",
                                   "sdot_acc_bab", "plain", "acc"])

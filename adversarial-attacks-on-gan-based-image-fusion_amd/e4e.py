@@ -45,8 +45,14 @@ from .weights import (E4E_COARSE, E4E_MIDDLE, E4E_SE_REDUCTION, STYLE_DIM, e4e_s
 BN_EPS = 1e-5
 BATCH_MAX = 16  # groups per mia_conv2d_batched launch
 # the style heads' first convs, one launch per FPN source map (mia_conv2d_planes) instead of one
-# per head; 0 = per head (A/B: MIA_E4E_MERGE_HEADS)
+# per head, where a per-head launch has fewer 128×128 output tiles than MERGE_BELOW_TILES (less
+# than one wave of blocks on the chip): measured (fp32, 128 images, profiles/r04_layers_*) the
+# c3 heads (16² → 8², 256 tiles per head) 15.9 → 12.4 ms per step merged, the p2 heads (1024
+# tiles) 63.5 → 63.5, the p1 heads (4096 tiles) 461.7 → 476.4 (the merged launch's 28 column
+# tiles per row tile cycle 99 MB of pre-split weights through L2). 0 = never (A/B:
+# MIA_E4E_MERGE_HEADS).
 MERGE_HEADS = int(__import__("os").environ.get("MIA_E4E_MERGE_HEADS", "1"))
+MERGE_BELOW_TILES = 1024
 
 
 def _bn_fold(p, pre):
@@ -333,11 +339,14 @@ class E4EEncoder:
         self._feats = feats
         # style heads: the first conv of each head from its FPN map into the head's slot of the
         # stacked level buffer, then one batched launch per resolution level
+        merged = set()
         for src, (idx, k0, r, wcat, bcat) in self.src_fwd.items():
+            if -(-N * r * r // 128) * (STYLE_DIM // 128) >= MERGE_BELOW_TILES:
+                continue  # enough tiles per head: one launch per head
+            merged.update(idx)
             ops.conv2d_planes(feats[src], wcat, bcat,
                               self._level_buf(ws, "a", r, N)[k0 * N:(k0 + len(idx)) * N], (r, r),
                               planes=len(idx), act_out=ACT_PRELU, act_slope=self.slope_cat)
-        merged = {i for idx, *_ in self.src_fwd.values() for i in idx}
         for i, hd in enumerate(self.heads):
             if i in merged:
                 continue

@@ -83,6 +83,31 @@ def vgg_forward(params, image):
     return c11, c12, c32, out
 
 
+def branch_masks(params, image):
+    """The ReLU positive sets and pool-window argmax one-hots (first maximum in row-major window
+    order, ceil-mode windows padded with −inf) that vgg_forward takes on ``image`` in image's own
+    dtype — e.g. the branches of a torch CPU fp32 run, for forced_masks."""
+    m, out = {}, image
+    pools = {"conv1_2": ("pool1", False), "conv2_2": ("pool2", False), "conv3_3": ("pool3", True)}
+    with torch.no_grad():
+        for name in LAYERS:
+            w, b = params[name]
+            pre = F.conv2d(out, w.to(out.dtype), b.to(out.dtype), padding=1)
+            m[name] = pre > 0
+            out = F.relu(pre)
+            if name in pools:
+                pn, ceil = pools[name]
+                N, C, H, W = out.shape
+                xp = F.pad(out, (0, W % 2, 0, H % 2), value=float("-inf"))
+                Hp, Wp = xp.shape[2], xp.shape[3]
+                win = xp.reshape(N, C, Hp // 2, 2, Wp // 2, 2).permute(0, 1, 2, 4, 3, 5)
+                oh = F.one_hot(win.reshape(N, C, Hp // 2, Wp // 2, 4).argmax(-1), 4).bool()
+                oh = oh.reshape(N, C, Hp // 2, Wp // 2, 2, 2).permute(0, 1, 2, 4, 3, 5)
+                m[pn] = oh.reshape(N, C, Hp, Wp)[:, :, :H, :W]
+                out = F.max_pool2d(out, 2, 2, ceil_mode=ceil)
+    return m
+
+
 def tap_mse_grad(params, image, targets):
     """Input gradient of Σ_k MSE(tap_k(image), target_k) (mean reduction, as interpolation.py:766)."""
     x = image.clone().requires_grad_(True)

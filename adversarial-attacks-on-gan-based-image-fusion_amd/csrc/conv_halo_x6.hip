@@ -488,6 +488,270 @@ static int launch_x6_(ConvK& k, hipStream_t st) {
   return launch_x6_e<BN_, PRO, EPI, true, true>(k, st);  // the rolled loop (T_X6_UNR = 0)
 }
 
+// ---- the 64-channel layers, two blocks per CU (round 4) ---------------------------------------
+// The 64-column tile above runs one 8-wave block per CU: its 18-step K loop (Cin = 64) leaves the
+// prologue (first halo from HBM + split, 15 % of a block), the epilogue (7 %) and every per-step
+// barrier exposed — the two waves of a SIMD belong to the same block and stall together (stamps:
+// loop at 64 % of its MFMA-only bound). Here a block is an 8 × 16 patch × 64 channels on 4 waves
+// (4 row waves of 2 × 4 fragments, the same wave tile), LDS = ONE halo buffer (raw, split in place)
+// + lo + a 2-stage pre-split weight ring = 58 KB, so two blocks share a CU and each one's halo
+// waits, splits, barriers and epilogue run under the other's MFMAs (the 2-byte halo kernel's
+// 8 × 16 / 2-blocks-per-CU arrangement). Every wave streams a share of the weights (3 pieces per
+// K-step); the next channel block's halo is fetched by all waves after the last tap of the current
+// one (single buffer). Same MFMAs in the same order per output as the 8-wave tile (bit-identical).
+struct HaloX6S {
+  static constexpr int PH = 8, PW = 16, NW = 4, NT = 64 * NW;
+  static constexpr int WN = 1, WM = 4, FM = 2, FN = 4;
+  static constexpr int BM = PH * PW, BN = 64, BK = 32;
+  static constexpr int HSIDE = PW + 2, HROWS = (PH + 2) * HSIDE;  // 180 halo pixels
+  static constexpr int HPIECES = (HROWS + 7) / 8;                 // 23 pieces of 8 rows
+  static constexpr int HBUF = HPIECES * 1024;
+  static constexpr int LROWB = 64, LBUF = HROWS * LROWB;
+  static constexpr int BHM = BN * ROWB, BL = BN * LROWB, BSTAGE = BHM + BL;  // 12 KB
+  static constexpr int B_HM_INS = BN / 8 / NW, B_L_INS = BN / 16 / NW;      // 2 + 1 per wave
+  static constexpr int H_INS = (HPIECES + NW - 1) / NW;                      // 6
+  static constexpr int EROWS = 128, ES = BN + 4;
+  static constexpr int LDS = HBUF + LBUF + 2 * BSTAGE;
+  static_assert(WM * FM * 16 == BM && WN * FN * 16 == BN, "");
+  static_assert(B_HM_INS * 8 * NW == BN && B_L_INS * 16 * NW == BN, "");
+  static_assert(LDS <= 80 * 1024, "two blocks per CU");
+};
+
+template <bool PRO, int EPI>
+__global__ __launch_bounds__(HaloX6S::NT, 2) void conv_halo_x6s_kernel(const ConvK k) {
+  static_assert(EPI >= 0, "the specialised register epilogues only");
+  typedef HaloX6S TL;
+  constexpr int FM = TL::FM, FN = TL::FN, NT = TL::NT, BN = TL::BN, BK = TL::BK;
+  constexpr int HSIDE = TL::HSIDE, HROWS = TL::HROWS, HPIECES = TL::HPIECES;
+  constexpr int H_INS = TL::H_INS, B_HM_INS = TL::B_HM_INS, B_L_INS = TL::B_L_INS;
+  constexpr int BSTAGE = TL::BSTAGE;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const hbuf = smem;                 // the halo: raw fp32, then [hi|mid] in place
+  char* const lbuf = smem + TL::HBUF;      // lo of the current channel block
+  char* const bring = lbuf + TL::LBUF;     // 2 stages of pre-split weights
+
+  const mia_conv_args& p = k.a;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid, wn = 0;
+  const ConvGroup G = k.g[0];
+  const int H = p.H, W = p.W, Cin = p.Cin, Cout = p.Cout, Kpad = G.kpad;
+  const int bl = xcd_remap(blockIdx.x, k.nblk);
+  const int mt = bl / k.nbn, n0 = (bl % k.nbn) * BN;
+  const int ptx = W / TL::PW, pty = H / TL::PH;
+  const int x0 = (mt % ptx) * TL::PW;
+  const int y0 = ((mt / ptx) % pty) * TL::PH;
+  const int n = mt / (ptx * pty);
+
+  const float* __restrict__ X = (const float*)p.x;
+  const unsigned* __restrict__ Whm = (const unsigned*)G.w_split;               // [Cout][Kpad]
+  const __bf16* __restrict__ Wl = (const __bf16*)(Whm + (size_t)Cout * Kpad);  // [Cout][Kpad]
+  const char* zero = (const char*)g_zero16;
+
+  // per-lane DMA sources: weight pieces (every wave) and halo pieces (every wave), byte pointers
+  const char* wsrc[B_HM_INS + B_L_INS];
+#pragma unroll
+  for (int j = 0; j < B_HM_INS + B_L_INS; ++j) {
+    // weight rows past Cout read row Cout − 1 (never stored or summed: register epilogues)
+    if (j < B_HM_INS) {
+      const int row = (wid * B_HM_INS + j) * 8 + (lane >> 3);
+      const int c = min(n0 + row, Cout - 1);
+      wsrc[j] = (const char*)(Whm + (size_t)c * Kpad + ((lane & 7) ^ fsw(row)) * 4);
+    } else {
+      const int row = (wid * B_L_INS + j - B_HM_INS) * 16 + (lane >> 2);
+      const int c = min(n0 + row, Cout - 1);
+      wsrc[j] = (const char*)(Wl + (size_t)c * Kpad + ((lane & 3) ^ (lsw(row) >> 1)) * 8);
+    }
+  }
+  const char* hsrc[H_INS];
+#pragma unroll
+  for (int j = 0; j < H_INS; ++j) {
+    hsrc[j] = nullptr;
+    const int hr = (wid + TL::NW * j) * 8 + (lane >> 3);
+    const int hy = hr / HSIDE, hx = hr - (hr / HSIDE) * HSIDE;
+    const int y = y0 + hy - 1, x = x0 + hx - 1;
+    if (hr < HROWS && y >= 0 && y < H && x >= 0 && x < W)
+      hsrc[j] = (const char*)(X + ((size_t)(n * H + y) * W + x) * Cin + ((lane & 7) ^ fsw(hr)) * 4);
+  }
+  const int ncb = Cin / BK, nk = 9 * ncb;
+
+  auto issue_b = [&](int s, int st) {  // this wave's weight pieces of K-step s = (cb, tap)
+    const int cb = s / 9, t = s - (s / 9) * 9;
+    const size_t koff = (size_t)t * Cin + cb * BK;
+    char* dst = bring + st * BSTAGE;
+#pragma unroll
+    for (int j = 0; j < B_HM_INS; ++j)
+      __builtin_amdgcn_global_load_lds((gptr_t)(wsrc[j] + koff * 4),
+                                       (lptr_t)(dst + (wid * B_HM_INS + j) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < B_L_INS; ++j)
+      __builtin_amdgcn_global_load_lds((gptr_t)(wsrc[B_HM_INS + j] + koff * 2),
+                                       (lptr_t)(dst + TL::BHM + (wid * B_L_INS + j) * 1024), 16,
+                                       0, 0);
+  };
+  auto issue_halo = [&](int cb) {  // this wave's halo pieces of channel block cb
+#pragma unroll
+    for (int j = 0; j < H_INS; ++j) {
+      if (wid + TL::NW * j >= HPIECES) break;
+      const char* a = hsrc[j] ? hsrc[j] + (size_t)cb * BK * 4 : zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)a, (lptr_t)(hbuf + (wid + TL::NW * j) * 1024), 16,
+                                       0, 0);
+    }
+  };
+  const bool lrelu_in = p.act_in == MIA_ACT_LRELU_S2;
+  auto convert = [&](int cb) {  // split the landed raw halo in place + lo into lbuf
+    for (int c = tid; c < HROWS * 8; c += NT) {
+      const int hr = c >> 3, pc = c & 7, lc = pc ^ fsw(hr);
+      f32x4 v = *(const f32x4*)(hbuf + hr * ROWB + pc * 16);
+      if constexpr (PRO) {  // x̃ = act(x)·s, rounded as the on-the-fly path (conv_common.h)
+        const float mul = lrelu_in ? SQRT2 : 1.f;
+        f32x4 s4 = {1.f, 1.f, 1.f, 1.f};
+        if (p.in_scale) s4 = *(const f32x4*)(p.in_scale + (size_t)n * Cin + cb * BK + lc * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float f = v[e];
+          if (lrelu_in) f = fmaxf(f, 0.2f * f);
+          v[e] = f * (s4[e] * mul);
+        }
+      }
+      u32x4 hm;
+      u32x2 lo;
+      split_quad(v, hm, lo);
+      *(u32x4*)(hbuf + hr * ROWB + pc * 16) = hm;
+      *(u32x2*)(lbuf + hr * TL::LROWB + ((lc ^ lsw(hr)) << 3)) = lo;
+    }
+  };
+
+  // prologue: halo of channel block 0 and the weights of step 0, then the split
+  issue_halo(0);
+  issue_b(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  convert(0);
+  __syncthreads();
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // the taps unrolled over lane-constant fragment offsets (as the 8-wave kernel's UNR loop)
+  const int frow = lane & 15, fq = lane >> 4;
+  int oh[FM + 2][3], ol[FM + 2][3];
+#pragma unroll
+  for (int q = 0; q < FM + 2; ++q)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int hr = (wm * FM + q) * HSIDE + frow + c;
+      int vh = hr * ROWB + ((fq ^ fsw(hr)) << 4), vl = hr * TL::LROWB + ((fq ^ lsw(hr)) << 3);
+      asm volatile("" : "+v"(vh), "+v"(vl));
+      oh[q][c] = vh;
+      ol[q][c] = vl;
+    }
+  int st = 0;
+  for (int cb = 0; cb < ncb; ++cb) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int s = cb * 9 + t;
+      int x1 = 64, x2 = 32;
+      asm volatile("" : "+s"(x1), "+s"(x2));
+      const int dy = t / 3, dx = t % 3;
+      const char* sb = bring + st * BSTAGE;
+      if (s + 1 < nk) issue_b(s + 1, st ^ 1);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ch = h * 4 + fq;
+        u32x4 ahm[FM], bhm[FN];
+        u32x2 al[FM], blo[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          ahm[i] = *(const u32x4*)(hbuf + (h ? oh[i + dy][dx] ^ x1 : oh[i + dy][dx]));
+          al[i] = *(const u32x2*)(lbuf + (h ? ol[i + dy][dx] ^ x2 : ol[i + dy][dx]));
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int row = 16 * j + frow;
+          bhm[j] = *(const u32x4*)(sb + row * ROWB + ((ch ^ fsw(row)) << 4));
+          blo[j] = *(const u32x2*)(sb + TL::BHM + row * TL::LROWB + ((ch ^ lsw(row)) << 3));
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = mfma_x6(bhm[j], blo[j], ahm[i], al[i], acc[i][j]);  // D[ch][px]
+        __builtin_amdgcn_s_setprio(0);
+      }
+      // the next step's weights landed (this wave's pieces; the barrier covers the others')
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_handoff();
+      __builtin_amdgcn_sched_barrier(0);
+      st ^= 1;
+    }
+    if (cb + 1 < ncb) {  // every wave is past its last read of the halo and lo: next block
+      issue_halo(cb + 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      convert(cb + 1);
+      __syncthreads();
+    }
+  }
+  halo_epilogue_f<float, TL, EPI>(k, acc, n, y0, x0, n0, wm, wn, lane, -1, -1, nullptr,
+                                  k.prered ? (float*)smem : nullptr, TL::WM, TL::BN);
+}
+
+template <bool PRO, int EPI>
+static int launch_x6s_(ConvK& k, hipStream_t st) {
+  typedef HaloX6S TL;
+  k.nbn = (k.a.Cout + TL::BN - 1) / TL::BN;
+  k.nblk = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW) * k.nbn;
+  size_t lds = TL::LDS;
+  lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
+  lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
+  auto fn = conv_halo_x6s_kernel<PRO, EPI>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            80 * 1024) != hipSuccess)
+      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+    attr_set = true;
+  }
+  k.prered = prered_enabled() && (EPI & epi::CSUM);
+  const int nslots = halo_red_slots(k.a.H, k.a.W, TL::FM, TL::WM, k.prered);
+  RedQ r;
+  int rc = conv_red_begin(k, r, nslots, st);
+  if (rc != MIA_OK) return rc;
+  hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), lds, st, k);
+  rc = check_launch("conv_halo_x6s");
+  return rc != MIA_OK ? rc : red_finish(r, st);
+}
+
+// T_X6_64S = 1 (default): the Cout = 64 launches with a specialised epilogue on the two-blocks-
+// per-CU tile; returns X6S_NONE (not handled) for any other feature mask
+constexpr int X6S_NONE = 1;  // not an MIA_* status (those are ≤ 0)
+static int launch_x6s(ConvK& k, hipStream_t st, bool pro) {
+  using namespace epi;
+  const int f = epi_mask(k);
+  if (pro) {
+    if (f == (OSC | NOISE | BIAS | LRELU)) return launch_x6s_<true, OSC | NOISE | BIAS | LRELU>(k, st);
+    return X6S_NONE;
+  }
+  switch (f) {
+    case 0: return launch_x6s_<false, 0>(k, st);
+    case BIAS: return launch_x6s_<false, BIAS>(k, st);
+    case BIAS | RELU: return launch_x6s_<false, BIAS | RELU>(k, st);
+    case PRELU: return launch_x6s_<false, PRELU>(k, st);
+    case MASK: return launch_x6s_<false, MASK>(k, st);
+    case TAP: return launch_x6s_<false, TAP>(k, st);
+    case TAP | MASK: return launch_x6s_<false, TAP | MASK>(k, st);
+    case ACC: return launch_x6s_<false, ACC>(k, st);
+    case MASK | MSL: return launch_x6s_<false, MASK | MSL>(k, st);
+    default: return X6S_NONE;
+  }
+}
+
 // The register epilogue specialised for the feature masks of the attack's fp32 launches (every aux
 // load of a row chunk hoisted, compile-time features; halo_epilogue.h): the runtime-generic one
 // issues its per-row loads one dependent round trip at a time, ≈ 10 % of a block's cycles
@@ -551,7 +815,7 @@ bool conv_halo_x6_eligible(const ConvK& k, int dtype) {
          // 64 channels: the 64-column tile, except with the tap pair (VGG gradient at a tap
          // layer: 1–2 % slower than the generic tile); with the specialised register epilogues
          // the mask / accumulate launches run 12–20 % faster on it (137 → 154 / 164 TFLOP/s)
-         (a.Cout > 64 || (a.Cout == 64 && (!a.tap_a || x6_64_aux())));
+         (a.Cout > 64 || (a.Cout == 64 && (!a.tap_a || x6_64_aux() || tune(T_X6_64S) != 0)));
 }
 
 #ifdef MIA_STAMPS
@@ -583,6 +847,10 @@ int launch_conv_halo_x6(ConvK& k, hipStream_t st) {
   }
 #endif
   const int sel = tune(T_HALO_EPI);  // 0 LDS-staged epilogue, 2 runtime; default 1 specialised
+  if (k.a.Cout == 64 && sel == 1 && tune(T_X6_64S) != 0 && k.a.H % HaloX6S::PH == 0) {
+    const int rc = launch_x6s(k, st, pro);
+    if (rc != X6S_NONE) return rc;
+  }
   if (k.a.Cout == 64) {
     if (sel == 0) return pro ? launch_x6_<64, true, -2>(k, st) : launch_x6_<64, false, -2>(k, st);
     if (sel == 1) return pro ? launch_x6_spec<64, true>(k, st) : launch_x6_spec<64, false>(k, st);

@@ -98,6 +98,8 @@ enum TuneKey {
   T_THIN_F32,        // fp32 thin layers: 3 (default) + sliding-window gradient strips, 2 hoisted
                      // forward loads, 1 more waves + LDS gradient weights, 0 round 2
                      // (profiles/r03_thin_f32_ab.txt)
+  T_X6_64S,          // fp32 Cout = 64: 1 (default) the two-blocks-per-CU x6 tile (conv_halo_x6.hip
+                     // HaloX6S, also the VGG tap-pair gradient), 0 the 8-wave 64-column tile
   T_NKEYS
 };
 int tune(TuneKey key);

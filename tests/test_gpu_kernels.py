@@ -1170,7 +1170,7 @@ def test_fp32_arithmetic_is_fp32_accurate(cuda, tune, path):
     assert mx <= 2 * native[path][0] and nrm <= 2 * native[path][1]
 
 
-@pytest.mark.parametrize("C,H,W", [(64, 32, 48), (128, 32, 16), (256, 16, 16)])
+@pytest.mark.parametrize("C,H,W", [(64, 32, 48), (64, 16, 32), (128, 32, 16), (256, 16, 16)])
 @pytest.mark.parametrize("mode", ["plain", "bias_relu", "prelu", "mask_slope", "acc", "mask",
                                   "tap_mask", "bias"])
 def test_x6_halo_variants_bitwise(cuda, tune, C, H, W, mode):
@@ -1179,8 +1179,9 @@ def test_x6_halo_variants_bitwise(cuda, tune, C, H, W, mode):
     computes the same products in the same order as the rolled loop with the runtime-feature
     epilogue (MIA_X6_UNR=0, MIA_HALO_EPI=2): outputs bit-identical, for every epilogue feature
     set of the attack's fp32 launches, on the 64- and 128-channel tiles; and both against fp64.
-    The 64-channel tile's two-taps-per-K-step loop (MIA_X6_UNR=2, default) equals its one-tap
-    form (MIA_X6_UNR=1) bit for bit."""
+    The 64-channel layers' default two-blocks-per-CU tile (MIA_X6_64S=1), the 8-wave tile's
+    two-taps-per-K-step loop (MIA_X6_UNR=2) and its one-tap form (MIA_X6_UNR=1) agree bit for
+    bit."""
     g = torch.Generator().manual_seed(C + H * 3 + W + len(mode))
     N = 2
     x = torch.randn(N, C, H, W, generator=g)
@@ -1233,7 +1234,9 @@ def test_x6_halo_variants_bitwise(cuda, tune, C, H, W, mode):
     if mode == "tap_mask":
         ref = (conv + 0.37 * (a.double() - t.double())) * (a.double() > 0)
     tune("MIA_X6_64AUX", "1")  # the 64-column tile for the tap launch too
-    y_def = run()  # MIA_X6_UNR=2: the 64-column tile with two taps per K-step
+    y_def = run()  # Cout 64: the two-blocks-per-CU tile (MIA_X6_64S=1)
+    tune("MIA_X6_64S", "0")  # the 8-wave 64-column tile, two taps per K-step (MIA_X6_UNR=2)
+    assert torch.equal(run(), y_def)
     tune("MIA_X6_UNR", "1")  # one tap per K-step: the same MFMAs in the same order
     assert torch.equal(run(), y_def)
     tune("MIA_X6_UNR", "0")

@@ -686,6 +686,264 @@ __global__ __launch_bounds__(DgX6::NT, 1) void upconv_x6_kernel(const UpK k) {
   }
 }
 
+// ---- the same on an 8 × 16 patch, two blocks per CU (round 4) --------------------------------
+// As conv_halo_x6.hip's HaloX6S for the 64-channel stride-1 layers: the kernel above is one 8-wave
+// block per CU, so its per-step barriers, channel-block splits, prologue and epilogue stall the
+// whole CU. Here a block is an 8 × 16 patch (4 row waves of 2 patch rows × 64 channels × the 4
+// phases: the same 128 accumulator VGPRs per wave), LDS = ONE halo buffer + lo + the 2-stage weight
+// ring = 77.6 KB, two blocks per CU; every wave streams a share of the weights (6 pieces per
+// K-step) and of the next channel block's halo (fetched after the block's last step). Same MFMAs
+// in the same order per output as the kernel above (bit-identical).
+struct DgX6S {
+  static constexpr int PH = 8, PW = 16, NW = 4, NT = 64 * NW;
+  static constexpr int WM = 4, WN = 1, FM = 2, FN = 4;
+  static constexpr int BN = WN * FN * 16, BK = 32;              // 64 output channels
+  static constexpr int HSIDE = PW + 1, HROWS = (PH + 1) * HSIDE;  // 153 halo pixels
+  static constexpr int HPIECES = (HROWS + 7) / 8;                 // 20 pieces of 8 rows
+  static constexpr int HBUF = HPIECES * 1024;
+  static constexpr int LROWB = 64, LBUF = HROWS * LROWB;
+  static constexpr int BROWS = 2 * BN;                            // two phase slots per K-step
+  static constexpr int BHM = BROWS * ROWB, BSTAGE = BHM + BROWS * LROWB;
+  static constexpr int B_HM_INS = BROWS / 8 / NW;                 // 4 [hi|mid] pieces per wave
+  static constexpr int B_L_INS = BROWS / 16 / NW;                 // 2 lo pieces per wave
+  static constexpr int H_INS = (HPIECES + NW - 1) / NW;           // 5
+  static constexpr int NSTEP = 5;
+  static constexpr int LDS = HBUF + LBUF + 2 * BSTAGE;
+  static_assert(WM * FM == PH && WN * FN * 16 == BN, "");
+  static_assert(B_HM_INS * 8 * NW == BROWS && B_L_INS * 16 * NW == BROWS, "");
+  static_assert(LDS <= 80 * 1024, "two blocks per CU");
+};
+
+template <bool DG, bool PRO>
+__global__ __launch_bounds__(DgX6S::NT, 2) void upconv_x6s_kernel(const UpK k) {
+  typedef DgX6S TL;
+  constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, BN = TL::BN, BK = TL::BK, NT = TL::NT;
+  constexpr int HSIDE = TL::HSIDE, HROWS = TL::HROWS, HPIECES = TL::HPIECES;
+  constexpr int H_INS = TL::H_INS, BSTAGE = TL::BSTAGE;
+  constexpr int B_HM_INS = TL::B_HM_INS, B_L_INS = TL::B_L_INS;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const hbuf = smem;                  // the halo: raw fp32, then [hi|mid] in place
+  char* const lbuf = smem + TL::HBUF;       // lo of the current channel block
+  char* const bring = lbuf + TL::LBUF;      // 2 stages of pre-split weights: [hi|mid] rows, lo rows
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / WN, wn = wid % WN;
+  const int R = k.R, Cin = k.Cin, Cout = k.Cout;
+  const int bl = xcd_remap(blockIdx.x, k.nblk);
+  const int mt = bl / k.nbn, n0 = (bl % k.nbn) * BN;
+  const int ptx = R / TL::PW, pty = R / TL::PH;
+  const int x0 = (mt % ptx) * TL::PW;
+  const int y0 = ((mt / ptx) % pty) * TL::PH;
+  const int n = mt / (ptx * pty);
+  const int ncb = Cin / BK, nk = TL::NSTEP * ncb;
+  const int csrc = k.cin_src, cbs = csrc / BK;
+  const char* Whm = (const char*)k.w_split;
+  const char* Wl = Whm + (size_t)nk * 2 * Cout * ROWB;
+  const size_t hm_step = (size_t)2 * Cout * ROWB, l_step = (size_t)2 * Cout * TL::LROWB;
+  const char* zero = (const char*)g_zero16;
+
+  // per-lane DMA offsets: this wave's weight pieces (bytes within a K-step's rows) and its halo
+  // pieces (elements in a source tensor, −1 → the zero page); < 2^31, checked at the API
+  int woff[B_HM_INS + B_L_INS], hoff[H_INS];
+#pragma unroll
+  for (int j = 0; j < B_HM_INS + B_L_INS; ++j) {
+    if (j < B_HM_INS) {
+      const int row = (wid * B_HM_INS + j) * 8 + (lane >> 3);
+      const int slot = row / BN, c = n0 + row % BN;
+      woff[j] = (slot * Cout + c) * ROWB + ((lane & 7) ^ fsw(row)) * 16;
+    } else {
+      const int row = (wid * B_L_INS + j - B_HM_INS) * 16 + (lane >> 2);
+      const int slot = row / BN, c = n0 + row % BN;
+      woff[j] = (slot * Cout + c) * TL::LROWB + ((lane & 3) ^ (lsw(row) >> 1)) * 16;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < H_INS; ++j) {
+    hoff[j] = -1;
+    const int hr = (wid + TL::NW * j) * 8 + (lane >> 3);
+    const int hy = hr / HSIDE, hx = hr - (hr / HSIDE) * HSIDE;
+    const int y = y0 + hy - (DG ? 0 : 1), x = x0 + hx - (DG ? 0 : 1);
+    if (hr < HROWS && y >= 0 && y < R && x >= 0 && x < R)
+      hoff[j] = ((n * R + y) * R + x) * csrc + ((lane & 7) ^ fsw(hr)) * 4;
+  }
+  auto opaque = [](int v) __attribute__((always_inline)) {
+    asm volatile("" : "+v"(v));
+    return v;
+  };
+  auto issue_b = [&](int s, int stg) {
+    char* dst = bring + stg * BSTAGE;
+    const char* hm = Whm + s * hm_step;
+    const char* lo = Wl + s * l_step;
+#pragma unroll
+    for (int j = 0; j < B_HM_INS; ++j)
+      __builtin_amdgcn_global_load_lds((gptr_t)(hm + opaque(woff[j])),
+                                       (lptr_t)(dst + (wid * B_HM_INS + j) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < B_L_INS; ++j)
+      __builtin_amdgcn_global_load_lds((gptr_t)(lo + opaque(woff[B_HM_INS + j])),
+                                       (lptr_t)(dst + TL::BHM + (wid * B_L_INS + j) * 1024), 16,
+                                       0, 0);
+  };
+  auto issue_halo = [&](int cb) {
+    const int sc = cb / cbs;  // source tensor of channel block cb (wave-uniform)
+    const float* xb = (const float*)up_src(k, sc) + (cb - sc * cbs) * BK;
+#pragma unroll
+    for (int j = 0; j < H_INS; ++j) {
+      if (wid + TL::NW * j >= HPIECES) break;
+      const int o = opaque(hoff[j]);
+      const char* a = o >= 0 ? (const char*)(xb + o) : zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)a, (lptr_t)(hbuf + (wid + TL::NW * j) * 1024), 16,
+                                       0, 0);
+    }
+  };
+  const bool lrelu_in = k.act_in == MIA_ACT_LRELU_S2;
+  auto convert = [&](int cb) {
+    for (int c = tid; c < HROWS * 8; c += NT) {
+      const int hr = c >> 3, pc = c & 7, lc = pc ^ fsw(hr);
+      f32x4 v = *(const f32x4*)(hbuf + hr * ROWB + pc * 16);
+      if constexpr (PRO) {
+        const float mul = lrelu_in ? SQRT2 : 1.f;
+        f32x4 s4 = {1.f, 1.f, 1.f, 1.f};
+        if (k.style) s4 = *(const f32x4*)(k.style + (size_t)n * Cin + cb * BK + lc * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float f = v[e];
+          if (lrelu_in) f = fmaxf(f, 0.2f * f);
+          v[e] = f * (s4[e] * mul);
+        }
+      }
+      u32x4 hm;
+      u32x2 lo;
+      split_quad(v, hm, lo);
+      *(u32x4*)(hbuf + hr * ROWB + pc * 16) = hm;
+      *(u32x2*)(lbuf + hr * TL::LROWB + ((lc ^ lsw(hr)) << 3)) = lo;
+    }
+  };
+
+  issue_halo(0);
+  issue_b(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  convert(0);
+  __syncthreads();
+
+  f32x4 acc[4][FM][FN];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[q][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int cb = 0; cb < ncb; ++cb) {
+#pragma unroll
+    for (int st = 0; st < TL::NSTEP; ++st) {
+      const int ln = opaque(lane);  // the fragment addresses are recomputed per K-step
+      const int frow = ln & 15, fq = ln >> 4;
+      const int s = cb * TL::NSTEP + st;
+      const char* sb = bring + (s & 1) * BSTAGE;
+      if (s + 1 < nk) issue_b(s + 1, (s & 1) ^ 1);
+      const int jy = up_jy(st), jx = up_jx(st);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int ch = h * 4 + fq;
+        u32x4 ahm[FM];
+        u32x2 al[FM];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int hr = DG ? (wm * FM + i + jy) * HSIDE + frow + jx
+                            : (wm * FM + i + 1 - jy) * HSIDE + frow + 1 - jx;
+          ahm[i] = *(const u32x4*)(hbuf + hr * ROWB + ((ch ^ fsw(hr)) << 4));
+          al[i] = *(const u32x2*)(lbuf + hr * TL::LROWB + ((ch ^ lsw(hr)) << 3));
+        }
+#pragma unroll
+        for (int slot = 0; slot < 2; ++slot) {
+          const int ph = up_phase(st, slot);
+          if (ph < 0) continue;
+          u32x4 bhm[FN];
+          u32x2 blo[FN];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int row = slot * BN + wn * FN * 16 + 16 * j + frow;
+            bhm[j] = *(const u32x4*)(sb + row * ROWB + ((ch ^ fsw(row)) << 4));
+            blo[j] = *(const u32x2*)(sb + TL::BHM + row * TL::LROWB + ((ch ^ lsw(row)) << 3));
+          }
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)  // D[channel][pixel]
+              acc[ph][i][j] = mfma_x6(bhm[j], blo[j], ahm[i], al[i], acc[ph][i][j]);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of step s+1
+      lds_handoff();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (cb + 1 < ncb) {  // every wave is past its last read of the halo and lo
+      issue_halo(cb + 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      convert(cb + 1);
+      __syncthreads();
+    }
+  }
+
+  const int frow = lane & 15, fq = lane >> 4;
+  float* __restrict__ Y = (float*)k.t;
+  const int TS = DG ? 2 * R : 2 * R + 1;
+  float msl[FN][4];
+#pragma unroll
+  for (int j = 0; j < FN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      msl[j][e] = k.mask_slope ? k.mask_slope[n0 + wn * FN * 16 + 16 * j + 4 * fq + e] : 0.f;
+#pragma unroll
+  for (int ph = 0; ph < 4; ++ph) {
+    const int py = ph >> 1, px = ph & 1;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int ty = 2 * (y0 + wm * FM + i) + (DG ? 1 - py : py);
+      const int tx = 2 * (x0 + frow) + (DG ? 1 - px : px);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = n0 + wn * FN * 16 + 16 * j + 4 * fq;
+        const size_t o = ((size_t)(n * TS + ty) * TS + tx) * Cout + c;
+        f32x4 v = acc[ph][i][j];
+        if (DG && k.mask_a) {
+          const f32x4 m = *(const f32x4*)((const float*)k.mask_a + o);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = m[e] > 0.f ? v[e] : msl[j][e] * v[e];
+        }
+        if (DG && k.accumulate) {
+          const f32x4 a = *(const f32x4*)(Y + o);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += a[e];
+        }
+        *(f32x4*)(Y + o) = v;
+      }
+    }
+  }
+}
+
+template <bool DG, bool PRO>
+static int launch_upconv_x6s(UpK& k, hipStream_t st) {
+  typedef DgX6S TL;
+  k.nbn = k.Cout / TL::BN;
+  k.nblk = k.N * (k.R / TL::PH) * (k.R / TL::PW) * k.nbn;
+  auto fn = upconv_x6s_kernel<DG, PRO>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            80 * 1024) != hipSuccess)
+      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), TL::LDS, st, k);
+  return check_launch("upconv_x6s");
+}
+
 template <bool DG, bool PRO, bool EARLY, bool PRIO>
 static int launch_upconv_x6_e(UpK& k, hipStream_t st) {
   typedef DgX6 TL;
@@ -705,6 +963,8 @@ static int launch_upconv_x6_e(UpK& k, hipStream_t st) {
 
 template <bool DG, bool PRO>
 static int launch_upconv_x6(UpK& k, hipStream_t st) {
+  // T_UPCONV_X6S = 1 (default): the 8 × 16-patch two-blocks-per-CU form
+  if (tune(T_UPCONV_X6S) != 0) return launch_upconv_x6s<DG, PRO>(k, st);
   // the next block's halo DMA at the step start (as the x6 halo kernel; neutral here against
   // issuing it between the two MFMA halves); no s_setprio (neutral, +1 / −1 % by layer)
   return launch_upconv_x6_e<DG, PRO, true, false>(k, st);

@@ -1327,3 +1327,42 @@ def test_halo_lowp_unrolled_bitwise(cuda, tune, dtype, C, H, W, mode):
         got = y_def.permute(0, 3, 1, 2).double().cpu()
         tol = 2e-2 if dtype == torch.float16 else 1e-1
         assert ((got - ref).abs().max() / ref.abs().max()).item() < tol, mode
+
+
+@pytest.mark.parametrize("R,cin,cout", [(16, 64, 128), (32, 128, 64)])
+def test_upconv_x6_two_block_form_bitwise(cuda, tune, R, cin, cout):
+    """fp32 split-once up-conv kernels: the 8 × 16-patch two-blocks-per-CU form (MIA_UPCONV_X6S=1,
+    default) computes the same MFMAs in the same order as the 8-wave 16 × 16 form (0): the
+    StyleGAN2 up-sampling conv forward (modulated, lrelu input) and the stride-2 input gradient
+    with mask + accumulate (2-source multi form) are bit-identical; and the forward against fp64."""
+    N = 2
+    g = torch.Generator().manual_seed(R + cin + cout)
+    x = torch.randn(N, cin, R, R, generator=g)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(9 * cin)
+    s = torch.rand(N, cin, generator=g) + 0.5
+    xd = nhwc(x, torch.float32).to(cuda)
+    wph = [m.to(cuda) for m in layouts.upconv_subpixel_matrices(w, torch.float32)]
+    wup = layouts.upconv_halo_matrix(w, torch.float32).to(cuda)
+    # s2 dgrad: two sources of Cg = cout channels each (the multi-source K loop), into cin channels
+    wd = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(9 * cin)
+    gs = [nhwc(torch.randn(N, cout, R, R, generator=g), torch.float32).to(cuda) for _ in range(2)]
+    wh = torch.cat([layouts.s2_dgrad_halo_matrix(wd, torch.float32)] * 2).to(cuda)
+    a_below = nhwc(torch.randn(N, cin, 2 * R, 2 * R, generator=g), torch.float32).to(cuda)
+    base = nhwc(torch.randn(N, cin, 2 * R, 2 * R, generator=g), torch.float32).to(cuda)
+    sl = torch.full((cin,), 0.25, device=cuda)
+
+    def run():
+        t = torch.full((N, 2 * R + 1, 2 * R + 1, cout), float("nan"), device=cuda)
+        ops.upconv_fwd(xd, wph, t, cout, act_in=ops.ACT_LRELU_S2, style=s.to(cuda), w_up=wup)
+        gx = base.clone()
+        ops.s2_dgrad_halo(gs, wh, gx, mask_a=a_below, mask_slope=sl, accumulate=True)
+        torch.cuda.synchronize()
+        return t, gx
+
+    t1, g1 = run()
+    tune("MIA_UPCONV_X6S", "0")
+    t0, g0 = run()
+    assert torch.equal(t1, t0) and torch.equal(g1, g0)
+    xin = F.leaky_relu(x.double(), 0.2) * math.sqrt(2) * s.double().view(N, cin, 1, 1)
+    ref = F.conv_transpose2d(xin, w.double().transpose(0, 1), stride=2)
+    assert rel_err(nchw(t1), ref) < 3 * TOL[torch.float32]

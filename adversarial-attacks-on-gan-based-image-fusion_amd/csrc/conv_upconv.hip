@@ -963,8 +963,12 @@ static int launch_upconv_x6_e(UpK& k, hipStream_t st) {
 
 template <bool DG, bool PRO>
 static int launch_upconv_x6(UpK& k, hipStream_t st) {
-  // T_UPCONV_X6S = 1 (default): the 8 × 16-patch two-blocks-per-CU form
-  if (tune(T_UPCONV_X6S) != 0) return launch_upconv_x6s<DG, PRO>(k, st);
+  // T_UPCONV_X6S = 1 (default): the 8 × 16-patch two-blocks-per-CU form for the stride-2 input
+  // gradients with Cin ≤ 512 (≤ 16 channel blocks: their prologue / splits / epilogue are the
+  // exposed share); measured (fp32, 128 images, profiles/r04_layers_fp32_b128_e4e_upx6s_*):
+  // e4e body / single heads R128 / R64 / R32 / R16 −9 / −12 / −11 / −2 % per call, the long
+  // multi-source K loops (7 × 512, 4 × 512 channels) +5 / +4 %, the up-conv forward ±0.5 %
+  if (DG && tune(T_UPCONV_X6S) != 0 && k.Cin <= 512) return launch_upconv_x6s<DG, PRO>(k, st);
   // the next block's halo DMA at the step start (as the x6 halo kernel; neutral here against
   // issuing it between the two MFMA halves); no s_setprio (neutral, +1 / −1 % by layer)
   return launch_upconv_x6_e<DG, PRO, true, false>(k, st);

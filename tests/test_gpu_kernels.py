@@ -1332,9 +1332,10 @@ def test_halo_lowp_unrolled_bitwise(cuda, tune, dtype, C, H, W, mode):
 @pytest.mark.parametrize("R,cin,cout", [(16, 64, 128), (32, 128, 64)])
 def test_upconv_x6_two_block_form_bitwise(cuda, tune, R, cin, cout):
     """fp32 split-once up-conv kernels: the 8 × 16-patch two-blocks-per-CU form (MIA_UPCONV_X6S=1,
-    default) computes the same MFMAs in the same order as the 8-wave 16 × 16 form (0): the
-    StyleGAN2 up-sampling conv forward (modulated, lrelu input) and the stride-2 input gradient
-    with mask + accumulate (2-source multi form) are bit-identical; and the forward against fp64."""
+    default for the stride-2 input gradients with Cin ≤ 512) computes the same MFMAs in the same
+    order as the 8-wave 16 × 16 form (0): the stride-2 input gradient with mask + accumulate
+    (2-source multi form) is bit-identical; the up-sampling conv forward (modulated, lrelu input)
+    too, and against fp64."""
     N = 2
     g = torch.Generator().manual_seed(R + cin + cout)
     x = torch.randn(N, cin, R, R, generator=g)
@@ -1359,7 +1360,7 @@ def test_upconv_x6_two_block_form_bitwise(cuda, tune, R, cin, cout):
         torch.cuda.synchronize()
         return t, gx
 
-    t1, g1 = run()
+    t1, g1 = run()  # the dgrad (Cin = 2·cout ≤ 512) on the two-block form, the forward 8-wave
     tune("MIA_UPCONV_X6S", "0")
     t0, g0 = run()
     assert torch.equal(t1, t0) and torch.equal(g1, g0)

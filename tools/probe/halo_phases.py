@@ -35,16 +35,23 @@ def main():
             b = (torch.randn(C, generator=g) * 0.1).to(dev)
             nz = torch.randn(H * H, generator=g).to(dev)
             y = torch.empty(N, H, H, C, dtype=dtype, device=dev)
-            for mode in ("mod", "plain"):
+            wmod = torch.empty((N,) + tuple(wm.shape), dtype=dtype, device=dev)
+            for mode in ("mod", "wmod", "plain"):
                 kw = dict(in_scale=s, out_scale=d, noise=nz, noise_w=0.3, bias=b,
-                          act_out=ops.ACT_LRELU_S2) if mode == "mod" else {}
-                ops.conv3x3(x, wm, y, cout=C, **kw)
+                          act_out=ops.ACT_LRELU_S2) if mode != "plain" else {}
+
+                def call():
+                    if mode == "wmod":  # per-image modulated weights (round 4)
+                        ops.conv3x3_modw(x, wm, y, wmod, cout=C, **kw)
+                    else:
+                        ops.conv3x3(x, wm, y, cout=C, **kw)
+                call()
                 torch.cuda.synchronize()
                 fn(out, 1)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(3):
-                    ops.conv3x3(x, wm, y, cout=C, **kw)
+                    call()
                 e1.record()
                 torch.cuda.synchronize()
                 fn(out, 1)

@@ -29,6 +29,13 @@
 #ifndef MIA_HALO_PREMOD
 #define MIA_HALO_PREMOD 1
 #endif
+// MIA_HALO_BMIX = 1 (tuning A/B build, `make variant VARIANT=bmix VARIANT_FLAGS=-DMIA_HALO_BMIX=1`):
+// on the 4-wave 2-stage tiles every wave streams a quarter of each K-step's weights (the H-waves
+// issue theirs before their halo pieces and wait with vmcnt(#halo pieces of the step)), instead of
+// the two B-waves 8 pieces each while the H-waves issue weights never
+#ifndef MIA_HALO_BMIX
+#define MIA_HALO_BMIX 0
+#endif
 
 
 namespace mia {
@@ -153,6 +160,27 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
     }
   }
   const int ncb = Cin / BK, nk = 9 * ncb;
+  // BMIX: every wave's weight pieces (rows (wid·BMI + j)·8 + lane/8)
+  constexpr bool BMIX = MIA_HALO_BMIX && TL::NW == 4 && TL::STAGES == 2 && EPI >= 0;
+  constexpr int BMI = BMIX ? BN / (8 * TL::NW) : 1;
+  const T* wsrc[BMI];
+#pragma unroll
+  for (int j = 0; j < BMI; ++j) {
+    const int row = (wid * BMI + j) * 8 + (lane >> 3);
+    wsrc[j] = n0 + row < Cout ? Wt + (size_t)(n0 + row) * G.kpad + ((lane & 7) ^ fsw(row)) * VEC
+                              : nullptr;
+  }
+  auto issue_bm = [&](int s, int st) {  // BMIX: this wave's share of K-step s's weights
+    const int cb = s / 9, t = s - (s / 9) * 9;
+    const int koff = t * Cin + cb * BK;
+    char* dst = bring + st * BSTAGE;
+#pragma unroll
+    for (int j = 0; j < BMI; ++j) {
+      const T* a = wsrc[j] ? wsrc[j] + koff : zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)a, (lptr_t)(dst + (wid * BMI + j) * 1024), 16, 0,
+                                       0);
+    }
+  };
 
   auto issue_b = [&](int s, int st) {  // B-wave: its weight pieces of K-step s = (cb, tap)
     const int cb = s / 9, t = s - (s / 9) * 9;
@@ -191,7 +219,14 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
   // (the style row after the DMA issue: its load latency overlaps the DMA's instead of preceding
   // it; with the epilogue-operand prefetch below +0.1 … +1.3 % on the modulated forward,
   // bit-identical, r03 A/B)
-  if (bwave) {
+  if constexpr (BMIX) {
+    issue_bm(0, 0);  // every wave: its share of step 0 (STAGES = 2)
+    if (!bwave) {
+#pragma unroll
+      for (int j = 0; j < H_INS; ++j)
+        if (j < my_pieces) issue_h(0, j, 0);
+    }
+  } else if (bwave) {
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s) issue_b(s, s);  // nk ≥ 9
   } else {
@@ -206,7 +241,7 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
       stab[i] = from_f<T>(sv * mul);
     }
   }
-  if (bwave) wait_vmcnt((STAGES - 2) * B_INS);  // step 0 landed, steps 1, 2 may stay in flight
+  if (bwave && !BMIX) wait_vmcnt((STAGES - 2) * B_INS);  // step 0 landed, 1, 2 may stay in flight
   else wait_vmcnt(0);
   __syncthreads();
   if constexpr (PRO && MIA_HALO_PREMOD) {
@@ -281,7 +316,11 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
         const char* ha = hbuf + hoff;
         const char* sb = bring + soff;
         const int dy = t / 3, dx = t % 3;
-        if (bwave && s + STAGES - 1 < nk) issue_b(s + STAGES - 1, st == 0 ? STAGES - 1 : st - 1);
+        if constexpr (BMIX) {
+          if (s + 1 < nk) issue_bm(s + 1, st ^ 1);
+        } else {
+          if (bwave && s + STAGES - 1 < nk) issue_b(s + STAGES - 1, st == 0 ? STAGES - 1 : st - 1);
+        }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           VT af[FM], bf[FN];
@@ -313,8 +352,15 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
             __builtin_amdgcn_sched_barrier(0);
           }
         }
-        if (bwave) wait_vmcnt(B_INS * max(0, min(STAGES - 2, nk - 2 - s)));
-        else if (t == 8) wait_vmcnt(0);
+        if constexpr (BMIX) {
+          // this wave's weights of step s+1 (issued before its halo pieces of this step)
+          const int hq = (!bwave && cb + 1 < ncb && t * HPS < H_INS)
+                             ? max(0, min(HPS, min(H_INS, my_pieces) - t * HPS)) : 0;
+          wait_vmcnt(hq);
+        } else {
+          if (bwave) wait_vmcnt(B_INS * max(0, min(STAGES - 2, nk - 2 - s)));
+          else if (t == 8) wait_vmcnt(0);
+        }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of stage st are done
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);

@@ -375,15 +375,17 @@ def test_style_fusion_simple_api(cuda):
     assert not torch.equal(sweep[0], fused[0])
 
 
-def test_cfg1_fusion_pair_fgsm(cuda):
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_cfg1_fusion_pair_fgsm(cuda, dtype):
     """BASELINE config #1 plumbing: a 256² pair from the fusion entry point, FGSM ε = 8/255 on one
     image toward the other through the attack engine, then the arithmetic fusion of the attacked
-    image's latent with its partner's."""
+    image's latent with its partner's — at fp32 (the reference's precision, config #1 as written)
+    and fp16."""
     from gfa_amd import StyleFusionSimple, fgsm
     drawer = StyleFusionSimple("church", None, None, cuda, n_mean_latent=256)
     pair = torch.cat([drawer.generate_img(drawer.seed_to_z((s, 0)), "z")[0] for s in (1, 2)])
     pair = pair.clamp(-1, 1)
-    net = networks.build_net(256, seed=0, dtype=torch.float16, device=cuda)
+    net = networks.build_net(256, seed=0, dtype=dtype, device=cuda)
     adv = fgsm(net, pair[:1], 8 / 255, target=pair[1:])
     d = (adv - pair[:1]).abs()
     assert d.max().item() <= 16 / 255 + 1e-6 and ((d - 16 / 255).abs() < 1e-6).float().mean() > 0.5

@@ -1329,6 +1329,89 @@ def test_halo_lowp_unrolled_bitwise(cuda, tune, dtype, C, H, W, mode):
         assert ((got - ref).abs().max() / ref.abs().max()).item() < tol, mode
 
 
+@pytest.mark.parametrize("Cin,Cout,H,W", [(128, 128, 16, 32), (256, 192, 16, 16),
+                                           (64, 128, 32, 16), (512, 512, 16, 16)])
+@pytest.mark.parametrize("mode", ["plain", "bias_relu", "prelu", "mask", "mask_slope", "acc", "tap",
+                                  "mod", "sdot_bab"])
+def test_x6_128_two_block_form_bitwise(cuda, tune, Cin, Cout, H, W, mode):
+    """fp32 split-once halo kernel, Cout > 64: the 8 × 16-patch two-blocks-per-CU tile with half-K
+    weight stages (MIA_X6_128S ≥ Cin) computes the same MFMAs in the same order as the 8-wave
+    16 × 16 tile (MIA_X6_128S=0): outputs bit-identical for every specialised epilogue of the
+    attack's fp32 launches (the modulated StyledConv forward and its backward front included;
+    Cout = 192 exercises the clamped weight rows of a partial column tile); the sdot / q sums,
+    whose slot partition follows the patch shape, within 1e-5; and against fp64."""
+    g = torch.Generator().manual_seed(Cin + 3 * Cout + H + W + len(mode))
+    N = 2
+    f32 = torch.float32
+    x = torch.randn(N, Cin, H, W, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)
+    y0 = torch.randn(N, Cout, H, W, generator=g)
+    b = torch.randn(Cout, generator=g) * 0.1
+    slope = torch.rand(Cout, generator=g) * 0.5 + 0.05
+    m = torch.randn(N, Cout, H, W, generator=g)
+    a = torch.randn(N, Cout, H, W, generator=g).relu()
+    t = torch.randn(N, Cout, H, W, generator=g)
+    s = torch.rand(N, Cin, generator=g) + 0.5
+    so = torch.rand(N, Cout, generator=g) + 0.5
+    d = torch.rand(N, Cout, generator=g) + 0.5
+    noise = torch.randn(H * W, generator=g)
+    wf = layouts.fwd_matrix(w, f32).to(cuda)
+
+    def run():
+        y = nhwc(y0, f32).to(cuda)
+        sd = torch.zeros(N * Cout, device=cuda) if mode == "sdot_bab" else None
+        q = torch.zeros(N * Cout, device=cuda) if mode == "sdot_bab" else None
+        kw = {}
+        if mode == "bias_relu":
+            kw = dict(bias=b.to(cuda), act_out=ops.ACT_RELU)
+        elif mode == "prelu":
+            kw = dict(act_out=ops.ACT_PRELU, act_slope=slope.to(cuda))
+        elif mode == "mask":
+            kw = dict(mask_a=nhwc(m, f32).to(cuda))
+        elif mode == "mask_slope":
+            kw = dict(mask_a=nhwc(m, f32).to(cuda), mask_slope=slope.to(cuda))
+        elif mode == "acc":
+            kw = dict(accumulate=True)
+        elif mode == "tap":
+            kw = dict(tap_a=nhwc(a, f32).to(cuda), tap_t=nhwc(t, f32).to(cuda), tap_coef=0.37)
+        elif mode == "mod":
+            kw = dict(in_scale=s.to(cuda), act_in=ops.ACT_LRELU_S2, out_scale=d.to(cuda),
+                      noise=noise.to(cuda), noise_w=0.3, bias=b.to(cuda),
+                      act_out=ops.ACT_LRELU_S2)
+        elif mode == "sdot_bab":
+            kw = dict(out_scale=so.to(cuda), aux_x=nhwc(a, f32).to(cuda), sdot=sd,
+                      bab=dict(demod=d.to(cuda), noise=noise.to(cuda), noise_w=0.3,
+                               bias=b.to(cuda), q=q))
+        ops.conv3x3(nhwc(x, f32).to(cuda), wf, y, cout=Cout, **kw)
+        torch.cuda.synchronize()
+        return y, sd, q
+
+    tune("MIA_X6_128S", "4096")
+    y1, sd1, q1 = run()
+    tune("MIA_X6_128S", "0")
+    y0_, sd0, q0 = run()
+    assert torch.equal(y1, y0_), (mode, (y1 - y0_).abs().max().item())
+    if mode == "sdot_bab":
+        for u, v in ((sd1, sd0), (q1, q0)):
+            assert ((u - v).abs().max() / v.abs().max()).item() < 1e-5
+        return
+    conv = F.conv2d(x.double(), w.double(), padding=1)
+    bd, sl = b.double().view(1, Cout, 1, 1), slope.double().view(1, Cout, 1, 1)
+    if mode == "mod":
+        xa = F.leaky_relu(x.double(), 0.2) * math.sqrt(2) * s.double().view(N, Cin, 1, 1)
+        pre = F.conv2d(xa, w.double(), padding=1) * d.double().view(N, Cout, 1, 1) \
+            + 0.3 * noise.double().view(1, 1, H, W) + bd
+        ref = F.leaky_relu(pre, 0.2) * math.sqrt(2)
+    else:
+        ref = {"plain": conv, "bias_relu": F.relu(conv + bd),
+               "prelu": torch.where(conv > 0, conv, sl * conv),
+               "mask": conv * (m.double() > 0),
+               "mask_slope": torch.where(m.double() > 0, conv, sl * conv),
+               "acc": conv + y0.double(),
+               "tap": conv + 0.37 * (a.double() - t.double())}[mode]
+    assert rel_err(nchw(y1), ref) < 2 * TOL[f32], mode
+
+
 @pytest.mark.parametrize("R,cin,cout", [(16, 64, 128), (32, 128, 64)])
 def test_upconv_x6_two_block_form_bitwise(cuda, tune, R, cin, cout):
     """fp32 split-once up-conv kernels: the 8 × 16-patch two-blocks-per-CU form (MIA_UPCONV_X6S=1,

@@ -215,6 +215,24 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
     }
   };
 
+  // NHBUF = 1 (one halo buffer, the LDS it frees going to a deeper weight ring): after the last
+  // tap of a channel block (every wave past its reads: the step-end barrier) the H-waves fetch the
+  // next block's halo into the same buffer; the block waits for it (the co-resident block's main
+  // loop runs meanwhile) while the B-waves' weight pieces stay in flight
+  auto next_block_single = [&](int cb) {
+    if (!bwave) {
+#pragma unroll
+      for (int j = 0; j < H_INS; ++j)
+        if (j < my_pieces) issue_h(cb, j, 0);
+      wait_vmcnt(0);
+    }
+    __syncthreads();
+    if constexpr (PRO && MIA_HALO_PREMOD) {
+      premod(cb, 0);
+      __syncthreads();
+    }
+  };
+
   // ---- prologue: halo of channel block 0, weights of steps 0 … STAGES−2, style row -----------
   // (the style row after the DMA issue: its load latency overlaps the DMA's instead of preceding
   // it; with the epilogue-operand prefetch below +0.1 … +1.3 % on the modulated forward,
@@ -370,6 +388,9 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
             __syncthreads();
           }
         }
+        if constexpr (TL::NHBUF == 1) {
+          if (t == 8 && cb + 1 < ncb) next_block_single(cb + 1);
+        }
         st = st + 1 == STAGES ? 0 : st + 1;
       }
     }
@@ -453,6 +474,9 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
         __syncthreads();
       }
     }
+    if constexpr (TL::NHBUF == 1) {
+      if (t == 8 && cb + 1 < ncb) next_block_single(cb + 1);
+    }
     st = st + 1 == STAGES ? 0 : st + 1;
     if (++t == 9) { t = 0; ++cb; }
   }
@@ -519,8 +543,6 @@ static int launch_halo_tile_(ConvK& k, hipStream_t st) {
   lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
   lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
   if (lds > 160 * 1024) return set_error("conv_halo: LDS budget exceeded");
-  if (TL::NHBUF == 1 && k.a.Cin != ROWB / (int)sizeof(T))
-    return set_error("conv_halo: single-buffer tile needs Cin = one channel block");
   auto fn = conv_halo_kernel<T, TL, PRO, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -610,6 +632,9 @@ int launch_conv_halo(ConvK& k, int dtype, hipStream_t st) {
   // (round 3, fp16 / bf16 modulated forward at 256² / 128² / 64², bit-identical outputs:
   // 16×16 patches on 8 waves with a 3-stage ring −1.9 … +2.1 %, on 4 waves −9 … −18 %)
   typedef HaloTile<128, 8, 2> Small;
+  // T_HALO_S3 (largest Cin taken): one halo buffer and a 3-stage weight ring, the weights issued
+  // two K-steps ahead (the L2 → LDS latency of a piece is about one K-step of the 2-stage ring)
+  typedef HaloTile<128, 8, 3, 1> Small3;
   typedef HaloTile<64, 8, 3> Small64;
   // Cout ≤ 32 (VGG input gradient): little MFMA work per K-step, so the weights of all nine taps
   // of a one-block Cin are DMA'd in the prologue (9 stages, 36 KB) and no step waits on L2.
@@ -626,6 +651,9 @@ int launch_conv_halo(ConvK& k, int dtype, hipStream_t st) {
     if (k.a.Cout <= 64)  // (specialised epilogues + unrolled taps, as the 128-channel tile)
       return pro ? launch_halo_tile<T, Small64, true, true>(k, st)
                  : launch_halo_tile<T, Small64, false, true>(k, st);
+    if (k.a.Cin <= tune(T_HALO_S3))  // one halo buffer + a 3-stage weight ring (74 KB)
+      return pro ? launch_halo_tile<T, Small3, true, true>(k, st)
+                 : launch_halo_tile<T, Small3, false, true>(k, st);
     return pro ? launch_halo_tile<T, Small, true, true>(k, st)
                : launch_halo_tile<T, Small, false, true>(k, st);
   });

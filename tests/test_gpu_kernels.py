@@ -1247,17 +1247,23 @@ def test_x6_halo_variants_bitwise(cuda, tune, C, H, W, mode):
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("C,H,W", [(128, 32, 16), (256, 16, 32), (64, 32, 32)])
+@pytest.mark.parametrize("C,H,W,s3", [(128, 32, 16, False), (256, 16, 32, False),
+                                      (64, 32, 32, False), (128, 32, 16, True),
+                                      (256, 16, 32, True)])
 @pytest.mark.parametrize("mode", ["plain", "bias_relu", "mask", "tap", "mod", "sdot_bab"])
-def test_halo_lowp_unrolled_bitwise(cuda, tune, dtype, C, H, W, mode):
+def test_halo_lowp_unrolled_bitwise(cuda, tune, dtype, C, H, W, s3, mode):
     """fp16 / bf16 halo kernel (conv_halo.hip): the specialised-epilogue launches run the taps
     unrolled over lane-constant fragment offsets; the runtime-feature epilogue (MIA_HALO_EPI=2)
     runs the rolled loop. Same reads, same MFMAs in the same order: outputs (and sdot / q sums)
     bit-identical; both within the dtype's tolerance of fp64. 'mod' = the StyledConv forward
-    (modulated input, halo modulated once in LDS; demod, noise, bias, LeakyReLU·√2)."""
+    (modulated input, halo modulated once in LDS; demod, noise, bias, LeakyReLU·√2).
+    s3: the one-halo-buffer tile with a 3-stage weight ring (MIA_HALO_S3), both loops, also
+    bit-identical to the default two-halo-buffer tile."""
     g = torch.Generator().manual_seed(C + H + W + len(mode) + (dtype == torch.bfloat16))
     if C == 64:  # the 64-channel halo tile for every 64-channel launch (default: bf16 forward)
         tune("MIA_HALO_C64", 1)
+    if s3:
+        tune("MIA_HALO_S3", "4096")
     N = 2
     x = torch.randn(N, C, H, W, generator=g)
     w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
@@ -1298,6 +1304,13 @@ def test_halo_lowp_unrolled_bitwise(cuda, tune, dtype, C, H, W, mode):
         return y.clone(), sd, q
 
     y_def, sd_def, q_def = run()
+    if s3:  # the default two-halo-buffer tile
+        tune("MIA_HALO_S3", "0")
+        y_2, sd_2, q_2 = run()
+        assert torch.equal(y_def, y_2), (mode, (y_def.float() - y_2.float()).abs().max().item())
+        if mode == "sdot_bab":
+            assert torch.equal(sd_def, sd_2) and torch.equal(q_def, q_2)
+        tune("MIA_HALO_S3", "4096")
     tune("MIA_HALO_EPI", "2")
     y_rol, sd_rol, q_rol = run()
     if mode != "sdot_bab":
@@ -1356,6 +1369,9 @@ def test_x6_128_two_block_form_bitwise(cuda, tune, Cin, Cout, H, W, mode):
     d = torch.rand(N, Cout, generator=g) + 0.5
     noise = torch.randn(H * W, generator=g)
     wf = layouts.fwd_matrix(w, f32).to(cuda)
+    wm = torch.zeros(Cout, ops.conv2d_kpad(9, Cin, f32))
+    wm[:, :9 * Cin] = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
+    grp = [dict(w=wm.to(cuda), kh=3, kw=3, pad=(1, 1), ho=H, wo=W)]
 
     def run():
         y = nhwc(y0, f32).to(cuda)
@@ -1382,7 +1398,10 @@ def test_x6_128_two_block_form_bitwise(cuda, tune, Cin, Cout, H, W, mode):
             kw = dict(out_scale=so.to(cuda), aux_x=nhwc(a, f32).to(cuda), sdot=sd,
                       bab=dict(demod=d.to(cuda), noise=noise.to(cuda), noise_w=0.3,
                                bias=b.to(cuda), q=q))
-        ops.conv3x3(nhwc(x, f32).to(cuda), wf, y, cout=Cout, **kw)
+        if mode in ("prelu", "mask_slope"):  # the e4e layers' entry point
+            ops.conv2d(nhwc(x, f32).to(cuda), grp, y, (H, W), cout=Cout, **kw)
+        else:
+            ops.conv3x3(nhwc(x, f32).to(cuda), wf, y, cout=Cout, **kw)
         torch.cuda.synchronize()
         return y, sd, q
 

@@ -29,13 +29,6 @@
 #ifndef MIA_HALO_PREMOD
 #define MIA_HALO_PREMOD 1
 #endif
-// MIA_HALO_BMIX = 1 (tuning A/B build, `make variant VARIANT=bmix VARIANT_FLAGS=-DMIA_HALO_BMIX=1`):
-// on the 4-wave 2-stage tiles every wave streams a quarter of each K-step's weights (the H-waves
-// issue theirs before their halo pieces and wait with vmcnt(#halo pieces of the step)), instead of
-// the two B-waves 8 pieces each while the H-waves issue weights never
-#ifndef MIA_HALO_BMIX
-#define MIA_HALO_BMIX 0
-#endif
 
 
 namespace mia {
@@ -160,28 +153,6 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
     }
   }
   const int ncb = Cin / BK, nk = 9 * ncb;
-  // BMIX: every wave's weight pieces (rows (wid·BMI + j)·8 + lane/8)
-  constexpr bool BMIX = MIA_HALO_BMIX && TL::NW == 4 && TL::STAGES == 2 && EPI >= 0;
-  constexpr int BMI = BMIX ? BN / (8 * TL::NW) : 1;
-  const T* wsrc[BMI];
-#pragma unroll
-  for (int j = 0; j < BMI; ++j) {
-    const int row = (wid * BMI + j) * 8 + (lane >> 3);
-    wsrc[j] = n0 + row < Cout ? Wt + (size_t)(n0 + row) * G.kpad + ((lane & 7) ^ fsw(row)) * VEC
-                              : nullptr;
-  }
-  auto issue_bm = [&](int s, int st) {  // BMIX: this wave's share of K-step s's weights
-    const int cb = s / 9, t = s - (s / 9) * 9;
-    const int koff = t * Cin + cb * BK;
-    char* dst = bring + st * BSTAGE;
-#pragma unroll
-    for (int j = 0; j < BMI; ++j) {
-      const T* a = wsrc[j] ? wsrc[j] + koff : zero;
-      __builtin_amdgcn_global_load_lds((gptr_t)a, (lptr_t)(dst + (wid * BMI + j) * 1024), 16, 0,
-                                       0);
-    }
-  };
-
   auto issue_b = [&](int s, int st) {  // B-wave: its weight pieces of K-step s = (cb, tap)
     const int cb = s / 9, t = s - (s / 9) * 9;
     const int koff = t * Cin + cb * BK;
@@ -215,36 +186,11 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
     }
   };
 
-  // NHBUF = 1 (one halo buffer, the LDS it frees going to a deeper weight ring): after the last
-  // tap of a channel block (every wave past its reads: the step-end barrier) the H-waves fetch the
-  // next block's halo into the same buffer; the block waits for it (the co-resident block's main
-  // loop runs meanwhile) while the B-waves' weight pieces stay in flight
-  auto next_block_single = [&](int cb) {
-    if (!bwave) {
-#pragma unroll
-      for (int j = 0; j < H_INS; ++j)
-        if (j < my_pieces) issue_h(cb, j, 0);
-      wait_vmcnt(0);
-    }
-    __syncthreads();
-    if constexpr (PRO && MIA_HALO_PREMOD) {
-      premod(cb, 0);
-      __syncthreads();
-    }
-  };
-
   // ---- prologue: halo of channel block 0, weights of steps 0 … STAGES−2, style row -----------
   // (the style row after the DMA issue: its load latency overlaps the DMA's instead of preceding
   // it; with the epilogue-operand prefetch below +0.1 … +1.3 % on the modulated forward,
   // bit-identical, r03 A/B)
-  if constexpr (BMIX) {
-    issue_bm(0, 0);  // every wave: its share of step 0 (STAGES = 2)
-    if (!bwave) {
-#pragma unroll
-      for (int j = 0; j < H_INS; ++j)
-        if (j < my_pieces) issue_h(0, j, 0);
-    }
-  } else if (bwave) {
+  if (bwave) {
 #pragma unroll
     for (int s = 0; s < STAGES - 1; ++s) issue_b(s, s);  // nk ≥ 9
   } else {
@@ -259,7 +205,7 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
       stab[i] = from_f<T>(sv * mul);
     }
   }
-  if (bwave && !BMIX) wait_vmcnt((STAGES - 2) * B_INS);  // step 0 landed, 1, 2 may stay in flight
+  if (bwave) wait_vmcnt((STAGES - 2) * B_INS);  // step 0 landed, 1, 2 may stay in flight
   else wait_vmcnt(0);
   __syncthreads();
   if constexpr (PRO && MIA_HALO_PREMOD) {
@@ -334,11 +280,7 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
         const char* ha = hbuf + hoff;
         const char* sb = bring + soff;
         const int dy = t / 3, dx = t % 3;
-        if constexpr (BMIX) {
-          if (s + 1 < nk) issue_bm(s + 1, st ^ 1);
-        } else {
-          if (bwave && s + STAGES - 1 < nk) issue_b(s + STAGES - 1, st == 0 ? STAGES - 1 : st - 1);
-        }
+        if (bwave && s + STAGES - 1 < nk) issue_b(s + STAGES - 1, st == 0 ? STAGES - 1 : st - 1);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           VT af[FM], bf[FN];
@@ -370,15 +312,8 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
             __builtin_amdgcn_sched_barrier(0);
           }
         }
-        if constexpr (BMIX) {
-          // this wave's weights of step s+1 (issued before its halo pieces of this step)
-          const int hq = (!bwave && cb + 1 < ncb && t * HPS < H_INS)
-                             ? max(0, min(HPS, min(H_INS, my_pieces) - t * HPS)) : 0;
-          wait_vmcnt(hq);
-        } else {
-          if (bwave) wait_vmcnt(B_INS * max(0, min(STAGES - 2, nk - 2 - s)));
-          else if (t == 8) wait_vmcnt(0);
-        }
+        if (bwave) wait_vmcnt(B_INS * max(0, min(STAGES - 2, nk - 2 - s)));
+        else if (t == 8) wait_vmcnt(0);
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of stage st are done
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
@@ -387,9 +322,6 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
             premod(cb + 1, (cb + 1) & 1);
             __syncthreads();
           }
-        }
-        if constexpr (TL::NHBUF == 1) {
-          if (t == 8 && cb + 1 < ncb) next_block_single(cb + 1);
         }
         st = st + 1 == STAGES ? 0 : st + 1;
       }
@@ -474,9 +406,6 @@ __global__ __launch_bounds__(TL::NT, TL::WAVES_PER_SIMD) void conv_halo_kernel(c
         __syncthreads();
       }
     }
-    if constexpr (TL::NHBUF == 1) {
-      if (t == 8 && cb + 1 < ncb) next_block_single(cb + 1);
-    }
     st = st + 1 == STAGES ? 0 : st + 1;
     if (++t == 9) { t = 0; ++cb; }
   }
@@ -543,6 +472,8 @@ static int launch_halo_tile_(ConvK& k, hipStream_t st) {
   lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
   lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
   if (lds > 160 * 1024) return set_error("conv_halo: LDS budget exceeded");
+  if (TL::NHBUF == 1 && k.a.Cin != ROWB / (int)sizeof(T))
+    return set_error("conv_halo: single-buffer tile needs Cin = one channel block");
   auto fn = conv_halo_kernel<T, TL, PRO, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -632,9 +563,6 @@ int launch_conv_halo(ConvK& k, int dtype, hipStream_t st) {
   // (round 3, fp16 / bf16 modulated forward at 256² / 128² / 64², bit-identical outputs:
   // 16×16 patches on 8 waves with a 3-stage ring −1.9 … +2.1 %, on 4 waves −9 … −18 %)
   typedef HaloTile<128, 8, 2> Small;
-  // T_HALO_S3 (largest Cin taken): one halo buffer and a 3-stage weight ring, the weights issued
-  // two K-steps ahead (the L2 → LDS latency of a piece is about one K-step of the 2-stage ring)
-  typedef HaloTile<128, 8, 3, 1> Small3;
   typedef HaloTile<64, 8, 3> Small64;
   // Cout ≤ 32 (VGG input gradient): little MFMA work per K-step, so the weights of all nine taps
   // of a one-block Cin are DMA'd in the prologue (9 stages, 36 KB) and no step waits on L2.
@@ -651,9 +579,6 @@ int launch_conv_halo(ConvK& k, int dtype, hipStream_t st) {
     if (k.a.Cout <= 64)  // (specialised epilogues + unrolled taps, as the 128-channel tile)
       return pro ? launch_halo_tile<T, Small64, true, true>(k, st)
                  : launch_halo_tile<T, Small64, false, true>(k, st);
-    if (k.a.Cin <= tune(T_HALO_S3))  // one halo buffer + a 3-stage weight ring (74 KB)
-      return pro ? launch_halo_tile<T, Small3, true, true>(k, st)
-                 : launch_halo_tile<T, Small3, false, true>(k, st);
     return pro ? launch_halo_tile<T, Small, true, true>(k, st)
                : launch_halo_tile<T, Small, false, true>(k, st);
   });

@@ -752,278 +752,6 @@ static int launch_x6s(ConvK& k, hipStream_t st, bool pro) {
   }
 }
 
-// ---- the ≥ 128-channel layers, two blocks per CU (round 4) -------------------------------------
-// The 128-column analogue of HaloX6S: an 8 × 16 patch × 128 channels on 4 waves (2 row × 2 column
-// waves of 4 × 4 fragments — the 8-wave tile's wave tile), one halo buffer + lo, and the weights
-// staged per HALF K-step (16 k): a stage is 128 rows of 64-B [hi|mid] + 32-B lo records (12 KB),
-// so the block fits 58 KB and two blocks share a CU. Each K-step (tap, half) is 48 MFMAs per wave
-// and 3 weight pieces per wave; the halo of the next 32-channel block is fetched by all waves after
-// the block's last step. Stage rows are 64 B: the [hi|mid] chunk is swizzled by
-// 3·((row >> 3) & 1) and the lo 8-B slot by 2·((row >> 3) & 1), which puts every ds_read_b128 lane
-// group (and both ds_read_b64 halves) of a fragment read on distinct bank slots. Same MFMAs in the
-// same order per output as the 8-wave tile (bit-identical).
-__device__ __forceinline__ int fsw64(int row) { return ((row >> 3) & 1) * 3; }
-__device__ __forceinline__ int lsw32(int row) { return ((row >> 3) & 1) * 2; }
-
-struct HaloX6H {
-  static constexpr int PH = 8, PW = 16, NW = 4, NT = 64 * NW;
-  static constexpr int WN = 2, WM = 2, FM = 4, FN = 4;
-  static constexpr int BM = PH * PW, BN = 128, BK = 32, KH = 16;  // KH: k per K-step
-  static constexpr int HSIDE = PW + 2, HROWS = (PH + 2) * HSIDE;  // 180 halo pixels
-  static constexpr int HPIECES = (HROWS + 7) / 8;                 // 23 pieces of 8 rows
-  // the halo buffer holds the 180 rows exactly: the last DMA piece's 4 extra rows (zero page)
-  // land in the first rows of the lo buffer, which the split rewrites after every halo DMA
-  static constexpr int HBUF = HROWS * ROWB;
-  static constexpr int LROWB = 64, LBUF = HROWS * LROWB;
-  static constexpr int SROWB = KH * 4, SLROWB = KH * 2;           // stage rows: 64 B, 32 B
-  static constexpr int BHM = BN * SROWB, BSTAGE = BHM + BN * SLROWB;  // 12 KB
-  static constexpr int B_HM_INS = BHM / 1024 / NW, B_L_INS = BN * SLROWB / 1024 / NW;  // 2 + 1
-  static constexpr int H_INS = (HPIECES + NW - 1) / NW;          // 6
-  static constexpr int EROWS = 128, ES = BN + 4;
-  static constexpr int LDS = HBUF + LBUF + 2 * BSTAGE;
-  static_assert(WM * FM * 16 == BM && WN * FN * 16 == BN, "");
-  static_assert(B_HM_INS * NW * 1024 == BHM && B_L_INS * NW * 1024 == BN * SLROWB, "");
-  static_assert(HPIECES * 1024 <= HBUF + 1024 && LDS <= 80 * 1024, "two blocks per CU");
-};
-
-template <bool PRO, int EPI>
-__global__ __launch_bounds__(HaloX6H::NT, 2) void conv_halo_x6h_kernel(const ConvK k) {
-  static_assert(EPI >= 0, "the specialised register epilogues only");
-  typedef HaloX6H TL;
-  constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, NT = TL::NT, BN = TL::BN, BK = TL::BK;
-  constexpr int KH = TL::KH, HSIDE = TL::HSIDE, HROWS = TL::HROWS, HPIECES = TL::HPIECES;
-  constexpr int H_INS = TL::H_INS, B_HM_INS = TL::B_HM_INS, B_L_INS = TL::B_L_INS;
-  constexpr int BSTAGE = TL::BSTAGE, SROWB = TL::SROWB, SLROWB = TL::SLROWB;
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* const hbuf = smem;                 // the halo: raw fp32, then [hi|mid] in place
-  char* const lbuf = smem + TL::HBUF;      // lo of the current channel block
-  char* const bring = lbuf + TL::LBUF;     // 2 half-step stages of pre-split weights
-
-  const mia_conv_args& p = k.a;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid / WN, wn = wid % WN;
-  const ConvGroup G = k.g[0];
-  const int H = p.H, W = p.W, Cin = p.Cin, Cout = p.Cout, Kpad = G.kpad;
-  const int bl = xcd_remap(blockIdx.x, k.nblk);
-  const int mt = bl / k.nbn, n0 = (bl % k.nbn) * BN;
-  const int ptx = W / TL::PW, pty = H / TL::PH;
-  const int x0 = (mt % ptx) * TL::PW;
-  const int y0 = ((mt / ptx) % pty) * TL::PH;
-  const int n = mt / (ptx * pty);
-
-  const float* __restrict__ X = (const float*)p.x;
-  const unsigned* __restrict__ Whm = (const unsigned*)G.w_split;               // [Cout][Kpad]
-  const __bf16* __restrict__ Wl = (const __bf16*)(Whm + (size_t)Cout * Kpad);  // [Cout][Kpad]
-  const char* zero = (const char*)g_zero16;
-
-  // this wave's weight pieces: [hi|mid] pieces of 16 rows × 64 B, lo pieces of 32 rows × 32 B
-  const char* wsrc[B_HM_INS + B_L_INS];
-#pragma unroll
-  for (int j = 0; j < B_HM_INS + B_L_INS; ++j) {
-    if (j < B_HM_INS) {
-      const int row = (wid * B_HM_INS + j) * 16 + (lane >> 2);
-      const int c = min(n0 + row, Cout - 1);  // rows past Cout: never stored or summed
-      wsrc[j] = (const char*)(Whm + (size_t)c * Kpad) + ((lane & 3) ^ fsw64(row)) * 16;
-    } else {
-      const int row = (wid * B_L_INS + j - B_HM_INS) * 32 + (lane >> 1);
-      const int c = min(n0 + row, Cout - 1);
-      wsrc[j] = (const char*)(Wl + (size_t)c * Kpad) + ((lane & 1) ^ (lsw32(row) >> 1)) * 16;
-    }
-  }
-  const char* hsrc[H_INS];
-#pragma unroll
-  for (int j = 0; j < H_INS; ++j) {
-    hsrc[j] = nullptr;
-    const int hr = (wid + TL::NW * j) * 8 + (lane >> 3);
-    const int hy = hr / HSIDE, hx = hr - (hr / HSIDE) * HSIDE;
-    const int y = y0 + hy - 1, x = x0 + hx - 1;
-    if (hr < HROWS && y >= 0 && y < H && x >= 0 && x < W)
-      hsrc[j] = (const char*)(X + ((size_t)(n * H + y) * W + x) * Cin + ((lane & 7) ^ fsw(hr)) * 4);
-  }
-  const int ncb = Cin / BK, nk = 18 * ncb;  // K-steps: (channel block, tap, half)
-
-  auto issue_b = [&](int s, int st) {  // this wave's weight pieces of K-step s
-    const int cb = s / 18, r = s - cb * 18, t = r >> 1, hh = r & 1;
-    const size_t koff = (size_t)t * Cin + cb * BK + hh * KH;
-    char* dst = bring + st * BSTAGE;
-#pragma unroll
-    for (int j = 0; j < B_HM_INS; ++j)
-      __builtin_amdgcn_global_load_lds((gptr_t)(wsrc[j] + koff * 4),
-                                       (lptr_t)(dst + (wid * B_HM_INS + j) * 1024), 16, 0, 0);
-#pragma unroll
-    for (int j = 0; j < B_L_INS; ++j)
-      __builtin_amdgcn_global_load_lds((gptr_t)(wsrc[B_HM_INS + j] + koff * 2),
-                                       (lptr_t)(dst + TL::BHM + (wid * B_L_INS + j) * 1024), 16,
-                                       0, 0);
-  };
-  auto issue_halo = [&](int cb) {
-#pragma unroll
-    for (int j = 0; j < H_INS; ++j) {
-      if (wid + TL::NW * j >= HPIECES) break;
-      const char* a = hsrc[j] ? hsrc[j] + (size_t)cb * BK * 4 : zero;
-      __builtin_amdgcn_global_load_lds((gptr_t)a, (lptr_t)(hbuf + (wid + TL::NW * j) * 1024), 16,
-                                       0, 0);
-    }
-  };
-  const bool lrelu_in = p.act_in == MIA_ACT_LRELU_S2;
-  auto convert = [&](int cb) {
-    for (int c = tid; c < HROWS * 8; c += NT) {
-      const int hr = c >> 3, pc = c & 7, lc = pc ^ fsw(hr);
-      f32x4 v = *(const f32x4*)(hbuf + hr * ROWB + pc * 16);
-      if constexpr (PRO) {
-        const float mul = lrelu_in ? SQRT2 : 1.f;
-        f32x4 s4 = {1.f, 1.f, 1.f, 1.f};
-        if (p.in_scale) s4 = *(const f32x4*)(p.in_scale + (size_t)n * Cin + cb * BK + lc * 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float f = v[e];
-          if (lrelu_in) f = fmaxf(f, 0.2f * f);
-          v[e] = f * (s4[e] * mul);
-        }
-      }
-      u32x4 hm;
-      u32x2 lo;
-      split_quad(v, hm, lo);
-      *(u32x4*)(hbuf + hr * ROWB + pc * 16) = hm;
-      *(u32x2*)(lbuf + hr * TL::LROWB + ((lc ^ lsw(hr)) << 3)) = lo;
-    }
-  };
-
-  issue_halo(0);
-  issue_b(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  convert(0);
-  __syncthreads();
-
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int frow = lane & 15, fq = lane >> 4;
-  int oh[FM + 2][3], ol[FM + 2][3], ob[FN], obl[FN];
-#pragma unroll
-  for (int q = 0; q < FM + 2; ++q)
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const int hr = (wm * FM + q) * HSIDE + frow + c;
-      int vh = hr * ROWB + ((fq ^ fsw(hr)) << 4), vl = hr * TL::LROWB + ((fq ^ lsw(hr)) << 3);
-      asm volatile("" : "+v"(vh), "+v"(vl));
-      oh[q][c] = vh;
-      ol[q][c] = vl;
-    }
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    const int row = wn * FN * 16 + 16 * j + frow;
-    int vb = row * SROWB + ((fq ^ fsw64(row)) << 4), vbl = TL::BHM + row * SLROWB +
-                                                          ((fq ^ lsw32(row)) << 3);
-    asm volatile("" : "+v"(vb), "+v"(vbl));
-    ob[j] = vb;
-    obl[j] = vbl;
-  }
-  int st = 0;
-  for (int cb = 0; cb < ncb; ++cb) {
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int s = (cb * 9 + t) * 2 + h;
-        int x1 = 64, x2 = 32, soff = st * BSTAGE;
-        asm volatile("" : "+s"(x1), "+s"(x2), "+s"(soff));
-        const int dy = t / 3, dx = t % 3;
-        const char* sb = bring + soff;
-        if (s + 1 < nk) issue_b(s + 1, st ^ 1);
-        u32x4 ahm[FM], bhm[FN];
-        u32x2 al[FM], blo[FN];
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          ahm[i] = *(const u32x4*)(hbuf + (h ? oh[i + dy][dx] ^ x1 : oh[i + dy][dx]));
-          al[i] = *(const u32x2*)(lbuf + (h ? ol[i + dy][dx] ^ x2 : ol[i + dy][dx]));
-        }
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          bhm[j] = *(const u32x4*)(sb + ob[j]);
-          blo[j] = *(const u32x2*)(sb + obl[j]);
-        }
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-            acc[i][j] = mfma_x6(bhm[j], blo[j], ahm[i], al[i], acc[i][j]);  // D[ch][px]
-        __builtin_amdgcn_s_setprio(0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of step s+1
-        lds_handoff();
-        __builtin_amdgcn_sched_barrier(0);
-        st ^= 1;
-      }
-    }
-    if (cb + 1 < ncb) {  // every wave is past its last read of the halo and lo
-      issue_halo(cb + 1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      convert(cb + 1);
-      __syncthreads();
-    }
-  }
-  halo_epilogue_f<float, TL, EPI>(k, acc, n, y0, x0, n0, wm, wn, lane, -1, -1, nullptr,
-                                  k.prered ? (float*)smem : nullptr, TL::WM, TL::BN);
-}
-
-template <bool PRO, int EPI>
-static int launch_x6h_(ConvK& k, hipStream_t st) {
-  typedef HaloX6H TL;
-  k.nbn = (k.a.Cout + TL::BN - 1) / TL::BN;
-  k.nblk = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW) * k.nbn;
-  size_t lds = TL::LDS;
-  lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
-  lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
-  auto fn = conv_halo_x6h_kernel<PRO, EPI>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            80 * 1024) != hipSuccess)
-      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-    attr_set = true;
-  }
-  k.prered = prered_enabled() && (EPI & epi::CSUM);
-  const int nslots = halo_red_slots(k.a.H, k.a.W, TL::FM, TL::WM, k.prered);
-  RedQ r;
-  int rc = conv_red_begin(k, r, nslots, st);
-  if (rc != MIA_OK) return rc;
-  hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), lds, st, k);
-  rc = check_launch("conv_halo_x6h");
-  return rc != MIA_OK ? rc : red_finish(r, st);
-}
-
-// T_X6_128S (largest Cin taken; 0 = never): the Cout > 64 launches with a specialised epilogue
-// on the two-blocks-per-CU 128-column tile; returns X6S_NONE (not handled) for any other mask
-static int launch_x6h(ConvK& k, hipStream_t st, bool pro) {
-  using namespace epi;
-  const int f = epi_mask(k);
-  if (pro) {
-    if (f == (OSC | NOISE | BIAS | LRELU)) return launch_x6h_<true, OSC | NOISE | BIAS | LRELU>(k, st);
-    return X6S_NONE;
-  }
-  switch (f) {
-    case 0: return launch_x6h_<false, 0>(k, st);
-    case BIAS: return launch_x6h_<false, BIAS>(k, st);
-    case BIAS | RELU: return launch_x6h_<false, BIAS | RELU>(k, st);
-    case PRELU: return launch_x6h_<false, PRELU>(k, st);
-    case MASK: return launch_x6h_<false, MASK>(k, st);
-    case TAP: return launch_x6h_<false, TAP>(k, st);
-    case ACC: return launch_x6h_<false, ACC>(k, st);
-    case MASK | MSL: return launch_x6h_<false, MASK | MSL>(k, st);
-    case OSC | SDOT: return launch_x6h_<false, OSC | SDOT>(k, st);
-    case OSC | SDOT | BAB: return launch_x6h_<false, OSC | SDOT | BAB>(k, st);
-    default: return X6S_NONE;
-  }
-}
-
 // The register epilogue specialised for the feature masks of the attack's fp32 launches (every aux
 // load of a row chunk hoisted, compile-time features; halo_epilogue.h): the runtime-generic one
 // issues its per-row loads one dependent round trip at a time, ≈ 10 % of a block's cycles
@@ -1127,10 +855,6 @@ int launch_conv_halo_x6(ConvK& k, hipStream_t st) {
     if (sel == 0) return pro ? launch_x6_<64, true, -2>(k, st) : launch_x6_<64, false, -2>(k, st);
     if (sel == 1) return pro ? launch_x6_spec<64, true>(k, st) : launch_x6_spec<64, false>(k, st);
     return pro ? launch_x6_<64, true, -1>(k, st) : launch_x6_<64, false, -1>(k, st);
-  }
-  if (sel == 1 && k.a.Cin <= tune(T_X6_128S) && k.a.H % HaloX6H::PH == 0) {
-    const int rc = launch_x6h(k, st, pro);
-    if (rc != X6S_NONE) return rc;
   }
   if (sel == 0) return pro ? launch_x6_<128, true, -2>(k, st) : launch_x6_<128, false, -2>(k, st);
   if (sel == 1) return pro ? launch_x6_spec<128, true>(k, st) : launch_x6_spec<128, false>(k, st);

@@ -100,10 +100,6 @@ enum TuneKey {
                      // (profiles/r03_thin_f32_ab.txt)
   T_X6_64S,          // fp32 Cout = 64: 1 (default) the two-blocks-per-CU x6 tile (conv_halo_x6.hip
                      // HaloX6S, also the VGG tap-pair gradient), 0 the 8-wave 64-column tile
-  T_X6_128S,         // fp32 Cout > 64 with Cin ≤ this value: the two-blocks-per-CU 128-column x6
-                     // tile (conv_halo_x6.hip HaloX6H, half-K steps); 0 = never
-  T_HALO_S3,         // 2-byte halo, Cout > 64 with Cin ≤ this value: one halo buffer + a 3-stage
-                     // weight ring (conv_halo.hip Small3); 0 = never
   T_UPCONV_X6S,      // fp32 split-once stride-2 input gradient with Cin ≤ 512: 1 (default) the
                      // 8 × 16-patch two-blocks-per-CU form (conv_upconv.hip DgX6S), 0 the 8-wave one
   T_NKEYS

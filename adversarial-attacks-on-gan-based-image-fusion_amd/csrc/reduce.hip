@@ -35,7 +35,7 @@ TuneDef g_tune[T_NKEYS] = {
     {"MIA_S2DG_X6", 1},   {"MIA_S2DG_HALO", 1},     {"MIA_UPCONV_X6", 1},   {"MIA_UPCONV_HALO", 1},
     {"MIA_EPI_PRERED", 1},    {"MIA_CONV_WRES32", 1},
     {"MIA_HALO_C64", 1},  {"MIA_THIN_F32", 3},      {"MIA_X6_64S", 1},
-    {"MIA_X6_128S", 0},   {"MIA_HALO_S3", 0},       {"MIA_UPCONV_X6S", 1}};
+    {"MIA_UPCONV_X6S", 1}};
 std::once_flag g_tune_once;
 void tune_init() {
   for (auto& d : g_tune) {

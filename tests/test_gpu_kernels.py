@@ -1247,23 +1247,17 @@ def test_x6_halo_variants_bitwise(cuda, tune, C, H, W, mode):
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("C,H,W,s3", [(128, 32, 16, False), (256, 16, 32, False),
-                                      (64, 32, 32, False), (128, 32, 16, True),
-                                      (256, 16, 32, True)])
+@pytest.mark.parametrize("C,H,W", [(128, 32, 16), (256, 16, 32), (64, 32, 32)])
 @pytest.mark.parametrize("mode", ["plain", "bias_relu", "mask", "tap", "mod", "sdot_bab"])
-def test_halo_lowp_unrolled_bitwise(cuda, tune, dtype, C, H, W, s3, mode):
+def test_halo_lowp_unrolled_bitwise(cuda, tune, dtype, C, H, W, mode):
     """fp16 / bf16 halo kernel (conv_halo.hip): the specialised-epilogue launches run the taps
     unrolled over lane-constant fragment offsets; the runtime-feature epilogue (MIA_HALO_EPI=2)
     runs the rolled loop. Same reads, same MFMAs in the same order: outputs (and sdot / q sums)
     bit-identical; both within the dtype's tolerance of fp64. 'mod' = the StyledConv forward
-    (modulated input, halo modulated once in LDS; demod, noise, bias, LeakyReLU·√2).
-    s3: the one-halo-buffer tile with a 3-stage weight ring (MIA_HALO_S3), both loops, also
-    bit-identical to the default two-halo-buffer tile."""
+    (modulated input, halo modulated once in LDS; demod, noise, bias, LeakyReLU·√2)."""
     g = torch.Generator().manual_seed(C + H + W + len(mode) + (dtype == torch.bfloat16))
     if C == 64:  # the 64-channel halo tile for every 64-channel launch (default: bf16 forward)
         tune("MIA_HALO_C64", 1)
-    if s3:
-        tune("MIA_HALO_S3", "4096")
     N = 2
     x = torch.randn(N, C, H, W, generator=g)
     w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
@@ -1304,13 +1298,6 @@ def test_halo_lowp_unrolled_bitwise(cuda, tune, dtype, C, H, W, s3, mode):
         return y.clone(), sd, q
 
     y_def, sd_def, q_def = run()
-    if s3:  # the default two-halo-buffer tile
-        tune("MIA_HALO_S3", "0")
-        y_2, sd_2, q_2 = run()
-        assert torch.equal(y_def, y_2), (mode, (y_def.float() - y_2.float()).abs().max().item())
-        if mode == "sdot_bab":
-            assert torch.equal(sd_def, sd_2) and torch.equal(q_def, q_2)
-        tune("MIA_HALO_S3", "4096")
     tune("MIA_HALO_EPI", "2")
     y_rol, sd_rol, q_rol = run()
     if mode != "sdot_bab":
@@ -1340,95 +1327,6 @@ def test_halo_lowp_unrolled_bitwise(cuda, tune, dtype, C, H, W, s3, mode):
         got = y_def.permute(0, 3, 1, 2).double().cpu()
         tol = 2e-2 if dtype == torch.float16 else 1e-1
         assert ((got - ref).abs().max() / ref.abs().max()).item() < tol, mode
-
-
-@pytest.mark.parametrize("Cin,Cout,H,W", [(128, 128, 16, 32), (256, 192, 16, 16),
-                                           (64, 128, 32, 16), (512, 512, 16, 16)])
-@pytest.mark.parametrize("mode", ["plain", "bias_relu", "prelu", "mask", "mask_slope", "acc", "tap",
-                                  "mod", "sdot_bab"])
-def test_x6_128_two_block_form_bitwise(cuda, tune, Cin, Cout, H, W, mode):
-    """fp32 split-once halo kernel, Cout > 64: the 8 × 16-patch two-blocks-per-CU tile with half-K
-    weight stages (MIA_X6_128S ≥ Cin) computes the same MFMAs in the same order as the 8-wave
-    16 × 16 tile (MIA_X6_128S=0): outputs bit-identical for every specialised epilogue of the
-    attack's fp32 launches (the modulated StyledConv forward and its backward front included;
-    Cout = 192 exercises the clamped weight rows of a partial column tile); the sdot / q sums,
-    whose slot partition follows the patch shape, within 1e-5; and against fp64."""
-    g = torch.Generator().manual_seed(Cin + 3 * Cout + H + W + len(mode))
-    N = 2
-    f32 = torch.float32
-    x = torch.randn(N, Cin, H, W, generator=g)
-    w = torch.randn(Cout, Cin, 3, 3, generator=g) / math.sqrt(9 * Cin)
-    y0 = torch.randn(N, Cout, H, W, generator=g)
-    b = torch.randn(Cout, generator=g) * 0.1
-    slope = torch.rand(Cout, generator=g) * 0.5 + 0.05
-    m = torch.randn(N, Cout, H, W, generator=g)
-    a = torch.randn(N, Cout, H, W, generator=g).relu()
-    t = torch.randn(N, Cout, H, W, generator=g)
-    s = torch.rand(N, Cin, generator=g) + 0.5
-    so = torch.rand(N, Cout, generator=g) + 0.5
-    d = torch.rand(N, Cout, generator=g) + 0.5
-    noise = torch.randn(H * W, generator=g)
-    wf = layouts.fwd_matrix(w, f32).to(cuda)
-    wm = torch.zeros(Cout, ops.conv2d_kpad(9, Cin, f32))
-    wm[:, :9 * Cin] = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
-    grp = [dict(w=wm.to(cuda), kh=3, kw=3, pad=(1, 1), ho=H, wo=W)]
-
-    def run():
-        y = nhwc(y0, f32).to(cuda)
-        sd = torch.zeros(N * Cout, device=cuda) if mode == "sdot_bab" else None
-        q = torch.zeros(N * Cout, device=cuda) if mode == "sdot_bab" else None
-        kw = {}
-        if mode == "bias_relu":
-            kw = dict(bias=b.to(cuda), act_out=ops.ACT_RELU)
-        elif mode == "prelu":
-            kw = dict(act_out=ops.ACT_PRELU, act_slope=slope.to(cuda))
-        elif mode == "mask":
-            kw = dict(mask_a=nhwc(m, f32).to(cuda))
-        elif mode == "mask_slope":
-            kw = dict(mask_a=nhwc(m, f32).to(cuda), mask_slope=slope.to(cuda))
-        elif mode == "acc":
-            kw = dict(accumulate=True)
-        elif mode == "tap":
-            kw = dict(tap_a=nhwc(a, f32).to(cuda), tap_t=nhwc(t, f32).to(cuda), tap_coef=0.37)
-        elif mode == "mod":
-            kw = dict(in_scale=s.to(cuda), act_in=ops.ACT_LRELU_S2, out_scale=d.to(cuda),
-                      noise=noise.to(cuda), noise_w=0.3, bias=b.to(cuda),
-                      act_out=ops.ACT_LRELU_S2)
-        elif mode == "sdot_bab":
-            kw = dict(out_scale=so.to(cuda), aux_x=nhwc(a, f32).to(cuda), sdot=sd,
-                      bab=dict(demod=d.to(cuda), noise=noise.to(cuda), noise_w=0.3,
-                               bias=b.to(cuda), q=q))
-        if mode in ("prelu", "mask_slope"):  # the e4e layers' entry point
-            ops.conv2d(nhwc(x, f32).to(cuda), grp, y, (H, W), cout=Cout, **kw)
-        else:
-            ops.conv3x3(nhwc(x, f32).to(cuda), wf, y, cout=Cout, **kw)
-        torch.cuda.synchronize()
-        return y, sd, q
-
-    tune("MIA_X6_128S", "4096")
-    y1, sd1, q1 = run()
-    tune("MIA_X6_128S", "0")
-    y0_, sd0, q0 = run()
-    assert torch.equal(y1, y0_), (mode, (y1 - y0_).abs().max().item())
-    if mode == "sdot_bab":
-        for u, v in ((sd1, sd0), (q1, q0)):
-            assert ((u - v).abs().max() / v.abs().max()).item() < 1e-5
-        return
-    conv = F.conv2d(x.double(), w.double(), padding=1)
-    bd, sl = b.double().view(1, Cout, 1, 1), slope.double().view(1, Cout, 1, 1)
-    if mode == "mod":
-        xa = F.leaky_relu(x.double(), 0.2) * math.sqrt(2) * s.double().view(N, Cin, 1, 1)
-        pre = F.conv2d(xa, w.double(), padding=1) * d.double().view(N, Cout, 1, 1) \
-            + 0.3 * noise.double().view(1, 1, H, W) + bd
-        ref = F.leaky_relu(pre, 0.2) * math.sqrt(2)
-    else:
-        ref = {"plain": conv, "bias_relu": F.relu(conv + bd),
-               "prelu": torch.where(conv > 0, conv, sl * conv),
-               "mask": conv * (m.double() > 0),
-               "mask_slope": torch.where(m.double() > 0, conv, sl * conv),
-               "acc": conv + y0.double(),
-               "tap": conv + 0.37 * (a.double() - t.double())}[mode]
-    assert rel_err(nchw(y1), ref) < 2 * TOL[f32], mode
 
 
 @pytest.mark.parametrize("R,cin,cout", [(16, 64, 128), (32, 128, 64)])

@@ -36,7 +36,7 @@ int main() {
                         "MIA_X6_64AUX", "MIA_CONV_THIN", "MIA_CONV_THIN32", "MIA_CONV_WRES",
                         "MIA_CONV_TILE", "MIA_CONV_REGEPI", "MIA_CONV_SMALLTILE", "MIA_S2DG_X6",
                         "MIA_S2DG_HALO", "MIA_UPCONV_X6", "MIA_UPCONV_HALO", "MIA_EPI_PRERED",
-                        "MIA_CONV_WRES32", "MIA_HALO_C64", "MIA_THIN_F32", "MIA_X6_64S", "MIA_X6_128S", "MIA_HALO_S3", "MIA_UPCONV_X6S"};
+                        "MIA_CONV_WRES32", "MIA_HALO_C64", "MIA_THIN_F32", "MIA_X6_64S", "MIA_UPCONV_X6S"};
   for (const char* k : keys) {
     int v = -1, w = -1;
     EXPECT(mia_get_tuning(k, &v) == MIA_OK, k);

@@ -257,7 +257,16 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
           blo[j] = *(const u32x2*)(sb + BN * ROWB + row * 64 + ((ch ^ lsw(row)) << 3));
         }
 #pragma unroll
-        for (int i = 0; i < FM; ++i) split_quad(af[i], ahm[i], alo[i]);
+        for (int i = 0; i < FM; ++i) {
+#ifdef MIA_PROBE_NOSPLIT_A  // timing probe only (wrong numerics): the A split's VALU removed
+          const u32x4 u = __builtin_bit_cast(u32x4, af[i]);  // hi = truncated bf16, mid = lo = 0
+          ahm[i] = u32x4{__builtin_amdgcn_perm(u[1], u[0], 0x07060302u),
+                         __builtin_amdgcn_perm(u[3], u[2], 0x07060302u), 0u, 0u};
+          alo[i] = u32x2{0u, 0u};
+#else
+          split_quad(af[i], ahm[i], alo[i]);
+#endif
+        }
         if (k.prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int i = 0; i < FM; ++i)

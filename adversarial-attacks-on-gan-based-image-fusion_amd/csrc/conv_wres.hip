@@ -237,7 +237,7 @@ static bool wres_mask_ok(int f) {
   using namespace epi;
   switch (f) {
     case BIAS | RELU: case TAP | MASK: case 0: case PRELU: case BIAS | CSUM: case MASK | MSL:
-    case ACC:
+    case ACC: case BIAS:
       return true;
     default:
       return false;
@@ -283,6 +283,7 @@ int launch_conv_wres(ConvK& k, int dtype, hipStream_t st) {
         case BIAS | CSUM: return launch_wres_<T, BIAS | CSUM>(k, grid, lds, st);
         case MASK | MSL: return launch_wres_<T, MASK | MSL>(k, grid, lds, st);
         case ACC: return launch_wres_<T, ACC>(k, grid, lds, st);
+        case BIAS: return launch_wres_<T, BIAS>(k, grid, lds, st);  // e4e conv2 (SE body)
         default: break;
       }
     }

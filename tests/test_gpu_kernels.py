@@ -817,7 +817,7 @@ def test_generic_tile_register_epilogues_stride2(cuda, tune, dtype, C, mode):
 @pytest.mark.parametrize("N,H,W,C", [(2, 192, 192, 64), (1, 16, 16, 64), (3, 16, 48, 64),
                                      (2, 32, 16, 128)])
 @pytest.mark.parametrize("mode", ["plain", "bias_relu", "tap_mask", "prelu", "bias_csum",
-                                  "mask_slope", "acc"])
+                                  "mask_slope", "acc", "bias"])
 @pytest.mark.parametrize("spec", ["1", "0"])
 def test_conv2d_register_epilogue_paths(cuda, tune, dtype, N, H, W, C, mode, spec):
     """Stride-1 C→C 3×3 convs with every epilogue feature set of the attack step (vgg.py, e4e
@@ -864,6 +864,10 @@ def test_conv2d_register_epilogue_paths(cuda, tune, dtype, N, H, W, C, mode, spe
         ref = conv + b.double().view(1, C, 1, 1)
         cs = torch.zeros(N, C, device=cuda)
         kw = dict(bias=b.to(cuda), csum=cs)
+    elif mode == "bias":  # e4e conv2 (the SE body; its pool sums in a separate pass)
+        b = torch.randn(C, generator=g) * 0.1
+        ref = conv + b.double().view(1, C, 1, 1)
+        kw = dict(bias=b.to(cuda))
     elif mode == "mask_slope":
         m = torch.randn(N, C, H, W, generator=g)
         ref = torch.where(m.to(dtype).double() > 0, conv, sl * conv)

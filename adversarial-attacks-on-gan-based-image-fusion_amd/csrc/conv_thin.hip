@@ -212,6 +212,95 @@ __global__ __launch_bounds__(256) void conv_thin_out_kernel(const T* __restrict_
   }
 }
 
+// Round 4: the same input gradient on sliding-window row strips (the fp32 kernel's round-3 scheme
+// on the MFMA form above): a work item is a 16-pixel column strip × THIN_SR output rows; the wave
+// keeps a ring of 4 input rows (18 pixels × 128 B, 3 LDS-DMA pieces each) and per output row DMAs
+// only the next input row, so each input row comes from L2 / HBM about once instead of twice
+// (rocprof: 2.24 GB fetched per 1.07 GB gradient with the 2-row items). Same MFMAs in the same
+// order per output (bit-identical). A/B build: MIA_THIN_OUT_RS2 keeps the 2-row items.
+constexpr int THIN_SR = 16, THIN_SLOT = 3 * 1024, THIN_RING = 4;
+
+template <typename T, int COUT>
+__global__ __launch_bounds__(256) void conv_thin_out_strip_kernel(const T* __restrict__ g,
+                                                                  const T* __restrict__ w,
+                                                                  int kpad, T* __restrict__ y,
+                                                                  int accumulate, int N, int H,
+                                                                  int W) {
+  typedef typename Vec<T>::type VT;
+  constexpr int CIN = 64, S = 18;
+  static_assert(COUT == 8, "");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, frow = lane & 15, fq = lane >> 4;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  char* const ring = smem + wid * THIN_RING * THIN_SLOT;
+  const int wave = blockIdx.x * 4 + wid, nwaves = gridDim.x * 4;
+  VT wr[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    wr[s] = ld16_or_zero<T>(w + (size_t)(frow < COUT ? frow : 0) * kpad + 32 * s + 8 * fq,
+                            frow < COUT);
+  const T* zero = (const T*)g_zero16;
+  const int gpr = W / 16, rbi = (H + THIN_SR - 1) / THIN_SR, nitems = N * rbi * gpr;
+
+  // input row sy (18 pixels from x0 − 1) of image n into ring slot `slot`: pixel px of the slot
+  // is a 128-B row, its 16-B chunk c stored at c ^ fsw(px)
+  auto issue_row = [&](int n, int sy, int x0, int slot) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int px = q * 8 + (lane >> 3);
+      const int sx = x0 + px - 1;
+      const bool ok = px < THIN_HW && sy >= 0 && sy < H && sx >= 0 && sx < W;
+      const T* src = ok ? g + ((size_t)(n * H + sy) * W + sx) * CIN + ((lane & 7) ^ fsw(px)) * 8
+                        : zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)src,
+                                       (lptr_t)(ring + slot * THIN_SLOT + q * 1024), 16, 0, 0);
+    }
+  };
+
+  for (int it = wave; it < nitems; it += nwaves) {
+    const int row = it / gpr, x0 = (it - row * gpr) * 16;
+    const int n = row / rbi, y0 = (row - n * rbi) * THIN_SR;
+    const int nr = min(THIN_SR, H - y0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the previous item's ring reads are done
+    issue_row(n, y0 - 1, x0, 0);
+    issue_row(n, y0, x0, 1);
+    issue_row(n, y0 + 1, x0, 2);
+    for (int r = 0; r < nr; ++r) {
+      // output row y0 + r reads input rows y0 + r − 1 … + 1 (slots r, r + 1, r + 2 mod 4)
+      if (r + 1 < nr) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // slot (r + 3) % 4 held row y0 + r − 2: reads done
+        issue_row(n, y0 + r + 2, x0, (r + 3) & 3);
+        asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // all but the row just issued
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const char* hb = ring + ((r + t / 3) & 3) * THIN_SLOT;
+        const int px = frow + t % 3;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const VT bf = *(const VT*)(hb + px * ROWB + (((4 * c + fq) ^ fsw(px)) << 4));
+          acc = mfma_chunk<T>(wr[2 * t + c], bf, acc);
+        }
+      }
+      const int yy = y0 + r;
+      if (fq < COUT / 4) {
+        float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+        T* yp = y + ((size_t)(n * H + yy) * W + x0 + frow) * COUT + 4 * fq;
+        if (accumulate) {
+          float yo[4];
+          load4<T>(yp, yo);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += yo[e];
+        }
+        store4<T>(yp, v);
+      }
+    }
+  }
+}
+
 // ---- 32 → 32-channel stride-1 3×3 layers (StyleGAN2 1024² StyledConvs, cm = 2) ----------------
 // K = 9 taps × 32 channels: ONE MFMA 16×16×32 K-chunk per tap. The wave holds all 9 × 2 weight
 // fragments in VGPRs (72 registers) and walks a contiguous run of 16-pixel groups (one image row
@@ -845,11 +934,19 @@ int launch_conv_thin(ConvK& k, int dtype, hipStream_t st) {
                            (const T*)a.x, (const T*)k.g[0].w, k.g[0].kpad, a.bias, a.act_out,
                            a.act_slope, (T*)a.y, a.N, a.H, a.W);
       } else {
+#ifdef MIA_THIN_OUT_RS2
         const int64_t items = (int64_t)a.N * ((a.H + THIN_RS - 1) / THIN_RS) * (a.W / 16);
         const int lds = 4 * 2 * THIN_WBUF;
         hipLaunchKernelGGL((conv_thin_out_kernel<T, 8>), dim3(grid_for(items, 16)), dim3(256),
                            lds, st, (const T*)a.x, (const T*)k.g[0].w, k.g[0].kpad, (T*)a.y,
                            a.accumulate, a.N, a.H, a.W);
+#else
+        const int64_t items = (int64_t)a.N * ((a.H + THIN_SR - 1) / THIN_SR) * (a.W / 16);
+        const int lds = 4 * THIN_RING * THIN_SLOT;  // 48 KB: 3 blocks per CU
+        hipLaunchKernelGGL((conv_thin_out_strip_kernel<T, 8>), dim3(grid_for(items, 12)),
+                           dim3(256), lds, st, (const T*)a.x, (const T*)k.g[0].w, k.g[0].kpad,
+                           (T*)a.y, a.accumulate, a.N, a.H, a.W);
+#endif
       }
       return check_launch("conv_thin");
     }

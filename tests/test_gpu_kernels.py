@@ -657,7 +657,8 @@ def test_fused_backward_front_epilogue(cuda, dtype, N, H, Cin, Cout, up):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 17, 16), (3, 16, 64), (9, 256, 256)])
+@pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 17, 16), (3, 16, 64), (4, 80, 32),
+                                   (9, 256, 256)])
 @pytest.mark.parametrize("thin", ["1", "0"])
 @pytest.mark.parametrize("e4e", [False, True])
 def test_conv_thin_vgg_input_layer(cuda, tune, dtype, N, H, W, thin, e4e):

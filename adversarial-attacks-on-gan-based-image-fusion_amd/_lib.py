@@ -140,7 +140,7 @@ SIGNATURES = {
     "mia_random_start": (c_int, [P, P, P, c_int64, c_float, c_float, c_float, P]),
     "mia_sign_project": (c_int, [P, P, P, c_int64, c_float, c_float, c_float, c_float, P]),
     "mia_ssim_workspace_size": (c_int64, [c_int, c_int, c_int]),
-    "mia_ssim": (c_int, [P, P, c_int, c_int, c_int, c_float, P, P, P]),
+    "mia_ssim2": (c_int, [P, P, c_int, c_int, c_int, c_float, P, c_int64, P, P]),
     "mia_adam_step": (c_int, [P, P, P, P, c_int64, c_float, c_float, c_float, c_float, c_int, P]),
     "mia_patch_update": (c_int, [P, P, P, P, P, c_int64, c_int64, c_float, c_float, P]),
     "mia_gemm_f32": (c_int, [c_int, c_int, c_int, c_float, P, c_int64, c_int64, P, c_int64,

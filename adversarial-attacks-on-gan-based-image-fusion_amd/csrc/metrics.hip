@@ -124,10 +124,17 @@ extern "C" int64_t mia_ssim_workspace_size(int N, int H, int W) {
   return (int64_t)N * ssim_tiles(H, W) * (int64_t)sizeof(double);
 }
 
-extern "C" int mia_ssim(const float* ref, const float* imgs, int N, int H, int W, float data_range,
-                        double* work, float* ssim_out, void* stream) {
+// The scratch grew from N doubles to one per image and tile (round 4); the old mia_ssim took no
+// size, so a caller sized for the old contract would have had its buffer overrun silently. That
+// symbol is gone: mia_ssim2 takes the scratch size and rejects one below
+// mia_ssim_workspace_size, and an old caller fails to link instead of corrupting memory.
+extern "C" int mia_ssim2(const float* ref, const float* imgs, int N, int H, int W,
+                         float data_range, double* work, int64_t work_bytes, float* ssim_out,
+                         void* stream) {
   MIA_CHECK_ARG(ref && imgs && work && ssim_out && N > 0, "bad args");
   MIA_CHECK_ARG(H >= 7 && W >= 7, "images smaller than the 7×7 window");
+  MIA_CHECK_ARG(work_bytes >= mia_ssim_workspace_size(N, H, W),
+                "work_bytes < mia_ssim_workspace_size(N, H, W)");
   MIA_CHECK_ARG(data_range > 0.f, "data_range must be > 0");
   hipStream_t st = (hipStream_t)stream;
   const float c1 = (0.01f * data_range) * (0.01f * data_range);

@@ -217,9 +217,10 @@ class E4EEncoder:
                 k0 = self.slot[r][idx[0]]
                 if [self.slot[r][i] for i in idx] != list(range(k0, k0 + len(idx))):
                     continue
-                self.src_fwd[src] = (idx, k0, r,
-                                     torch.cat([self.heads[i]["convs"][0]["w"] for i in idx]),
-                                     torch.cat([self.heads[i]["convs"][0]["b"] for i in idx]))
+                self.src_fwd[src] = (idx, k0, r)
+        # their concatenated weights / biases, built on the first forward that merges that source
+        # (at the bench batch only c3 merges: no p1 / p2 copies are held)
+        self._src_cat = {}
         # w = w0 + delta_i: the linear biases of rows i ≥ 1 include style 0's; the backward of
         # style 0 reads the sum of every row (mia_sum_slices)
         b0l = self.heads[0]["lb"]
@@ -340,10 +341,15 @@ class E4EEncoder:
         # style heads: the first conv of each head from its FPN map into the head's slot of the
         # stacked level buffer, then one batched launch per resolution level
         merged = set()
-        for src, (idx, k0, r, wcat, bcat) in self.src_fwd.items():
+        for src, (idx, k0, r) in self.src_fwd.items():
             if -(-N * r * r // 128) * (STYLE_DIM // 128) >= MERGE_BELOW_TILES:
                 continue  # enough tiles per head: one launch per head
             merged.update(idx)
+            if src not in self._src_cat:
+                self._src_cat[src] = (
+                    torch.cat([self.heads[i]["convs"][0]["w"] for i in idx]),
+                    torch.cat([self.heads[i]["convs"][0]["b"] for i in idx]))
+            wcat, bcat = self._src_cat[src]
             ops.conv2d_planes(feats[src], wcat, bcat,
                               self._level_buf(ws, "a", r, N)[k0 * N:(k0 + len(idx)) * N], (r, r),
                               planes=len(idx), act_out=ACT_PRELU, act_slope=self.slope_cat)

@@ -449,19 +449,19 @@ def mse_sum(a, b, loss, coef=1.0):
 
 
 def ssim_workspace_numel(N, H, W):
-    """fp64 elements of mia_ssim's scratch (one partial per image and output tile)."""
+    """fp64 elements of mia_ssim2's scratch (one partial per image and output tile)."""
     return int(_lib.load().mia_ssim_workspace_size(N, H, W)) // 8
 
 
 def ssim(ref, imgs, data_range, work, out):
-    """mia_ssim: ref (3,H,W), imgs (N,3,H,W) fp32 → out[n] = SSIM(gray(ref), gray(imgs[n]))."""
+    """mia_ssim2: ref (3,H,W), imgs (N,3,H,W) fp32 → out[n] = SSIM(gray(ref), gray(imgs[n]))."""
     N, _, H, W = imgs.shape
     _need(ref, (3, H, W), torch.float32, "ref")
     _need(imgs, (N, 3, H, W), torch.float32, "imgs")
     _numel_ok(work, ssim_workspace_numel(N, H, W), torch.float64, "work")
     _numel_ok(out, N, torch.float32, "out")
-    call("mia_ssim", ptr(ref), ptr(imgs), N, H, W, float(data_range), ptr(work), ptr(out),
-         stream())
+    call("mia_ssim2", ptr(ref), ptr(imgs), N, H, W, float(data_range), ptr(work),
+         work.numel() * work.element_size(), ptr(out), stream())
     return out
 
 

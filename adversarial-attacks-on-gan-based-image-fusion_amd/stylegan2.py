@@ -177,8 +177,18 @@ class SynthesisNet:
         self.styles(lat, ws)
         return self._synthesize(N, ws)
 
+    def _wmod(self, L):
+        """Does StyledConv L run on per-image modulated weights (ops.conv3x3_modw)?"""
+        r = L["res"]
+        return (not L["up"] and self.dtype != torch.float32 and WMOD_MIN_RES
+                and r >= WMOD_MIN_RES and r % 16 == 0 and L["cout"] > 64)
+
     def _synthesize(self, N, ws):
         T = self.dtype
+        # one workspace buffer for every layer's per-image weights: they are written and read
+        # inside that layer's forward only (no backward reads them), so the layers share it
+        wm_numel = max((N * L["wf"].numel() for L in self.convs if self._wmod(L)), default=0)
+        wm_buf = ws.get("g.wmod", (wm_numel,), T) if wm_numel else None
         x0 = ws.get("g.const", (N, 4, 4, self.const.shape[-1]), T)
         ops.repeat(self.const, x0, N)
         x = x0
@@ -193,9 +203,8 @@ class SynthesisNet:
                                w_up=L.get("wup"))
                 ops.upconv_blur_fwd(t, pre, L["_d"], L["noise"], L["noise_w"], L["bias"],
                                     act_out=ACT_LRELU_S2)
-            elif (not L["up"] and T != torch.float32 and WMOD_MIN_RES
-                  and r >= WMOD_MIN_RES and r % 16 == 0 and cout > 64):
-                wm = ws.get(f"g.wmod{i}", (N,) + tuple(L["wf"].shape), T)
+            elif self._wmod(L):
+                wm = wm_buf[:N * L["wf"].numel()].view((N,) + tuple(L["wf"].shape))
                 ops.conv3x3_modw(x, L["wf"], pre, wm, cout=cout, in_scale=L["_s"],
                                  out_scale=L["_d"], noise=L["noise"], noise_w=L["noise_w"],
                                  bias=L["bias"], act_out=ACT_LRELU_S2,

@@ -62,7 +62,8 @@ def arith_key(dtype):
 
 def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU (default: WORLD_SIZE under a launcher, else 1)")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=128, help="images per GPU")
@@ -95,26 +96,43 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def free_port():
-    import socket
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
-
 def spawn_workers(n, argv):
     """`--gpus N` without a launcher: start the N one-process-per-GPU ranks as ONE child
     (`python -m torch.distributed.run --nproc-per-node N … bench.py <same args>`) and return its
     exit code. This process touches no GPU (no HIP call before or after), so nothing is exec'd
-    from an initialised process; the ranks' rank 0 prints the JSON line on the shared stdout."""
+    from an initialised process; the ranks' rank 0 prints the JSON line on the shared stdout.
+    The rendezvous store binds its own free port (c10d endpoint 127.0.0.1:0: no probe-then-bind
+    race), and SIGTERM / SIGINT to this process are forwarded to the child's process group, so a
+    `timeout` around the bench also ends the launcher and its ranks."""
+    import signal
     import subprocess
+    import uuid
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           f"--nproc-per-node={n}", "--rdzv-backend=c10d", "--rdzv-endpoint=127.0.0.1:0",
+           f"--rdzv-id={uuid.uuid4().hex}", "--local-addr=127.0.0.1",
            os.path.abspath(__file__), *argv]
-    log(f"spawning {n} ranks: {' '.join(cmd[1:6])} …")
-    return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    log(f"spawning {n} ranks: {' '.join(cmd[1:5])} …")
+    child = subprocess.Popen(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"),
+                             start_new_session=True)
+
+    def forward(signum, _frame):
+        try:
+            os.killpg(child.pid, signum)
+        except ProcessLookupError:
+            pass
+
+    old = {sig: signal.signal(sig, forward) for sig in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        return child.wait()
+    finally:
+        for sig, h in old.items():
+            signal.signal(sig, h)
+        if child.poll() is None:  # the parent is leaving early (an exception): end the ranks
+            forward(signal.SIGTERM, None)
+            try:
+                child.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                forward(signal.SIGKILL, None)
 
 
 def encoder_weights(kind, size):
@@ -394,13 +412,15 @@ def headline_record(args, r, world, dist_world):
 
 def main():
     args = parse()
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
         # `python bench.py --gpus N` (no launcher): this process becomes the launcher
         sys.exit(spawn_workers(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
+    if args.gpus is None:  # under an external launcher without --gpus: one rank per GPU
+        args.gpus = world
+    elif world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (one process per GPU)")
     make_engine = build_engine
     if args.engine_factory:

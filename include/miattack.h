@@ -494,11 +494,12 @@ int mia_memset(void* dst, int value, int64_t bytes, void* stream);
  * SSIM of ref (3,H,W) against each of imgs (N,3,H,W), fp32 NCHW, the way cal_SSMI calls
  * skimage.metrics.structural_similarity on rgb2gray images (7×7 uniform window, sample
  * covariance, K1 0.01, K2 0.03, border of 3 cropped). work: device scratch of
- * mia_ssim_workspace_size(N, H, W) bytes (one fp64 partial per image and 32×32 output tile,
- * summed in tile order: deterministic, batch-independent). */
+ * work_bytes ≥ mia_ssim_workspace_size(N, H, W) bytes (one fp64 partial per image and 32×32
+ * output tile, summed in tile order: deterministic, batch-independent); a smaller work_bytes is
+ * MIA_ERR_ARG. (Replaces round 3's size-less mia_ssim, whose scratch contract changed.) */
 int64_t mia_ssim_workspace_size(int N, int H, int W);
-int mia_ssim(const float* ref, const float* imgs, int N, int H, int W, float data_range,
-             double* work, float* ssim_out, void* stream);
+int mia_ssim2(const float* ref, const float* imgs, int N, int H, int W, float data_range,
+              double* work, int64_t work_bytes, float* ssim_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -67,29 +67,53 @@ def test_bench_multi_rank_leg_gloo_world2():
         assert c["algorithmic_gflop_per_image_step"] == pytest.approx((2 * 10 + 4 * 1 + 6) / 1e9)
 
 
-def test_bench_self_spawns_ranks_gloo_world2():
-    """`python bench.py --gpus 2` with no launcher starts the two ranks itself (one
-    torch.distributed.run child; the parent touches no GPU) and exactly ONE JSON line reaches
-    stdout, from rank 0, with the whole-job fields of a world-2 run — the command form the
-    driver's N>1 bench may use."""
+def _clean_env():
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)
     env["PYTHONPATH"] = os.pathsep.join([os.path.join(ROOT, "tests"), ROOT,
                                          env.get("PYTHONPATH", "")])
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
-           "--engine-factory", "bench_stub:make_engine", "--steps", "2", "--warmup", "1",
+    return env
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_self_spawns_ranks_gloo(world):
+    """`python bench.py --gpus N` with no launcher starts the N ranks itself (one
+    torch.distributed.run child; the parent touches no GPU) and exactly ONE JSON line reaches
+    stdout, from rank 0, with the whole-job fields of a world-N run — the command form the
+    driver's N>1 bench may use (verdict r04 item 7: world 4 as well as 2)."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--device",
+           "cpu", "--engine-factory", "bench_stub:make_engine", "--steps", "2", "--warmup", "1",
            "--batch", "3", "--size", "16", "--no-roofline", "--no-cpu-baseline"]
-    p = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
-                       timeout=240, cwd=ROOT)
+    p = subprocess.run(cmd, env=_clean_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True, timeout=240, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
+    # exactly one JSON line (gloo's own C++ connection notices also go to stdout)
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout
     out = json.loads(lines[0])
     c = out["config"]
-    assert out["n_gpus"] == 2 and c["dist_world_size"] == 2 and c["parallelism"] == "dp2"
-    assert c["global_batch"] == 6 and c["gathered_output_ok"] is True
-    assert out["value"] == pytest.approx(6 * 2 / (out["ms_per_step"] * 2 / 1e3))
+    assert out["n_gpus"] == world and c["dist_world_size"] == world
+    assert c["parallelism"] == f"dp{world}"
+    assert c["global_batch"] == 3 * world and c["gathered_output_ok"] is True
+    assert out["value"] == pytest.approx(3 * world * 2 / (out["ms_per_step"] * 2 / 1e3))
+
+
+def test_bench_under_torchrun_without_gpus_flag():
+    """An external `torchrun --nproc-per-node 2 bench.py` without --gpus takes the world size
+    from the launcher (advisor r04: the stricter check had rejected it)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--rdzv-backend=c10d", "--rdzv-endpoint=127.0.0.1:0", "--local-addr=127.0.0.1",
+           os.path.join(ROOT, "bench.py"), "--device", "cpu",
+           "--engine-factory", "bench_stub:make_engine", "--steps", "1", "--warmup", "1",
+           "--batch", "2", "--size", "16", "--no-roofline", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, env=_clean_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True, timeout=240, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["dist_world_size"] == 2
 
 
 def test_bench_rejects_world_mismatch():

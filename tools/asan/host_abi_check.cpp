@@ -90,8 +90,11 @@ int main() {
                                     nullptr), "modw Cin");
   expect_error(mia_modulate_weights(nullptr, dummy, nullptr, dummy, 2, 64, 64,
                                     mia_conv_kpad(64, MIA_F16), MIA_F16, nullptr), "modw null");
-  expect_error(mia_ssim(dummy, dummy, 1, 5, 5, 2.f, nullptr, dummy, nullptr), "ssim small");
-  expect_error(mia_ssim(dummy, dummy, 1, 64, 64, 0.f, (double*)dummy, dummy, nullptr), "ssim dr");
+  expect_error(mia_ssim2(dummy, dummy, 1, 5, 5, 2.f, nullptr, 0, dummy, nullptr), "ssim small");
+  expect_error(mia_ssim2(dummy, dummy, 1, 64, 64, 0.f, (double*)dummy, 1 << 20, dummy, nullptr),
+               "ssim dr");
+  expect_error(mia_ssim2(dummy, dummy, 4, 64, 64, 2.f, (double*)dummy, 8 * 4, dummy, nullptr),
+               "ssim work size");  // the round-3 contract (N doubles) is rejected
   expect_error(mia_gemm_f32_grouped(nullptr, 0, nullptr), "gemm groups");
   expect_error(mia_reserve_reduction_scratch(-1, nullptr), "scratch negative");
   EXPECT(mia_reserve_reduction_scratch(0, nullptr) == MIA_OK, "scratch zero");

@@ -612,6 +612,8 @@ int launch_upconv_halo(const void* x, const void* w_up, const void* w_up_split, 
 // 64 → 64-channel stride-1 layers, weights resident in VGPRs, persistent (conv_wres.hip)
 bool conv_wres_eligible(const ConvK& k, int dtype);
 int launch_conv_wres(ConvK& k, int dtype, hipStream_t st);
+bool conv_wres128_eligible(const ConvK& k, int dtype);
+int launch_conv_wres128(ConvK& k, int dtype, hipStream_t st);
 bool conv_wres32_eligible(const ConvK& k, int dtype);
 int launch_conv_wres32(ConvK& k, int dtype, hipStream_t st);
 // thin-channel layers: VGG conv1_1 forward and its input gradient (conv_thin.hip)

@@ -673,6 +673,7 @@ extern "C" int mia_conv3x3_wmod(const mia_conv_args* args, int64_t w_nstride, in
                 "bad conv args");
   MIA_CHECK_ARG(a.Kpad == mia_conv_kpad(a.Cin, dtype), "Kpad must be mia_conv_kpad()");
   MIA_CHECK_ARG((int64_t)a.N * a.H * a.W * a.Cin < (1LL << 31), "input too large");
+  if (conv_wres128_eligible(k, dtype)) return launch_conv_wres128(k, dtype, (hipStream_t)stream);
   MIA_CHECK_ARG(conv_halo_eligible(k, dtype), "per-image weights need the halo kernel's shapes "
                                               "(H, W multiples of 16)");
   return launch_conv_halo(k, dtype, (hipStream_t)stream);

@@ -769,7 +769,7 @@ static int launch_x6_spec(ConvK& k, hipStream_t st) {
       case BIAS: return launch_x6_<BN_, PRO, BIAS>(k, st);            // e4e conv2 (SE body)
       case BIAS | RELU: return launch_x6_<BN_, PRO, BIAS | RELU>(k, st);  // VGG forward
       case PRELU: return launch_x6_<BN_, PRO, PRELU>(k, st);          // e4e conv1
-      // per-pixel aux operands (the tap pair only under MIA_X6_64AUX=1)
+      // per-pixel aux operands (the tap pair: MIA_X6_64S=0, A/B and bitwise tests only)
       case MASK: return launch_x6_<BN_, PRO, MASK>(k, st);
       case TAP: return launch_x6_<BN_, PRO, TAP>(k, st);
       case ACC: return launch_x6_<BN_, PRO, ACC>(k, st);
@@ -794,9 +794,6 @@ static int launch_x6_spec(ConvK& k, hipStream_t st) {
   return launch_x6_<BN_, PRO, -1>(k, st);
 }
 
-// MIA_X6_64AUX=1: the 64-column tile also for launches with the tap pair (A/B)
-static bool x6_64_aux() { return tune(T_X6_64AUX) != 0; }
-
 // Eligible: fp32 with pre-split weights (mia_conv_args.w_split / mia_conv_group.w_split), one
 // group, stride 1, 3×3 pad 1, identity placement, 16-divisible maps, Cin % 32 == 0, Cout ≥ 64.
 bool conv_halo_x6_eligible(const ConvK& k, int dtype) {
@@ -812,10 +809,9 @@ bool conv_halo_x6_eligible(const ConvK& k, int dtype) {
          G.kw == 3 && G.pad_y == 1 && G.pad_x == 1 && G.ho == a.H && G.wo == a.W && G.ay == 1 &&
          G.ax == 1 && G.by == 0 && G.bx == 0 && !a.shuffle_out && a.H % 16 == 0 &&
          a.W % 16 == 0 && a.Cin % 32 == 0 && k.HT == a.H && k.WT == a.W &&
-         // 64 channels: the 64-column tile, except with the tap pair (VGG gradient at a tap
-         // layer: 1–2 % slower than the generic tile); with the specialised register epilogues
-         // the mask / accumulate launches run 12–20 % faster on it (137 → 154 / 164 TFLOP/s)
-         (a.Cout > 64 || (a.Cout == 64 && (!a.tap_a || x6_64_aux() || tune(T_X6_64S) != 0)));
+         // 64 channels: the two-blocks-per-CU x6s tile (T_X6_64S = 1, default; with the tap pair
+         // too), or the 8-wave 64-column tile (0, A/B)
+         a.Cout >= 64;
 }
 
 #ifdef MIA_STAMPS

@@ -382,7 +382,6 @@ static int launch_tile(ConvK& k, hipStream_t st) {
 
 typedef Tile<2, 2, 4, 2, 2> Tile128x64;
 typedef Tile<2, 2, 4, 4, 2> Tile128x128;
-typedef Tile<4, 2, 4, 4, 3> Tile256x128;
 typedef Tile<2, 2, 2, 2, 2> Tile64x64;
 
 // Register epilogue on the 128x128 tile: 2-byte types, one group, identity output placement,
@@ -414,10 +413,9 @@ template <typename T, bool PRO, bool SMALLC>
 static int launch_bn(ConvK& k, hipStream_t st) {
   int64_t m = 0;
   for (int g = 0; g < k.ng; ++g) m += k.g[g].m;
-  // Tuning override T_CONV_TILE (tests / tuning): 2 = 256x128 3-stage tile where the launch
-  // has ≥ 2 waves of them. Default 128x128: measured faster on every StyleGAN2/VGG shape of the
-  // 256² attack step (2 blocks/CU hide each other's DMA waits better than 1 deeper ring).
-  const int force = tune(T_CONV_TILE);
+  // (a 256x128 3-stage tile measured slower than 128x128 on every StyleGAN2 / VGG shape of the
+  // 256² attack step — 2 blocks per CU hide each other's DMA waits better than 1 deeper ring —
+  // and was removed in round 5)
   if (k.a.Cout <= 64) {
     // the 64-column tile with the specialised register epilogue for the same feature masks as
     // the 128-column tile below (the 512² StyledConv input gradients and the up-conv adjoints of
@@ -469,8 +467,6 @@ static int launch_bn(ConvK& k, hipStream_t st) {
       default: break;
     }
   }
-  const int64_t big_blocks = (m / 256) * ((k.a.Cout + 127) / 128);
-  if (force == 2 && big_blocks >= 512) return launch_tile<T, Tile256x128, PRO, SMALLC>(k, st);
   return launch_tile<T, Tile128x128, PRO, SMALLC>(k, st);
 }
 

@@ -1,0 +1,287 @@
+// Weights-resident persistent 3×3 conv with 128 output channels (NHWC, fp16 / bf16, CDNA4):
+// the StyledConv forward of the 256² generator block on per-image modulated + demodulated weights
+// (rosinality ModulatedConv2d's weight path, code/attack/attack_main2.py:619-621 decoder call;
+// channel_multiplier 2: 128 → 128 channels at 256², K = 9·128 = 1 152).
+//
+// Why: the halo tile (conv_halo.hip, 8×16 patch × 128 channels, one block per patch) spends a
+// fifth of every block in its prologue (the first halo from HBM) and its epilogue, and streams
+// every K-step's weights through an LDS ring with a block barrier per step; at K = 1 152 those
+// fixed costs are not amortised (profiles/r04_fp16_halo_phases_wmod.txt: prologue 8.4 k +
+// epilogue 4.9 k of ≈ 41 k cycles per block, 837–866 TFLOP/s). Here:
+//   * each of the 8 waves (two per SIMD) holds the B fragment of ITS 16 output channels over the
+//     whole K in VGPRs: 9 taps × (Cin/32) K-chunks × 4 VGPRs = 144 at Cin = 128, loaded once per
+//     image (per-image weights: a block's run covers about half an image, so one reload per run)
+//     — no weight ring, no per-step barrier. Two waves per SIMD: one wave's epilogue, DMA issue
+//     and LDS waits run under its partner's MFMAs (the first form, 4 waves × 32 channels with 288
+//     weight VGPRs and one wave per SIMD, measured 831 TFLOP/s against the halo tile's 868);
+//   * the block is persistent over a contiguous run of 8×16-pixel patches; the (8+2)×(16+2)
+//     halo of the next patch is DMA'd into the other LDS buffer a whole patch ahead (one barrier
+//     per patch), so no patch waits for HBM;
+//   * every wave computes all 128 patch pixels × its 16 channels (acc 8 fragments). The A
+//     fragment of halo row q, column shift dx and K-chunk s feeds the three taps (dy = 0, 1, 2)
+//     of output rows q − dy: 120 ds_read_b128 per wave per patch for 288 MFMAs, read two ahead;
+//   * the epilogue (noise, bias, leaky ReLU · √2) runs in registers; the patch's noise rows are
+//     DMA'd into LDS with the halo and the bias sits in VGPRs, so it waits on nothing.
+// Halo LDS image (2-byte types, PB = 2·Cin bytes per pixel): halo rows padded to HS = 20 pixels
+// (columns 18, 19 never read), pixels in groups of 4 (GB = 4·PB bytes): pixel hr, 32-channel
+// sub-plane s, 16-B chunk c at (hr / 4)·GB + s·256 + (hr % 4)·64 + (c ^ sw(hr % 20))·16. Row q
+// starts at group 5q, so a fragment address is a lane constant per column shift dx plus the
+// immediate q·5·GB + s·256; sw(v) = (v >> 1) & 3 keeps every ds_read_b128 lane group on 16
+// distinct 16-B bank slots for any dx (checked exhaustively, tests/test_host.py).
+#include "conv_common.h"
+#include "halo_epilogue.h"
+
+namespace mia {
+
+template <int CIN>
+struct Wres128Tile {
+  static constexpr int FM = 8, NW = 8, NT = 512, PH = 8, PW = 16, BN = 16 * NW;  // 128
+  static constexpr int HS = 20, HROWS = (PH + 2) * HS;  // 200 halo pixels
+  static constexpr int PB = 2 * CIN, GB = 4 * PB;       // bytes per pixel / per 4-pixel group
+  static constexpr int NS = CIN / 32;                   // K-chunks (32-channel sub-planes) per tap
+  static constexpr int HBUF = HROWS * PB;               // 51 200 B at Cin = 128
+  static constexpr int NPIECE = HBUF / 1024;            // 1-KB DMA pieces per halo (50)
+  static constexpr int P_INS = (NPIECE + NW - 1) / NW;  // pieces per wave (≤ 7)
+  static constexpr int NZB = 1024;                      // per wave: the patch's noise rows
+  static constexpr int LDS = 2 * HBUF + NW * NZB;
+  static_assert(CIN == 128, "one DMA piece = one 4-pixel group (GB = 1 KB)");
+  static_assert(HBUF % 1024 == 0 && GB == 1024, "halo layout");
+};
+
+__device__ __forceinline__ int sw128(int v) { return (v >> 1) & 3; }
+
+// EPI: NOISE | BIAS | LRELU (the StyledConv forward on modulated + demodulated weights).
+// k.wn > 0: per-image weight matrices wn elements apart; 0: one shared matrix.
+template <typename T, int CIN, int EPI>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wres128_kernel(const ConvK k) {
+  typedef Wres128Tile<CIN> TL;
+  typedef typename Vec<T>::type VT;
+  constexpr int FM = TL::FM, NW = TL::NW, NS = TL::NS, HBUF = TL::HBUF, NPIECE = TL::NPIECE;
+  constexpr int GB = TL::GB, P_INS = TL::P_INS;
+  static_assert(EPI == (epi::NOISE | epi::BIAS | epi::LRELU), "the StyledConv forward epilogue");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const mia_conv_args& p = k.a;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int frow = lane & 15, fq = lane >> 4;
+  const int H = p.H, W = p.W;
+  const int ptx = W / TL::PW, pty = H / TL::PH;
+  const int ntiles = p.N * ptx * pty;
+  const int per = (ntiles + gridDim.x - 1) / gridDim.x;
+  const int t0 = blockIdx.x * per, t1 = min(t0 + per, ntiles);
+  if (t0 >= t1) return;
+  const T* __restrict__ X = (const T*)p.x;
+  const T* __restrict__ W0 = (const T*)k.g[0].w;
+  const int kpad = k.g[0].kpad;
+  T* __restrict__ Y = (T*)p.y;
+  const int cw0 = 16 * wid;  // this wave's first output channel
+  // the zero page for padding lanes, loaded once (not rematerialised per DMA piece)
+  const T* zero = (const T*)g_zero16;
+  asm volatile("" : "+s"(zero));
+
+  auto tile_pos = [&](int tile, int& n, int& y0, int& x0) {
+    x0 = (tile % ptx) * TL::PW;
+    y0 = ((tile / ptx) % pty) * TL::PH;
+    n = tile / (ptx * pty);
+  };
+
+  // B fragments of this wave's 16 channels: (tap t, K-chunk s) = input channels s·32 + fq·8 …
+  // +7 of tap t for output channel cw0 + frow
+  VT wreg[9][NS];
+  auto load_w = [&](int n) {
+    const T* Wn = W0 + (size_t)n * k.wn + (size_t)(cw0 + frow) * kpad + fq * 8;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) wreg[t][s] = *(const VT*)(Wn + t * CIN + s * 32);
+  };
+
+  // the lane's part of a DMA piece (one 4-pixel group of a halo row): sub-plane s, pixel pp of
+  // the group, stored chunk cs (LDS byte 16·lane of the piece)
+  const int ls = lane >> 4, lpp = (lane >> 2) & 3, lcs = lane & 3;
+  // wave wid DMAs halo pieces wid + NW·j; piece pc = halo row pc / 5, pixels 4·(pc % 5) …
+  auto issue_halo = [&](int tile, int buf) {
+    int n, y0, x0;
+    tile_pos(tile, n, y0, x0);
+#pragma unroll
+    for (int j = 0; j < P_INS; ++j) {
+      const int pc = wid + NW * j;  // wave-uniform
+      if (pc < NPIECE) {
+        const int hy = pc / 5, c5 = pc - 5 * hy;
+        const int y = y0 + hy - 1;
+        const int hx = 4 * c5 + lpp;
+        const int x = x0 + hx - 1;
+        const bool ok = y >= 0 && y < H && hx < TL::PW + 2 && x >= 0 && x < W;
+        const int yc = ok ? y : 0, xc = ok ? x : 0;
+        const T* a = X + ((size_t)(n * H + yc) * W + xc) * CIN + ls * 32 +
+                     ((lcs ^ sw128(hx)) << 3);
+        __builtin_amdgcn_global_load_lds((gptr_t)(ok ? a : zero),
+                                         (lptr_t)(smem + buf * HBUF + pc * 1024), 16, 0, 0);
+      }
+    }
+  };
+  // this wave's copy of the patch's noise rows (8 rows × 16 floats; lanes ≥ 32 read zeros)
+  char* const nzl = smem + 2 * HBUF + wid * TL::NZB;
+  auto issue_noise = [&](int y0, int x0) {
+    const float* src = lane < 32 ? p.noise + (size_t)(y0 + (lane >> 2)) * W + x0 + 4 * (lane & 3)
+                                 : (const float*)zero;
+    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)nzl, 16, 0, 0);
+  };
+
+  // the bias of this lane's 4 channels (lane row r: channels cw0 + 4r …)
+  const f32x4 bia = *(const f32x4*)(p.bias + cw0 + ((lane >> 4) << 2));
+
+  // lane-constant A-fragment offsets per column shift dx (pixel column v = frow + dx)
+  int offa[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) {
+    const int v = frow + dx;
+    int o = (v >> 2) * GB + (v & 3) * 64 + ((fq ^ sw128(v)) << 4);
+    asm volatile("" : "+v"(o));
+    offa[dx] = o;
+  }
+
+  int wimg = -1;
+  {
+    int n, y0, x0;
+    tile_pos(t0, n, y0, x0);
+    load_w(n);
+    wimg = n;
+  }
+  issue_halo(t0, 0);
+  // vmcnt(0) as the builtin (the compiler's wait insertion sees it and adds none later for the
+  // weight registers; an inline-asm wait is opaque to it)
+  __builtin_amdgcn_s_waitcnt(0x0f70);
+  int buf = 0;
+  for (int tile = t0; tile < t1; ++tile) {
+    // every wave finished the previous patch (buffer buf^1 and its noise slot are free) and
+    // drained its DMA pieces of this patch (buffer buf is complete). LDS-only hand-off: no
+    // vector-memory wait, so the previous epilogue's stores stay in flight
+    lds_handoff();
+    int n, y0, x0;
+    tile_pos(tile, n, y0, x0);
+    issue_noise(y0, x0);
+    if (tile + 1 < t1) issue_halo(tile + 1, buf ^ 1);
+    const char* hb = smem + buf * HBUF;
+    f32x4 acc[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // the 120 fragment reads in (dx, s, q) order, each feeding the taps dy = 0, 1, 2 of output
+    // row q − dy; the next read is issued before the current fragment's MFMAs
+    const char* hd[3] = {hb + offa[0], hb + offa[1], hb + offa[2]};
+    VT cur = *(const VT*)hd[0];
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int q = 0; q < FM + 2; ++q) {
+          int q2 = q + 1, s2 = s, dx2 = dx;
+          if (q2 == FM + 2) { q2 = 0; ++s2; }
+          if (s2 == NS) { s2 = 0; ++dx2; }
+          VT nxt = cur;
+          if (dx2 < 3) nxt = *(const VT*)(hd[dx2] + q2 * 5 * GB + s2 * 256);
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy) {
+            const int i = q - dy;
+            if (i < 0 || i >= FM) continue;
+            acc[i] = mfma_chunk<T>(wreg[dy * 3 + dx][s], cur, acc[i]);  // D[channel][pixel]
+          }
+          cur = nxt;
+        }
+    // the next patch's halo and this patch's noise were issued a whole patch ago: drain them
+    // before the epilogue's stores (vmcnt retires in order)
+    __builtin_amdgcn_s_waitcnt(0x0f70);
+    const int px = lane & 15, lrow = lane >> 4;
+    const float* nz = (const float*)nzl;
+#pragma unroll
+    for (int i = 0; i < FM; i += 2) {
+      // rows i, i+1: after the swap lane row r holds channels 8·(r >> 1) … +7 of row i + (r & 1)
+      float vo[2][4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float z = p.noise_w * nz[(i + u) * 16 + px];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = acc[i + u][e];
+          v += z;
+          v += bia[e];
+          vo[u][e] = lrelu_s2(v);
+        }
+      }
+      typedef T t2 __attribute__((ext_vector_type(2)));
+      unsigned a[2], b[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const t2 ta = {(T)vo[0][2 * h], (T)vo[0][2 * h + 1]};
+        const t2 tb = {(T)vo[1][2 * h], (T)vo[1][2 * h + 1]};
+        const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, ta),
+                                                        __builtin_bit_cast(unsigned, tb), false,
+                                                        false);
+        a[h] = r[0];
+        b[h] = r[1];
+      }
+      const int m = (n * H + y0 + i + (lrow & 1)) * W + x0 + px;
+      const int c = cw0 + 8 * (lrow >> 1);
+      *(uint4*)(Y + (size_t)m * k.ystride + c) = make_uint4(a[0], a[1], b[0], b[1]);
+    }
+    if (tile + 1 < t1) {
+      int n1, y1, x1;
+      tile_pos(tile + 1, n1, y1, x1);
+      if (n1 != wimg) {  // block-uniform: the run reaches the next image's weights. Loaded and
+        load_w(n1);      // waited for here, so no wait for them (which would also wait for the
+        wimg = n1;       // next halo, in flight behind them) lands in the next patch's MFMAs
+        __builtin_amdgcn_s_waitcnt(0x0f70);
+      }
+    }
+    buf ^= 1;
+  }
+}
+
+template <typename T, int CIN, int EPI>
+static int launch_wres128_(ConvK& k, hipStream_t st) {
+  typedef Wres128Tile<CIN> TL;
+  auto fn = conv_wres128_kernel<T, CIN, EPI>;
+  static int ncu = 0;
+  if (!ncu) {
+    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            TL::LDS) != hipSuccess)
+      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      ncu = 256;
+  }
+  const int ntiles = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW);
+  const int per = (ntiles + ncu - 1) / ncu;
+  const int grid = (ntiles + per - 1) / per;  // every block has a non-empty run
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(TL::NT), TL::LDS, st, k);
+  return check_launch("conv_wres128");
+}
+
+// Eligible: 2-byte type, Cin 128 → Cout 128, one group, stride 1, 3×3 pad 1, identity placement,
+// H % 8 == 0, W % 16 == 0, dense output rows, the StyledConv forward epilogue (noise, bias,
+// leaky ReLU, no demod: per-image modulated + demodulated weights). T_CONV_WRES128 = 0 disables.
+bool conv_wres128_eligible(const ConvK& k, int dtype) {
+  if (tune(T_CONV_WRES128) == 0) return false;
+  const mia_conv_args& a = k.a;
+  const ConvGroup& G = k.g[0];
+  using namespace epi;
+  return dtype != MIA_F32 && k.ng == 1 && k.stride == 1 && G.kh == 3 && G.kw == 3 &&
+         G.pad_y == 1 && G.pad_x == 1 && G.ho == a.H && G.wo == a.W && G.ay == 1 && G.ax == 1 &&
+         G.by == 0 && G.bx == 0 && !a.shuffle_out && a.H % 8 == 0 && a.W % 16 == 0 &&
+         a.Cin == 128 && a.Cout == 128 && k.HT == a.H && k.WT == a.W && !a.in_scale &&
+         a.act_in == MIA_ACT_NONE && G.kpad >= 9 * 128 && a.y && a.noise && a.bias &&
+         epi_mask(k) == (NOISE | BIAS | LRELU);
+}
+
+int launch_conv_wres128(ConvK& k, int dtype, hipStream_t st) {
+  using namespace epi;
+  MIA_DISPATCH_DTYPE(dtype, T, {
+    if constexpr (sizeof(T) == 2) return launch_wres128_<T, 128, NOISE | BIAS | LRELU>(k, st);
+  });
+  return set_error("conv_wres128: 2-byte dtypes only");
+}
+
+}  // namespace mia

@@ -81,11 +81,9 @@ enum TuneKey {
   T_HALO_EPI,        // halo tiles' epilogue: 0 LDS-staged, 1 specialised (default), 2 runtime
   T_X6_UNR,          // x6 halo kernel: 0 rolled tap loop, 1 unrolled taps, 2 (default) + two
                      // taps per K-step on the 64-column tile
-  T_X6_64AUX,        // 1: the 64-column x6 tile for the tap-pair launches too
   T_CONV_THIN,       // 0: no thin-channel input-layer kernels
   T_CONV_THIN32,     // 0: no 32-channel thin kernel
   T_CONV_WRES,       // 0: no weights-resident 64 → 64 kernel
-  T_CONV_TILE,       // 2: the 256×128 generic tile where it has ≥ 2 waves of blocks
   T_CONV_REGEPI,     // 0: no register epilogue on the generic 128×128 tile
   T_CONV_SMALLTILE,  // 64×64 generic tiles below this many 128×128 tiles (2-byte types)
   T_S2DG_X6,         // 0: the stride-2 input gradients on the on-the-fly split up-conv kernel
@@ -102,6 +100,8 @@ enum TuneKey {
                      // HaloX6S, also the VGG tap-pair gradient), 0 the 8-wave 64-column tile
   T_UPCONV_X6S,      // fp32 split-once stride-2 input gradient with Cin ≤ 512: 1 (default) the
                      // 8 × 16-patch two-blocks-per-CU form (conv_upconv.hip DgX6S), 0 the 8-wave one
+  T_CONV_WRES128,    // 0: the 2-byte 128 → 128 StyledConv forward on per-image weights on the
+                     // halo tile instead of the weights-resident kernel (conv_wres128.hip)
   T_NKEYS
 };
 int tune(TuneKey key);

@@ -30,12 +30,12 @@ struct TuneDef {
 };
 TuneDef g_tune[T_NKEYS] = {
     {"MIA_CONV_HALO", 1}, {"MIA_CONV_X6", 1},       {"MIA_HALO_EPI", 1},    {"MIA_X6_UNR", 2},
-    {"MIA_X6_64AUX", 0},  {"MIA_CONV_THIN", 1},     {"MIA_CONV_THIN32", 1}, {"MIA_CONV_WRES", 1},
-    {"MIA_CONV_TILE", 0}, {"MIA_CONV_REGEPI", 1},   {"MIA_CONV_SMALLTILE", 512},
+    {"MIA_CONV_THIN", 1}, {"MIA_CONV_THIN32", 1},   {"MIA_CONV_WRES", 1},
+    {"MIA_CONV_REGEPI", 1},   {"MIA_CONV_SMALLTILE", 512},
     {"MIA_S2DG_X6", 1},   {"MIA_S2DG_HALO", 1},     {"MIA_UPCONV_X6", 1},   {"MIA_UPCONV_HALO", 1},
     {"MIA_EPI_PRERED", 1},    {"MIA_CONV_WRES32", 1},
     {"MIA_HALO_C64", 1},  {"MIA_THIN_F32", 3},      {"MIA_X6_64S", 1},
-    {"MIA_UPCONV_X6S", 1}};
+    {"MIA_UPCONV_X6S", 1}, {"MIA_CONV_WRES128", 1}};
 std::once_flag g_tune_once;
 void tune_init() {
   for (auto& d : g_tune) {

@@ -217,6 +217,59 @@ def test_modconv_fwd_per_image_weights(cuda, dtype, N, cin, cout, R):
                          **dict(kw, noise=None))
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,R,W", [(20, 64, 64), (3, 256, 256), (5, 40, 48)])
+def test_wres128_modconv_fwd(cuda, tune, dtype, N, R, W):
+    """The weights-resident 128 → 128 StyledConv forward (conv_wres128.hip, the 256² layer of the
+    fp16 / bf16 synthesis) on per-image weights: persistent runs that cross image boundaries
+    (weights reloaded mid-run), 8×16 patches (R = 40: H % 16 ≠ 0), against (a) a torch fp32 GPU
+    conv of the same rounded operands and per-image weights + the same epilogue, and (b) the halo
+    tile (MIA_CONV_WRES128=0) on the same weights: both accumulate in fp32 in different orders,
+    so the outputs agree to the output rounding."""
+    cin = cout = 128
+    g = torch.Generator().manual_seed(N * 31 + R)
+    x = torch.randn(N, R, W, cin, generator=g).to(dtype)
+    w = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(9 * cin)
+    s = (torch.rand(N, cin, generator=g) + 0.5)
+    noise = torch.randn(R * W, generator=g)
+    bias = 0.1 * torch.randn(cout, generator=g)
+    wf = layouts.fwd_matrix(w.double(), dtype).to(cuda)
+    wsq = (w.double() ** 2).sum((2, 3)).float().to(cuda)
+    s_d = s.to(cuda)
+    demod = torch.empty(N, cout, device=cuda)
+    ops.style_demod(s_d, wsq, demod)
+    xd = x.to(cuda)
+    kw = dict(cout=cout, in_scale=s_d, out_scale=demod, noise=noise.to(cuda), noise_w=0.3,
+              bias=bias.to(cuda), act_out=ops.ACT_LRELU_S2)
+    wm = torch.empty((N,) + tuple(wf.shape), dtype=dtype, device=cuda)
+    y = torch.empty(N, R, W, cout, dtype=dtype, device=cuda)
+    ops.conv3x3_modw(xd, wf, y, wm, **kw)
+    tune("MIA_CONV_WRES128", 0)
+    y_halo = torch.empty_like(y)
+    wm2 = torch.empty_like(wm)
+    if R % 16 == 0:
+        ops.conv3x3_modw(xd, wf, y_halo, wm2, **kw)
+    torch.cuda.synchronize()
+    # fp32 reference on the device's own per-image weights (grouped conv: one group per image)
+    K = 9 * cin
+    wr = wm[:, :, :K].float().view(N, cout, 3, 3, cin).permute(0, 1, 4, 2, 3)
+    ref = F.conv2d(xd.float().permute(0, 3, 1, 2).reshape(1, N * cin, R, W),
+                   wr.reshape(N * cout, cin, 3, 3), padding=1, groups=N).view(N, cout, R, W)
+    ref = F.leaky_relu(ref + 0.3 * noise.to(cuda).view(1, 1, R, W) + bias.to(cuda).view(1, -1, 1, 1),
+                       0.2) * math.sqrt(2)
+    e_ref = rel_err(nchw(y), ref)
+    ulp = 2.0 ** (-10 if dtype == torch.float16 else -7)
+    print(f"wres128 {dtype} {N}x{R}x{W}: rel err vs fp32 {e_ref:.2e}")
+    assert e_ref < 2 * ulp
+    if R % 16 == 0:
+        assert torch.equal(wm, wm2)
+        d = (y.float() - y_halo.float()).abs()
+        lim = y_halo.float().abs() * (2 * ulp) + 2 * ulp * float(y_halo.float().abs().max()) * 1e-3
+        print(f"wres128 vs halo: max |diff| {float(d.max()):.3e}, "
+              f"{int((y != y_halo).sum())} of {y.numel()} differ")
+        assert (d <= lim + 1e-6).all()
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("up", [False, True])
 @pytest.mark.parametrize("store_act", [False, True])
@@ -560,11 +613,8 @@ def test_upconv_subpixel_fwd_bwd(cuda, dtype, N, cin, cout, R, store_act):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("kind", ["plain", "modconv", "dgrad_sdot"])
-@pytest.mark.parametrize("tile", ["1", "2"])
-def test_conv_large_m_tiles(cuda, dtype, kind, tile, tune):
-    """Large-M launches on the default 128×128 tile and on the 256×128 3-stage DMA-ring tile
-    (MIA_CONV_TILE=2), checked against torch's conv."""
-    tune("MIA_CONV_TILE", tile)
+def test_conv_large_m_tiles(cuda, dtype, kind):
+    """Large-M launches on the 128×128 tile, checked against torch's conv."""
     g = torch.Generator().manual_seed(17)
     N, H, Cin, Cout = 8, 128, 64, 128
     x = torch.randn(N, Cin, H, H, generator=g)
@@ -1238,7 +1288,6 @@ def test_x6_halo_variants_bitwise(cuda, tune, C, H, W, mode):
 
     if mode == "tap_mask":
         ref = (conv + 0.37 * (a.double() - t.double())) * (a.double() > 0)
-    tune("MIA_X6_64AUX", "1")  # the 64-column tile for the tap launch too
     y_def = run()  # Cout 64: the two-blocks-per-CU tile (MIA_X6_64S=1)
     tune("MIA_X6_64S", "0")  # the 8-wave 64-column tile, two taps per K-step (MIA_X6_UNR=2)
     assert torch.equal(run(), y_def)

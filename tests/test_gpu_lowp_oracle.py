@@ -1,0 +1,93 @@
+"""The reduced-precision attack gradients against the fp64 ORACLE (verdict r04 item 2), not only
+against the fp32 device path: the full pixel gradient ∇_x L of the objective
+(code/attack/interpolation.py:786-818, the PGD rule's input :62-96) of the bench's networks (e4e +
+StyleGAN2 + VGG16, seeded random init) at
+
+* bf16, 1024² (BASELINE cfg3's precision and size),
+* fp16, 256² (cfg4's per-GPU share) and fp16, 1024² (cfg5's),
+
+each compared with autograd through the fp64 oracle forced onto every branch the device pass took
+(gpu_helpers.forced_all: PReLU / LeakyReLU / SE ReLU / VGG ReLU and pool windows). The forced
+oracle isolates the arithmetic error of the reduced-precision kernels from branch decisions; the
+audit bounds the forced disagreements with the oracle's own decisions (near-ties only, and rare).
+Tolerances (stated per case, measured values printed): the relative L2 norm of the difference and
+the sign agreement on the pixels whose oracle gradient exceeds 1 % of its max.
+
+Plus BASELINE cfg1 (FGSM ε = 8/255 on a 256² pair, the reference's `fgsm` through `attack`): the
+device output equals the oracle's FGSM step (attack_ref.pgd, steps = 1) bit for bit on every
+sign-stable pixel at fp32, and on ≥ 99.9 % of them at fp16 (measured: all of them).
+"""
+import numpy as np
+import pytest
+import torch
+
+from gpu_helpers import capture_vgg, engine, forced_all, free, grad_stats, seeded, to64
+from oracle import attack_ref, vgg_ref
+
+pytestmark = pytest.mark.gpu
+
+EPS = 8 / 255
+
+# (dtype, size, rel-norm bound, sign-agreement bound, forced-flip gap bound, flip fraction bound);
+# measured (round 5, profiles/r05_lowp_oracle.log): bf16 1024² norm 4.5e-2, agreement 0.99992,
+# flips 0.58 % of sites with gaps ≤ 3.3e-2 of the layer max; fp16 256² 3.9e-3, 1.00000, 0.065 %,
+# ≤ 3.2e-3; fp16 1024² 2.5e-3, 1.00000, 0.064 %, ≤ 2.3e-3. bf16 keeps 8 significant bits (2^-9
+# relative rounding per stored activation), fp16 11.
+CASES = [
+    (torch.bfloat16, 1024, 6e-2, 0.999, 6e-2, 1e-2),
+    (torch.float16, 256, 1e-2, 0.9999, 1e-2, 2e-3),
+    (torch.float16, 1024, 1e-2, 0.9999, 1e-2, 2e-3),
+]
+
+
+@pytest.mark.parametrize("dtype,size,nrm_tol,agree_tol,gap_tol,frac_tol", CASES)
+def test_lowp_gradient_vs_forced_oracle(cuda, dtype, size, nrm_tol, agree_tol, gap_tol, frac_tol):
+    eng, params = engine(size, dtype, cuda)
+    x0, t = seeded(600 + size, (1, 3, size, size)), seeded(601 + size, (1, 3, size, size))
+    x = (x0 + 0.02 * seeded(602 + size, x0.shape)).clamp(-1, 1)
+    eng.prepare(x0.to(cuda), t.to(cuda))
+    with capture_vgg(eng.V, n=1) as cap:
+        g = eng.full_gradient(x.to(cuda)).cpu().double()
+    assert torch.isfinite(g).all()
+    p64 = to64(params)
+    refs = attack_ref.Refs(*p64, x0.double(), t.double(), size)
+    fa = forced_all(eng, cap, n=1)
+    with fa:
+        _, gr = attack_ref.loss_grad(*p64, x.double(), refs, size)
+    print(f"{dtype} {size}²: " + fa.check(tol=gap_tol, frac=frac_tol))
+    nrm, mx, agree = grad_stats(g, gr)
+    print(f"{dtype} {size}² gradient vs forced fp64 oracle: norm {nrm:.3e} max {mx:.3e} "
+          f"sign agreement {agree:.5f} (bounds: norm {nrm_tol:g}, agreement {agree_tol})")
+    assert nrm < nrm_tol and agree > agree_tol
+    del eng
+    free()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_cfg1_fgsm_vs_oracle(cuda, dtype):
+    """BASELINE cfg1: FGSM ε = 8/255 on a 256² image toward its pair (the attack() entry point)
+    against the oracle's FGSM (attack_ref.pgd with steps = 1, α = ε). Where the oracle's gradient
+    is not tiny the projected step is exact fp32 arithmetic given the sign, so the device output
+    must equal the oracle's there."""
+    from gfa_amd import fgsm, networks
+    size = 256
+    net = networks.build_net(size, seed=0, dtype=dtype, device=cuda)
+    x0, t = seeded(700, (1, 3, size, size)), seeded(701, (1, 3, size, size))
+    adv = fgsm(net, x0.to(cuda), EPS, target=t.to(cuda)).cpu()
+    gp, ep = net.params["generator"], net.params["encoder"]
+    vp = vgg_ref.load_positional(net.params["vgg"])
+    p64 = to64((gp, vp, ep))
+    refs = attack_ref.Refs(*p64, x0.double(), t.double(), size)
+    _, gr = attack_ref.loss_grad(*p64, x0.double(), refs, size)
+    want = attack_ref.project_step(x0, x0, gr.float(), 2 * EPS, 2 * EPS)
+    ref = attack_ref.pgd(gp, vp, ep, x0, t, size, EPS, EPS, 1)
+    stable = gr.abs() > 1e-3 * gr.abs().max()
+    eq = (adv[stable] == want[stable]).float().mean().item()
+    eq_ref = (adv[stable] == ref[stable]).float().mean().item()
+    print(f"cfg1 FGSM {dtype}: equal to the fp64-gradient projection on {eq:.5f} and to the fp32 "
+          f"oracle FGSM on {eq_ref:.5f} of {int(stable.sum())} sign-stable pixels")
+    assert ((adv - x0).abs() <= float(np.float32(2 * EPS)) + 1e-6).all()
+    if dtype == torch.float32:
+        assert torch.equal(adv[stable], want[stable])
+    else:
+        assert eq >= 0.999

@@ -146,14 +146,16 @@ __global__ __launch_bounds__(256) void chan_dot_kernel(const T* __restrict__ a,
       }
     }
   }
+  // LDS image red[e][thread]: consecutive lanes on consecutive banks for the stores and for the
+  // reads below (the [thread][e] image put 8 lanes on one bank: 0.645 bank-conflict ratio, r04)
 #pragma unroll
-  for (int e = 0; e < 8; ++e) red[tid * 8 + e] = acc[e];
+  for (int e = 0; e < 8; ++e) red[e * 256 + tid] = acc[e];
   __syncthreads();
   if (tid < lanes_per_pix) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float s = 0.f;
-      for (int q = 0; q < pr; ++q) s += red[(q * lanes_per_pix + tid) * 8 + e];
+      for (int q = 0; q < pr; ++q) s += red[e * 256 + q * lanes_per_pix + tid];
       red_store(part, gridDim.x, gridDim.y * C, 0, blockIdx.x, n * C + tid * 8 + e, s);
     }
   }
@@ -197,14 +199,14 @@ __global__ __launch_bounds__(256) void chan_part_kernel(const T* __restrict__ a,
   }
   // (C > 2048 is rejected: every channel chunk c8 < cv maps to one lane, lanes_per_pix = cv)
 #pragma unroll
-  for (int e = 0; e < 8; ++e) red[tid * 8 + e] = acc[e];
+  for (int e = 0; e < 8; ++e) red[e * 256 + tid] = acc[e];  // conflict-free image (chan_dot)
   __syncthreads();
   if (tid < lanes_per_pix) {
     float* dst = part + ((size_t)n * gridDim.x + blockIdx.x) * C + tid * 8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float s = 0.f;
-      for (int q = 0; q < pr; ++q) s += red[(q * lanes_per_pix + tid) * 8 + e];
+      for (int q = 0; q < pr; ++q) s += red[e * 256 + q * lanes_per_pix + tid];
       dst[e] = s;
     }
   }

@@ -93,6 +93,9 @@ class E4EEncoder:
         self.size = int(size)
         self.n_latent = n_latent_for(self.size)
         self.R = min(self.size, 256)
+        if self.R != 256:  # the style-head pyramid (16², 32², 64² FPN maps) needs a 256² input
+            raise ValueError("E4EEncoder: the encoder runs on 256² inputs (pSp resizes to 256; "
+                             f"avg_pool2d for larger images): size {self.size} < 256")
         self.dtype = T = dtype
         self.device = dev = torch.device(device)
         self.latent_avg = p["latent_avg"].float().to(dev)

@@ -272,7 +272,9 @@ def run_leg(args, dtype, steps, warmup, dev, world, rank, roofline, make_engine=
         else:
             adv = eng.run(x0, tgt, args.pgd_steps, eps, alpha, group=grp)
         if world > 1:
-            gathered[:] = [gather_shards(adv, n_total)]
+            # gloo (the CPU tests, and several ranks sharing one GPU) gathers host tensors
+            gloo = dist.get_backend() == "gloo"
+            gathered[:] = [gather_shards(adv.cpu() if gloo else adv, n_total)]
         return adv
 
     cuda = dev.type == "cuda"
@@ -317,7 +319,7 @@ def run_leg(args, dtype, steps, warmup, dev, world, rank, roofline, make_engine=
     if gathered:  # the all-gathered job output: n_total images, this rank's shard in place
         ga = gathered[0]
         r["gathered_ok"] = (tuple(ga.shape) == (n_total,) + tuple(adv.shape[1:])
-                            and torch.equal(ga[rank * B:(rank + 1) * B], adv))
+                            and torch.equal(ga[rank * B:(rank + 1) * B], adv.to(ga.device)))
     if prof:
         # The conv-busy time is the union of the conv API calls' [start, end] event intervals
         # (device clock, origin t_ref; one stream, so no overlap); achieved = algorithmic FLOPs ÷

@@ -588,6 +588,7 @@ static int run_conv(ConvK& k, int dtype, hipStream_t st) {
   if (conv_wres32_eligible(k, dtype)) return launch_conv_wres32(k, dtype, st);
   if (conv_thin32_eligible(k, dtype)) return launch_conv_thin32(k, dtype, st);
   if (conv_wres_eligible(k, dtype)) return launch_conv_wres(k, dtype, st);
+  if (conv_wres128_eligible(k, dtype)) return launch_conv_wres128(k, dtype, st);
   if (conv_halo_x6_eligible(k, dtype)) return launch_conv_halo_x6(k, st);
   if (conv_halo_eligible(k, dtype)) return launch_conv_halo(k, dtype, st);
   MIA_DISPATCH_DTYPE(dtype, T, return launch_conv<T>(k, st));

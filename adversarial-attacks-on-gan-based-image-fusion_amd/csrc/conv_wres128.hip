@@ -43,29 +43,38 @@ struct Wres128Tile {
   static constexpr int NPIECE = HBUF / 1024;            // 1-KB DMA pieces per halo (50)
   static constexpr int P_INS = (NPIECE + NW - 1) / NW;  // pieces per wave (≤ 7)
   static constexpr int NZB = 1024;                      // per wave: the patch's noise rows
-  static constexpr int LDS = 2 * HBUF + NW * NZB;
+  static constexpr int AXB = FM * 16 * 32;              // per wave: 16 channels of aux_x (4 KB)
+  static constexpr int CHB = 256;                       // per wave: 3 × 16 per-channel constants
   static_assert(CIN == 128, "one DMA piece = one 4-pixel group (GB = 1 KB)");
   static_assert(HBUF % 1024 == 0 && GB == 1024, "halo layout");
 };
 
 __device__ __forceinline__ int sw128(int v) { return (v >> 1) & 3; }
 
-// EPI: NOISE | BIAS | LRELU (the StyledConv forward on modulated + demodulated weights).
-// k.wn > 0: per-image weight matrices wn elements apart; 0: one shared matrix.
+// EPI (halo_epilogue.h feature masks, the same per-element operations in the same order):
+//   NOISE | BIAS | LRELU — the StyledConv forward on per-image modulated + demodulated weights
+//     (k.wn > 0: the images' matrices wn elements apart);
+//   OSC | SDOT | BAB — the StyledConv input gradient of the 256² block with the style-gradient dot
+//     (sdot) and the fused backward front of the layer below (bab: its lrelu', demod scale and the
+//     q sum), on the shared dgrad matrix (k.wn = 0).
 template <typename T, int CIN, int EPI>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wres128_kernel(const ConvK k) {
   typedef Wres128Tile<CIN> TL;
   typedef typename Vec<T>::type VT;
+  using namespace epi;
   constexpr int FM = TL::FM, NW = TL::NW, NS = TL::NS, HBUF = TL::HBUF, NPIECE = TL::NPIECE;
   constexpr int GB = TL::GB, P_INS = TL::P_INS;
-  static_assert(EPI == (epi::NOISE | epi::BIAS | epi::LRELU), "the StyledConv forward epilogue");
+  constexpr bool FWD = EPI == (NOISE | BIAS | LRELU);
+  constexpr bool DG = EPI == (OSC | SDOT | BAB);
+  static_assert(FWD || DG, "the StyledConv forward / input-gradient epilogues");
+  constexpr int SLOTB = TL::CHB + TL::NZB + (DG ? TL::AXB : 0);  // per-wave epilogue operands
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const mia_conv_args& p = k.a;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int frow = lane & 15, fq = lane >> 4;
-  const int H = p.H, W = p.W;
+  const int H = p.H, W = p.W, Cout = p.Cout;
   const int ptx = W / TL::PW, pty = H / TL::PH;
   const int ntiles = p.N * ptx * pty;
   const int per = (ntiles + gridDim.x - 1) / gridDim.x;
@@ -76,6 +85,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int kpad = k.g[0].kpad;
   T* __restrict__ Y = (T*)p.y;
   const int cw0 = 16 * wid;  // this wave's first output channel
+  const int cl = cw0 + ((lane >> 4) << 2);  // this lane's 4 channels (lane row r: cw0 + 4r …)
   // the zero page for padding lanes, loaded once (not rematerialised per DMA piece)
   const T* zero = (const T*)g_zero16;
   asm volatile("" : "+s"(zero));
@@ -96,14 +106,36 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
       for (int s = 0; s < NS; ++s) wreg[t][s] = *(const VT*)(Wn + t * CIN + s * 32);
   };
+  // per-channel epilogue constants of image n (FWD: the bias; DG: style s, the layer below's
+  // demod and bias), kept in this wave's LDS slot [3][16] (not in registers across the MFMAs)
+  char* const slot = smem + 2 * HBUF + wid * SLOTB;
+  float* const chl = (float*)slot;
+  auto load_chan = [&](int n) {
+    f32x4 c0, c1 = {0.f, 0.f, 0.f, 0.f}, c2 = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (FWD) {
+      c0 = *(const f32x4*)(p.bias + cl);
+    } else {
+      c0 = *(const f32x4*)(p.out_scale + (size_t)n * k.cout_mod + cl);
+      c1 = *(const f32x4*)(p.bab_demod + (size_t)n * Cout + cl);
+      c2 = *(const f32x4*)(p.bab_bias ? p.bab_bias + cl : (const float*)zero);
+    }
+    if ((lane & 15) == 0) {  // (a wave's LDS accesses execute in order: no wait before reads)
+      *(f32x4*)(chl + cl - cw0) = c0;
+      *(f32x4*)(chl + 16 + cl - cw0) = c1;
+      *(f32x4*)(chl + 32 + cl - cw0) = c2;
+    }
+  };
 
-  // the lane's part of a DMA piece (one 4-pixel group of a halo row): sub-plane s, pixel pp of
-  // the group, stored chunk cs (LDS byte 16·lane of the piece)
-  const int ls = lane >> 4, lpp = (lane >> 2) & 3, lcs = lane & 3;
   // wave wid DMAs halo pieces wid + NW·j; piece pc = halo row pc / 5, pixels 4·(pc % 5) …
   auto issue_halo = [&](int tile, int buf) {
     int n, y0, x0;
     tile_pos(tile, n, y0, x0);
+    // the lane's part of a DMA piece (one 4-pixel group of a halo row): sub-plane s, pixel pp of
+    // the group, stored chunk cs (LDS byte 16·lane of the piece); from an opaque copy of the lane
+    // id, so the per-piece lane terms are recomputed per patch instead of hoisted (they spilled)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int ls = ln >> 4, lpp = (ln >> 2) & 3, lcs = ln & 3;
 #pragma unroll
     for (int j = 0; j < P_INS; ++j) {
       const int pc = wid + NW * j;  // wave-uniform
@@ -121,32 +153,36 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       }
     }
   };
-  // this wave's copy of the patch's noise rows (8 rows × 16 floats; lanes ≥ 32 read zeros)
-  char* const nzl = smem + 2 * HBUF + wid * TL::NZB;
-  auto issue_noise = [&](int y0, int x0) {
-    const float* src = lane < 32 ? p.noise + (size_t)(y0 + (lane >> 2)) * W + x0 + 4 * (lane & 3)
-                                 : (const float*)zero;
-    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)nzl, 16, 0, 0);
-  };
-
-  // the bias of this lane's 4 channels (lane row r: channels cw0 + 4r …)
-  const f32x4 bia = *(const f32x4*)(p.bias + cw0 + ((lane >> 4) << 2));
-
-  // lane-constant A-fragment offsets per column shift dx (pixel column v = frow + dx)
-  int offa[3];
+  // this wave's epilogue operands of the patch, DMA'd at its start (they land during the MFMAs):
+  // the noise rows (FWD: the layer's noise; DG: the layer below's) as 8 rows × 16 floats (lanes
+  // ≥ 32 read zeros), and (DG) its 16 channels of aux_x for the 128 pixels: pixel q's two 16-B
+  // chunks at q·32 + ((c ^ (q >> 3)) & 1)·16 (ds_read_b64 of the epilogue conflict-free)
+  char* const aux = slot + TL::CHB;
+  auto issue_aux = [&](int n, int y0, int x0) {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const float* nzp = FWD ? p.noise : p.bab_noise;
+    const float* src = ln < 32 && nzp ? nzp + (size_t)(y0 + (ln >> 2)) * W + x0 + 4 * (ln & 3)
+                                      : (const float*)zero;
+    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)aux, 16, 0, 0);
+    if constexpr (DG) {
+      const T* AX = (const T*)p.aux_x;
 #pragma unroll
-  for (int dx = 0; dx < 3; ++dx) {
-    const int v = frow + dx;
-    int o = (v >> 2) * GB + (v & 3) * 64 + ((fq ^ sw128(v)) << 4);
-    asm volatile("" : "+v"(o));
-    offa[dx] = o;
-  }
+      for (int j = 0; j < 4; ++j) {
+        const int q = j * 32 + (ln >> 1), c = (ln & 1) ^ ((q >> 3) & 1);
+        const T* a = AX + ((size_t)(n * H + y0 + (q >> 4)) * W + x0 + (q & 15)) * Cout + cw0 + 8 * c;
+        __builtin_amdgcn_global_load_lds((gptr_t)a, (lptr_t)(aux + TL::NZB + j * 1024), 16, 0,
+                                         0);
+      }
+    }
+  };
 
   int wimg = -1;
   {
     int n, y0, x0;
     tile_pos(t0, n, y0, x0);
     load_w(n);
+    load_chan(n);
     wimg = n;
   }
   issue_halo(t0, 0);
@@ -155,15 +191,28 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __builtin_amdgcn_s_waitcnt(0x0f70);
   int buf = 0;
   for (int tile = t0; tile < t1; ++tile) {
-    // every wave finished the previous patch (buffer buf^1 and its noise slot are free) and
+    // every wave finished the previous patch (buffer buf^1 and its operand slot are free) and
     // drained its DMA pieces of this patch (buffer buf is complete). LDS-only hand-off: no
     // vector-memory wait, so the previous epilogue's stores stay in flight
     lds_handoff();
     int n, y0, x0;
     tile_pos(tile, n, y0, x0);
-    issue_noise(y0, x0);
+    issue_aux(n, y0, x0);
     if (tile + 1 < t1) issue_halo(tile + 1, buf ^ 1);
     const char* hb = smem + buf * HBUF;
+    // lane-constant A-fragment offsets per column shift dx (pixel column v = frow + dx),
+    // recomputed per patch from an opaque lane id (held across the whole run they were spilled,
+    // and the reload's vmcnt wait then also waited for the next halo's DMA)
+    int offa[3];
+    {
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const int v = (ln & 15) + dx, f = ln >> 4;
+        offa[dx] = (v >> 2) * GB + (v & 3) * 64 + ((f ^ sw128(v)) << 4);
+      }
+    }
     f32x4 acc[FM];
 #pragma unroll
     for (int i = 0; i < FM; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -190,24 +239,50 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           }
           cur = nxt;
         }
-    // the next patch's halo and this patch's noise were issued a whole patch ago: drain them
+    // the next patch's halo and this patch's operands were issued a whole patch ago: drain them
     // before the epilogue's stores (vmcnt retires in order)
     __builtin_amdgcn_s_waitcnt(0x0f70);
     const int px = lane & 15, lrow = lane >> 4;
-    const float* nz = (const float*)nzl;
+    const float* nz = (const float*)aux;
+    const float nzw = FWD ? p.noise_w : p.bab_noise_w;
+    const f32x4 c0 = *(const f32x4*)(chl + cl - cw0);
+    f32x4 c1, c2;
+    if constexpr (DG) {
+      c1 = *(const f32x4*)(chl + 16 + cl - cw0);
+      c2 = *(const f32x4*)(chl + 32 + cl - cw0);
+    }
+    float part[4] = {0.f, 0.f, 0.f, 0.f}, partq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < FM; i += 2) {
       // rows i, i+1: after the swap lane row r holds channels 8·(r >> 1) … +7 of row i + (r & 1)
       float vo[2][4];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const float z = p.noise_w * nz[(i + u) * 16 + px];
+        const float z = nzw * nz[(i + u) * 16 + px];
+        if constexpr (FWD) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = acc[i + u][e];
-          v += z;
-          v += bia[e];
-          vo[u][e] = lrelu_s2(v);
+          for (int e = 0; e < 4; ++e) {
+            float v = acc[i + u][e];
+            v += z;
+            v += c0[e];
+            vo[u][e] = lrelu_s2(v);
+          }
+        } else {
+          const int q = (i + u) * 16 + px;
+          typedef T t4 __attribute__((ext_vector_type(4)));
+          const t4 xr = *(const t4*)(aux + TL::NZB + q * 32 +
+                                     ((((lrow >> 1) ^ (q >> 3)) & 1) << 4) + ((lrow & 1) << 3));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float v = acc[i + u][e];
+            const float xv = (float)xr[e];
+            part[e] += v * xv;
+            v *= c0[e];
+            const float gr = lrelu_s2_grad(xv);
+            const float gp = v * gr;
+            partq[e] += gp * (xv * lrelu_s2_inv_grad(xv) - z - c2[e]);
+            vo[u][e] = gp * c1[e];
+          }
         }
       }
       typedef T t2 __attribute__((ext_vector_type(2)));
@@ -226,12 +301,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const int c = cw0 + 8 * (lrow >> 1);
       *(uint4*)(Y + (size_t)m * k.ystride + c) = make_uint4(a[0], a[1], b[0], b[1]);
     }
+    if constexpr (DG) {
+      // the patch's sdot / q partials of this wave's channels: one contributor slot per patch
+      // (ordered finish, mia_common.h RedQ)
+      const int slt = (y0 / TL::PH) * ptx + x0 / TL::PW;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a = row16_sum(part[e]), b = row16_sum(partq[e]);
+        if (px == 0) {
+          red_put(k, 0, slt, n * Cout + cl + e, a);
+          red_put(k, 1, slt, n * Cout + cl + e, b);
+        }
+      }
+    }
     if (tile + 1 < t1) {
       int n1, y1, x1;
       tile_pos(tile + 1, n1, y1, x1);
-      if (n1 != wimg) {  // block-uniform: the run reaches the next image's weights. Loaded and
-        load_w(n1);      // waited for here, so no wait for them (which would also wait for the
-        wimg = n1;       // next halo, in flight behind them) lands in the next patch's MFMAs
+      if (n1 != wimg) {  // block-uniform: the run reaches the next image. Its weights (per-image
+        if constexpr (FWD) load_w(n1);  // matrices) and constants are loaded and waited for here, so no
+        load_chan(n1);         // wait for them (which would also wait for the next halo, in
+        wimg = n1;             // flight behind them) lands in the next patch's MFMAs
         __builtin_amdgcn_s_waitcnt(0x0f70);
       }
     }
@@ -242,11 +331,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 template <typename T, int CIN, int EPI>
 static int launch_wres128_(ConvK& k, hipStream_t st) {
   typedef Wres128Tile<CIN> TL;
+  constexpr bool DG = (EPI & epi::SDOT) != 0;
+  constexpr int LDS = 2 * TL::HBUF + TL::NW * (TL::CHB + TL::NZB + (DG ? TL::AXB : 0));
+  static_assert(LDS <= 160 * 1024, "LDS budget");
   auto fn = conv_wres128_kernel<T, CIN, EPI>;
   static int ncu = 0;
   if (!ncu) {
-    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            TL::LDS) != hipSuccess)
+    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS) !=
+        hipSuccess)
       return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
     int dev = 0;
     (void)hipGetDevice(&dev);
@@ -256,32 +348,48 @@ static int launch_wres128_(ConvK& k, hipStream_t st) {
   const int ntiles = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW);
   const int per = (ntiles + ncu - 1) / ncu;
   const int grid = (ntiles + per - 1) / per;  // every block has a non-empty run
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(TL::NT), TL::LDS, st, k);
-  return check_launch("conv_wres128");
+  k.prered = 0;
+  RedQ r;
+  int rc = conv_red_begin(k, r, DG ? (k.a.H / TL::PH) * (k.a.W / TL::PW) : 1, st);
+  if (rc != MIA_OK) return rc;
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(TL::NT), LDS, st, k);
+  rc = check_launch("conv_wres128");
+  return rc != MIA_OK ? rc : red_finish(r, st);
 }
 
 // Eligible: 2-byte type, Cin 128 → Cout 128, one group, stride 1, 3×3 pad 1, identity placement,
-// H % 8 == 0, W % 16 == 0, dense output rows, the StyledConv forward epilogue (noise, bias,
-// leaky ReLU, no demod: per-image modulated + demodulated weights). T_CONV_WRES128 = 0 disables.
+// H % 8 == 0, W % 16 == 0, dense output rows, and either the StyledConv forward epilogue on
+// per-image weights (noise, bias, leaky ReLU; mia_conv3x3_wmod) or the StyledConv input gradient
+// with the style dot and the fused backward front (OSC | SDOT | BAB, shared weights).
+// T_CONV_WRES128 = 0 disables.
 bool conv_wres128_eligible(const ConvK& k, int dtype) {
   if (tune(T_CONV_WRES128) == 0) return false;
   const mia_conv_args& a = k.a;
   const ConvGroup& G = k.g[0];
   using namespace epi;
-  return dtype != MIA_F32 && k.ng == 1 && k.stride == 1 && G.kh == 3 && G.kw == 3 &&
-         G.pad_y == 1 && G.pad_x == 1 && G.ho == a.H && G.wo == a.W && G.ay == 1 && G.ax == 1 &&
-         G.by == 0 && G.bx == 0 && !a.shuffle_out && a.H % 8 == 0 && a.W % 16 == 0 &&
-         a.Cin == 128 && a.Cout == 128 && k.HT == a.H && k.WT == a.W && !a.in_scale &&
-         a.act_in == MIA_ACT_NONE && G.kpad >= 9 * 128 && a.y && a.noise && a.bias &&
-         epi_mask(k) == (NOISE | BIAS | LRELU);
+  if (dtype == MIA_F32 || k.ng != 1 || k.stride != 1 || G.kh != 3 || G.kw != 3 ||
+      G.pad_y != 1 || G.pad_x != 1 || G.ho != a.H || G.wo != a.W || G.ay != 1 || G.ax != 1 ||
+      G.by != 0 || G.bx != 0 || a.shuffle_out || a.H % 8 != 0 || a.W % 16 != 0 ||
+      a.Cin != 128 || a.Cout != 128 || k.HT != a.H || k.WT != a.W || a.in_scale ||
+      a.act_in != MIA_ACT_NONE || G.kpad < 9 * 128 || !a.y || k.ystride != a.Cout ||
+      k.ysplit > 0)
+    return false;
+  const int f = epi_mask(k);
+  if (f == (NOISE | BIAS | LRELU)) return a.noise && a.bias && k.wn > 0;
+  if (f == (OSC | SDOT | BAB)) return k.wn == 0 && k.cout_mod == a.Cout;
+  return false;
 }
 
 int launch_conv_wres128(ConvK& k, int dtype, hipStream_t st) {
   using namespace epi;
+  const int f = epi_mask(k);
   MIA_DISPATCH_DTYPE(dtype, T, {
-    if constexpr (sizeof(T) == 2) return launch_wres128_<T, 128, NOISE | BIAS | LRELU>(k, st);
+    if constexpr (sizeof(T) == 2) {
+      if (f == (NOISE | BIAS | LRELU)) return launch_wres128_<T, 128, NOISE | BIAS | LRELU>(k, st);
+      if (f == (OSC | SDOT | BAB)) return launch_wres128_<T, 128, OSC | SDOT | BAB>(k, st);
+    }
   });
-  return set_error("conv_wres128: 2-byte dtypes only");
+  return set_error("conv_wres128: no specialisation for this launch");
 }
 
 }  // namespace mia

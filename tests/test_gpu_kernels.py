@@ -270,6 +270,67 @@ def test_wres128_modconv_fwd(cuda, tune, dtype, N, R, W):
         assert (d <= lim + 1e-6).all()
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,R,W,with_noise", [(20, 64, 64, True), (2, 256, 256, True),
+                                               (3, 40, 48, False)])
+def test_wres128_dgrad_sdot_bab(cuda, tune, dtype, N, R, W, with_noise):
+    """The weights-resident kernel's StyledConv input gradient (OSC | SDOT | BAB: the 256² block's
+    dgrad with the style-gradient dot and the fused backward front of the layer below) against
+    the halo tile on the same operands (MIA_CONV_WRES128=0; R = 40 is not a halo shape, so there
+    against the fp32 torch formula only) and against fp32 torch: the stored output to the output
+    rounding, the ordered sdot / q sums to fp32 summation-order noise."""
+    C = 128
+    g = torch.Generator().manual_seed(N * 7 + R)
+    gy = (torch.randn(N, R, W, C, generator=g) * 0.5).to(dtype)
+    w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
+    ax = (torch.randn(N, R, W, C, generator=g)).to(dtype)
+    s = torch.rand(N, C, generator=g) + 0.5
+    dm = torch.rand(N, C, generator=g) + 0.5
+    nz = torch.randn(R * W, generator=g)
+    bb = 0.1 * torch.randn(C, generator=g)
+    wd = layouts.dgrad_matrix(w.double(), dtype).to(cuda)
+
+    def run():
+        y = torch.empty(N, R, W, C, dtype=dtype, device=cuda)
+        sd = torch.zeros(N, C, device=cuda)
+        q = torch.zeros(N, C, device=cuda)
+        bab = dict(demod=dm.to(cuda), q=q, bias=bb.to(cuda))
+        if with_noise:
+            bab.update(noise=nz.to(cuda), noise_w=0.3)
+        ops.conv3x3(gy.to(cuda), wd, y, cout=C, out_scale=s.to(cuda), aux_x=ax.to(cuda),
+                    sdot=sd, bab=bab)
+        torch.cuda.synchronize()
+        return y, sd, q
+
+    y, sd, q = run()
+    # fp32 reference: gx = dgrad(gy); sdot = Σ gx·x; v = gx·s; front of the layer below
+    wq = w.to(dtype).float().to(cuda)
+    gyf = gy.float().to(cuda).permute(0, 3, 1, 2)
+    xx = torch.zeros(N, C, R, W, device=cuda, requires_grad=True)
+    (gx,) = torch.autograd.grad((F.conv2d(xx, wq, padding=1) * gyf).sum(), xx)
+    xv = ax.float().to(cuda).permute(0, 3, 1, 2)
+    sd_ref = (gx * xv).sum((2, 3))
+    v = gx * s.to(cuda).view(N, C, 1, 1)
+    gr = torch.where(xv > 0, math.sqrt(2), 0.2 * math.sqrt(2))
+    gp = v * gr
+    inv = torch.where(xv > 0, 1 / math.sqrt(2), 1 / (0.2 * math.sqrt(2)))
+    z = (0.3 * nz.to(cuda).view(1, 1, R, W)) if with_noise else 0.0
+    q_ref = (gp * (xv * inv - z - bb.to(cuda).view(1, C, 1, 1))).sum((2, 3))
+    y_ref = gp * dm.to(cuda).view(N, C, 1, 1)
+    e_y, e_s, e_q = rel_err(nchw(y), y_ref), rel_err(sd, sd_ref), rel_err(q, q_ref)
+    print(f"wres128 dgrad {dtype} {N}x{R}x{W}: rel err y {e_y:.2e} sdot {e_s:.2e} q {e_q:.2e}")
+    ulp = 2.0 ** (-10 if dtype == torch.float16 else -7)
+    assert e_y < 2 * ulp and e_s < 1e-4 and e_q < 1e-4
+    if R % 16 == 0:
+        tune("MIA_CONV_WRES128", 0)
+        y2, sd2, q2 = run()
+        d = (y.float() - y2.float()).abs()
+        print(f"wres128 vs halo dgrad: {int((y != y2).sum())} of {y.numel()} outputs differ, "
+              f"max {float(d.max()):.2e}; sdot {rel_err(sd, sd2):.2e} q {rel_err(q, q2):.2e}")
+        assert (d <= y2.float().abs() * (2 * ulp) + 1e-6).all()
+        assert rel_err(sd, sd2) < 1e-5 and rel_err(q, q2) < 1e-5
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("up", [False, True])
 @pytest.mark.parametrize("store_act", [False, True])

@@ -68,6 +68,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   constexpr bool DG = EPI == (OSC | SDOT | BAB);
   static_assert(FWD || DG, "the StyledConv forward / input-gradient epilogues");
   constexpr int SLOTB = TL::CHB + TL::NZB + (DG ? TL::AXB : 0);  // per-wave epilogue operands
+  // DG: the next halo's DMA pieces are issued one per (dx, s) fragment group inside the MFMA loop
+  // (868 → 906 TFLOP/s); the forward keeps them at the patch start (1207 vs 1182 spread;
+  // profiles/r05_layers_fp16_{spread,nospread}.txt)
+  constexpr bool SPREAD = DG;
+  static_assert(!SPREAD || 3 * NS >= P_INS, "one piece per fragment group");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const mia_conv_args& p = k.a;
@@ -127,31 +132,30 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   };
 
   // wave wid DMAs halo pieces wid + NW·j; piece pc = halo row pc / 5, pixels 4·(pc % 5) …
-  auto issue_halo = [&](int tile, int buf) {
-    int n, y0, x0;
-    tile_pos(tile, n, y0, x0);
+  auto issue_piece = [&](int j, int n, int y0, int x0, int buf) {
+    const int pc = wid + NW * j;  // wave-uniform
+    if (pc >= NPIECE) return;
     // the lane's part of a DMA piece (one 4-pixel group of a halo row): sub-plane s, pixel pp of
     // the group, stored chunk cs (LDS byte 16·lane of the piece); from an opaque copy of the lane
     // id, so the per-piece lane terms are recomputed per patch instead of hoisted (they spilled)
     int ln = lane;
     asm volatile("" : "+v"(ln));
     const int ls = ln >> 4, lpp = (ln >> 2) & 3, lcs = ln & 3;
+    const int hy = pc / 5, c5 = pc - 5 * hy;
+    const int y = y0 + hy - 1;
+    const int hx = 4 * c5 + lpp;
+    const int x = x0 + hx - 1;
+    const bool ok = y >= 0 && y < H && hx < TL::PW + 2 && x >= 0 && x < W;
+    const int yc = ok ? y : 0, xc = ok ? x : 0;
+    const T* a = X + ((size_t)(n * H + yc) * W + xc) * CIN + ls * 32 + ((lcs ^ sw128(hx)) << 3);
+    __builtin_amdgcn_global_load_lds((gptr_t)(ok ? a : zero),
+                                     (lptr_t)(smem + buf * HBUF + pc * 1024), 16, 0, 0);
+  };
+  auto issue_halo = [&](int tile, int buf) {
+    int n, y0, x0;
+    tile_pos(tile, n, y0, x0);
 #pragma unroll
-    for (int j = 0; j < P_INS; ++j) {
-      const int pc = wid + NW * j;  // wave-uniform
-      if (pc < NPIECE) {
-        const int hy = pc / 5, c5 = pc - 5 * hy;
-        const int y = y0 + hy - 1;
-        const int hx = 4 * c5 + lpp;
-        const int x = x0 + hx - 1;
-        const bool ok = y >= 0 && y < H && hx < TL::PW + 2 && x >= 0 && x < W;
-        const int yc = ok ? y : 0, xc = ok ? x : 0;
-        const T* a = X + ((size_t)(n * H + yc) * W + xc) * CIN + ls * 32 +
-                     ((lcs ^ sw128(hx)) << 3);
-        __builtin_amdgcn_global_load_lds((gptr_t)(ok ? a : zero),
-                                         (lptr_t)(smem + buf * HBUF + pc * 1024), 16, 0, 0);
-      }
-    }
+    for (int j = 0; j < P_INS; ++j) issue_piece(j, n, y0, x0, buf);
   };
   // this wave's epilogue operands of the patch, DMA'd at its start (they land during the MFMAs):
   // the noise rows (FWD: the layer's noise; DG: the layer below's) as 8 rows × 16 floats (lanes
@@ -198,7 +202,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     int n, y0, x0;
     tile_pos(tile, n, y0, x0);
     issue_aux(n, y0, x0);
-    if (tile + 1 < t1) issue_halo(tile + 1, buf ^ 1);
+    // SPREAD: the next patch's halo pieces go out inside the MFMA loop, each wave's DMA issue
+    // overlapping its own MFMAs
+    const bool more = tile + 1 < t1;
+    int n1 = 0, y1 = 0, x1 = 0;
+    if (more) tile_pos(tile + 1, n1, y1, x1);
+    if (more && !SPREAD) issue_halo(tile + 1, buf ^ 1);
     const char* hb = smem + buf * HBUF;
     // lane-constant A-fragment offsets per column shift dx (pixel column v = frow + dx),
     // recomputed per patch from an opaque lane id (held across the whole run they were spilled,
@@ -237,20 +246,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             if (i < 0 || i >= FM) continue;
             acc[i] = mfma_chunk<T>(wreg[dy * 3 + dx][s], cur, acc[i]);  // D[channel][pixel]
           }
+          if constexpr (SPREAD) {
+            const int g = dx * NS + s;
+            if (q == 1 && g < P_INS && more) {
+              __builtin_amdgcn_sched_barrier(0);
+              issue_piece(g, n1, y1, x1, buf ^ 1);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
           cur = nxt;
         }
-    // the next patch's halo and this patch's operands were issued a whole patch ago: drain them
+    // the next patch's halo and this patch's operands were issued during its MFMAs: drain them
     // before the epilogue's stores (vmcnt retires in order)
     __builtin_amdgcn_s_waitcnt(0x0f70);
     const int px = lane & 15, lrow = lane >> 4;
     const float* nz = (const float*)aux;
     const float nzw = FWD ? p.noise_w : p.bab_noise_w;
-    const f32x4 c0 = *(const f32x4*)(chl + cl - cw0);
-    f32x4 c1, c2;
-    if constexpr (DG) {
-      c1 = *(const f32x4*)(chl + 16 + cl - cw0);
-      c2 = *(const f32x4*)(chl + 32 + cl - cw0);
-    }
+    // (DG: the per-channel constants are re-read from LDS per row pair below — held across the
+    // epilogue they pushed the kernel past 256 VGPRs)
+    const f32x4 c0 = FWD ? *(const f32x4*)(chl + cl - cw0) : f32x4{0.f, 0.f, 0.f, 0.f};
     float part[4] = {0.f, 0.f, 0.f, 0.f}, partq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < FM; i += 2) {
@@ -268,6 +282,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             vo[u][e] = lrelu_s2(v);
           }
         } else {
+          const f32x4 c0 = *(const f32x4*)(chl + cl - cw0);
+          const f32x4 c1 = *(const f32x4*)(chl + 16 + cl - cw0);
+          const f32x4 c2 = *(const f32x4*)(chl + 32 + cl - cw0);
           const int q = (i + u) * 16 + px;
           typedef T t4 __attribute__((ext_vector_type(4)));
           const t4 xr = *(const t4*)(aux + TL::NZB + q * 32 +
@@ -314,9 +331,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
       }
     }
-    if (tile + 1 < t1) {
-      int n1, y1, x1;
-      tile_pos(tile + 1, n1, y1, x1);
+    if (more) {
       if (n1 != wimg) {  // block-uniform: the run reaches the next image. Its weights (per-image
         if constexpr (FWD) load_w(n1);  // matrices) and constants are loaded and waited for here, so no
         load_chan(n1);         // wait for them (which would also wait for the next halo, in

@@ -218,15 +218,15 @@ def test_modconv_fwd_per_image_weights(cuda, dtype, N, cin, cout, R):
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("N,R,W", [(20, 64, 64), (3, 256, 256), (5, 40, 48)])
-def test_wres128_modconv_fwd(cuda, tune, dtype, N, R, W):
-    """The weights-resident 128 → 128 StyledConv forward (conv_wres128.hip, the 256² layer of the
+@pytest.mark.parametrize("N,R,W,C", [(20, 64, 64, 128), (3, 256, 256, 128), (5, 40, 48, 128)])
+def test_wres128_modconv_fwd(cuda, tune, dtype, N, R, W, C):
+    """The weights-resident StyledConv forward (conv_wres128.hip: 128 → 128, the 256² layer of the
     fp16 / bf16 synthesis) on per-image weights: persistent runs that cross image boundaries
-    (weights reloaded mid-run), 8×16 patches (R = 40: H % 16 ≠ 0), against (a) a torch fp32 GPU
-    conv of the same rounded operands and per-image weights + the same epilogue, and (b) the halo
-    tile (MIA_CONV_WRES128=0) on the same weights: both accumulate in fp32 in different orders,
-    so the outputs agree to the output rounding."""
-    cin = cout = 128
+    (weights reloaded mid-run), patches on a map that is not a halo shape (R = 40), against (a) a torch fp32 GPU conv of the same
+    rounded operands and per-image weights + the same epilogue, and (b) the halo tile
+    (MIA_CONV_WRES128=0) on the same weights: both accumulate in fp32 in different orders, so the
+    outputs agree to the output rounding."""
+    cin = cout = C
     g = torch.Generator().manual_seed(N * 31 + R)
     x = torch.randn(N, R, W, cin, generator=g).to(dtype)
     w = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(9 * cin)

@@ -257,8 +257,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           cur = nxt;
         }
     // the next patch's halo and this patch's operands were issued during its MFMAs: drain them
-    // before the epilogue's stores (vmcnt retires in order)
+    // before the epilogue's stores (vmcnt retires in order); the empty asm keeps the epilogue's
+    // LDS reads of the DMA'd operands below the wait
     __builtin_amdgcn_s_waitcnt(0x0f70);
+    asm volatile("" ::: "memory");
     const int px = lane & 15, lrow = lane >> 4;
     const float* nz = (const float*)aux;
     const float nzw = FWD ? p.noise_w : p.bab_noise_w;

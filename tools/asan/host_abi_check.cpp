@@ -33,8 +33,8 @@ int main() {
   EXPECT(mia_version() > 0, "version");
   // tuning table: every documented switch round-trips; unknown / null names are refused
   const char* keys[] = {"MIA_CONV_HALO", "MIA_CONV_X6", "MIA_HALO_EPI", "MIA_X6_UNR",
-                        "MIA_X6_64AUX", "MIA_CONV_THIN", "MIA_CONV_THIN32", "MIA_CONV_WRES",
-                        "MIA_CONV_TILE", "MIA_CONV_REGEPI", "MIA_CONV_SMALLTILE", "MIA_S2DG_X6",
+                        "MIA_CONV_WRES128", "MIA_CONV_THIN", "MIA_CONV_THIN32", "MIA_CONV_WRES",
+                        "MIA_CONV_REGEPI", "MIA_CONV_SMALLTILE", "MIA_S2DG_X6",
                         "MIA_S2DG_HALO", "MIA_UPCONV_X6", "MIA_UPCONV_HALO", "MIA_EPI_PRERED",
                         "MIA_CONV_WRES32", "MIA_HALO_C64", "MIA_THIN_F32", "MIA_X6_64S", "MIA_UPCONV_X6S"};
   for (const char* k : keys) {

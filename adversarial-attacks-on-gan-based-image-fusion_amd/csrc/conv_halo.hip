@@ -589,32 +589,34 @@ int launch_conv_halo(ConvK& k, int dtype, hipStream_t st) {
 // weight path, the form the reference's generator computes: w' = w·s[n][ci]·demod[n][co]), for
 // the 2-byte halo kernel at high resolution: the activations enter the MFMAs unmodulated, so the
 // kernel has no per-channel-block modulation pass over the halo in LDS and no demod in the
-// epilogue. One thread per 16-B vector of a weight row; rows [n][co] of the [N][Cout][Kpad] out.
+// epilogue. A block writes MW_ROWS rows [n][co0 .. co0+MW_ROWS) of the [N][Cout][Kpad] output, one
+// 16-B vector per thread and pass, with the image's styles staged in LDS (the K index is tap-major,
+// so a vector's 8 styles are 8 consecutive floats); no 64-bit index arithmetic.
+constexpr int MW_ROWS = 16;
 template <typename T>
 __global__ __launch_bounds__(256) void modulate_weights_kernel(const T* __restrict__ w,
                                                                const float* __restrict__ s,
                                                                const float* __restrict__ d,
                                                                T* __restrict__ out, int Cout,
-                                                               int Cin, int K, int Kpad,
-                                                               int64_t nvec) {
+                                                               int Cin, int K, int Kpad) {
   typedef typename Vec<T>::type VT;
   constexpr int VEC = Vec<T>::N;
-  const int vpr = Kpad / VEC;  // vectors per row
-  for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < nvec;
-       v += (int64_t)gridDim.x * 256) {
-    const int64_t row = v / vpr;  // n·Cout + co
-    const int kv = (int)(v - row * vpr) * VEC;
-    const int n = (int)(row / Cout), co = (int)(row - (int64_t)n * Cout);
+  __shared__ float sl[2048];
+  const int n = blockIdx.y, co0 = blockIdx.x * MW_ROWS;
+  for (int c = threadIdx.x; c < Cin; c += 256) sl[c] = s[(size_t)n * Cin + c];
+  __syncthreads();
+  const int vpr = Kpad / VEC, nv = MW_ROWS * vpr;
+  for (int i = threadIdx.x; i < nv; i += 256) {
+    const int r = i / vpr, kv = (i - r * vpr) * VEC, co = co0 + r;
+    if (co >= Cout) break;
     const VT wv = *(const VT*)(w + (size_t)co * Kpad + kv);
-    const float dm = d ? d[row] : 1.f;
-    const float* sn = s + (size_t)n * Cin;
+    const float dm = d ? d[(size_t)n * Cout + co] : 1.f;
+    const int c0 = kv & (Cin - 1);  // Cin ≥ 8 and a power of two: the vector stays in one tap
     VT o;
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) {
-      const int kk = kv + e;
-      o[e] = kk < K ? from_f<T>(to_f(wv[e]) * sn[kk & (Cin - 1)] * dm) : from_f<T>(0.f);
-    }
-    *(VT*)(out + (size_t)row * Kpad + kv) = o;
+    for (int e = 0; e < VEC; ++e)
+      o[e] = kv + e < K ? from_f<T>(to_f(wv[e]) * sl[c0 + e] * dm) : from_f<T>(0.f);
+    *(VT*)(out + ((size_t)n * Cout + co) * Kpad + kv) = o;
   }
 }
 
@@ -627,14 +629,15 @@ extern "C" int mia_modulate_weights(const void* w, const float* in_scale, const 
                                     void* stream) {
   MIA_CHECK_ARG(w && in_scale && w_mod && N > 0 && Cout > 0, "bad args");
   MIA_CHECK_ARG(dtype == MIA_F16 || dtype == MIA_BF16, "2-byte dtypes only");
-  MIA_CHECK_ARG(Cin >= 8 && (Cin & (Cin - 1)) == 0, "Cin must be a power of two >= 8");
+  MIA_CHECK_ARG(Cin >= 8 && Cin <= 2048 && (Cin & (Cin - 1)) == 0,
+                "Cin must be a power of two in [8, 2048]");
   MIA_CHECK_ARG(Kpad == mia_conv_kpad(Cin, dtype), "Kpad must be mia_conv_kpad()");
-  const int64_t nvec = (int64_t)N * Cout * (Kpad / 8);
-  const int grid = (int)std::min<int64_t>((nvec + 255) / 256, 8192);
+  MIA_CHECK_ARG(N <= 65535, "N > 65535");
+  const dim3 grid((Cout + MW_ROWS - 1) / MW_ROWS, N);
   hipStream_t st = (hipStream_t)stream;
   MIA_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL(modulate_weights_kernel<T>, dim3(grid), dim3(256), 0, st, (const T*)w,
-                       in_scale, out_scale, (T*)w_mod, Cout, Cin, 9 * Cin, Kpad, nvec);
+    hipLaunchKernelGGL(modulate_weights_kernel<T>, grid, dim3(256), 0, st, (const T*)w,
+                       in_scale, out_scale, (T*)w_mod, Cout, Cin, 9 * Cin, Kpad);
   });
   return check_launch("modulate_weights");
 }

@@ -342,7 +342,7 @@ def roofline_record(args, dtype, r):
     pmc, src = pmc_profile(key, args.batch, args.size, args.pgd_steps, args.encoder)
     rec = {"kernel": "3x3 conv: every conv API call of the step (mia::conv_halo_kernel, "
                      "mia::upconv_halo_kernel + its edge launch, mia::conv_kernel, "
-                     "mia::conv_wres_kernel, mia::conv_thin_*: StyledConv fwd, up-conv, dgrads, "
+                     "mia::conv_wres_kernel, mia::conv_wres128_kernel, mia::conv_thin_*: StyledConv fwd, up-conv, dgrads, "
                      "VGG fwd/dgrad" + (", e4e convs and their input gradients)"
                                         if args.encoder == "e4e" else ")"),
            "bound": "mfma", "achieved": ach, "peak": peak, "unit": "TFLOP/s", "frac": ach / peak,

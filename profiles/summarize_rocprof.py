@@ -23,8 +23,8 @@ from collections import defaultdict
 # tiles, the halo tiles (fp32 x6 and fp16 / bf16), the halo up-convs (fp32 upconv_x6_kernel and
 # fp16 / bf16 upconv_halo_kernel, both also in DG mode for the stride-2 input gradients), the
 # weights-resident and thin-channel kernels (the fp32 VALU VGG / e4e input layers included)
-CONV = re.compile(r"conv_(halo_|wres_|halo_x6_|halo_x6s_|halo_x6h_)?kernel|upconv_(halo|x6|x6s)_kernel|"
-                  r"conv_thin(_in|_out|32)(_f32)?_kernel|modulate_weights_kernel")
+CONV = re.compile(r"conv_(halo_|wres_|wres32_|wres128_|halo_x6_|halo_x6s_|halo_x6h_)?kernel|upconv_(halo|x6|x6s)_kernel|"
+                  r"conv_thin(_in|_out|_out_strip|32)(_f32)?_kernel|modulate_weights_kernel")
 # the up-conv FORWARD through the halo kernel (mia_upconv_fwd_halo[_split]) is ONE API call that
 # launches TWO kernels (the halo up-conv for the interior + a generic conv_kernel for the last row
 # / column), so the per-call count that bench.py's HIP events see is launches − these launches

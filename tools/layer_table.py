@@ -60,6 +60,17 @@ def main():
     step = e0.elapsed_time(e1)
     print(f"step {step:.1f} ms, conv calls {len(prof)}, conv time {tot:.1f} ms "
           f"({sum(r[2] for r in agg.values()) / tot / 1e9:.0f} TFLOP/s)")
+    peak = 416.7 if a.dtype == "fp32" else 2500.0
+    # the StyleGAN2 modulated convs' forward, FLOP-weighted: the stride-1 StyledConvs ("mod"
+    # labels, the per-image weight pass included), then with the up-sampling convs' forwards
+    for name, sel in (("stride-1 StyledConv", lambda t: " mod" in t),
+                      ("+ up-conv forwards", lambda t: " mod" in t or "upconv_fwd" in t)):
+        rows = [r for t, r in agg.items() if sel(t)]
+        if rows:
+            n, ms, fl = (sum(r[i] for r in rows) for i in range(3))
+            print(f"modulated forward ({name}): {n} calls, {fl / 1e12:.1f} TFLOP in {ms:.1f} ms "
+                  f"= {fl / (ms * 1e-3) / 1e12:.1f} TF/s = {fl / (ms * 1e-3) / 1e12 / peak:.3f} "
+                  f"of {peak:.0f}")
     for t, (n, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.top]:
         print(f"{t:48s} {n:5d} calls {ms:8.2f} ms {ms / n * 1e3:8.1f} us/call "
               f"{fl / (ms * 1e-3) / 1e12:7.1f} TF/s {100 * ms / step:5.1f}%")

@@ -170,6 +170,8 @@ SIGNATURES = {
     "mia_chan_sum": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_chan_dot": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_se_bwd": (c_int, [P, P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
+    "mia_se_fwd_parts": (c_int, [P, c_int, P, P, P, P, c_int, c_int, c_int, c_float, P]),
+    "mia_se_bwd_parts": (c_int, [P, c_int, P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
     "mia_se_grad_scale": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "mia_prelu_bwd_scale": (c_int, [P, P, P, P, P, c_int64, c_int, c_int, P]),
     "mia_subsample_add": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),

@@ -18,15 +18,25 @@ static int ew_grid(int64_t n) {
   return (int)std::min<int64_t>(b, 65536);
 }
 
+// the per-(image, channel) sum of mia_chan_sum: its nch ordered pixel-chunk partials added in
+// chunk order from 0 (the additions of chan_fin_kernel), or the finished sum when nch == 0
+__device__ __forceinline__ float chan_total(const float* __restrict__ v, int nch, int n, int C,
+                                            int c) {
+  if (nch == 0) return v[(size_t)n * C + c];
+  float s = 0.f;
+  for (int q = 0; q < nch; ++q) s += v[((size_t)n * nch + q) * C + c];
+  return s;
+}
+
 // ---- SE forward: u = relu(W1·avg), s = sigmoid(W2·u), one block per image ----------------------
-__global__ __launch_bounds__(256) void se_fwd_kernel(const float* __restrict__ csum,
+__global__ __launch_bounds__(256) void se_fwd_kernel(const float* __restrict__ csum, int nch,
                                                      const float* __restrict__ w1,
                                                      const float* __restrict__ w2, float* u_out,
                                                      float* s_out, int C, int Cr, float inv_hw) {
   __shared__ float avg[512];
   __shared__ float uu[64];
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int c = tid; c < C; c += 256) avg[c] = csum[(size_t)n * C + c] * inv_hw;
+  for (int c = tid; c < C; c += 256) avg[c] = chan_total(csum, nch, n, C, c) * inv_hw;
   __syncthreads();
   for (int j = wid; j < Cr; j += 4) {
     float a = 0.f;
@@ -47,7 +57,7 @@ __global__ __launch_bounds__(256) void se_fwd_kernel(const float* __restrict__ c
 }
 
 // ---- SE backward: gz = gs·s(1−s); gu = (W2ᵀ gz)·[u>0]; gavg = inv_hw·W1ᵀ gu -------------------
-__global__ __launch_bounds__(256) void se_bwd_kernel(const float* __restrict__ gs,
+__global__ __launch_bounds__(256) void se_bwd_kernel(const float* __restrict__ gs, int nch,
                                                      const float* __restrict__ s,
                                                      const float* __restrict__ u,
                                                      const float* __restrict__ w1,
@@ -58,7 +68,7 @@ __global__ __launch_bounds__(256) void se_bwd_kernel(const float* __restrict__ g
   const int n = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int c = tid; c < C; c += 256) {
     const float sv = s[(size_t)n * C + c];
-    gz[c] = gs[(size_t)n * C + c] * sv * (1.f - sv);
+    gz[c] = chan_total(gs, nch, n, C, c) * sv * (1.f - sv);
   }
   __syncthreads();
   for (int j = wid; j < Cr; j += 4) {
@@ -418,20 +428,32 @@ using namespace mia;
 
 extern "C" int mia_se_fwd(const float* csum, const float* w1, const float* w2, float* u, float* s,
                           int N, int C, int Cr, float inv_hw, void* stream) {
-  MIA_CHECK_ARG(csum && w1 && w2 && u && s && N > 0, "bad args");
+  return mia_se_fwd_parts(csum, 0, w1, w2, u, s, N, C, Cr, inv_hw, stream);
+}
+
+extern "C" int mia_se_fwd_parts(const float* part, int nch, const float* w1, const float* w2,
+                                float* u, float* s, int N, int C, int Cr, float inv_hw,
+                                void* stream) {
+  MIA_CHECK_ARG(part && w1 && w2 && u && s && N > 0 && nch >= 0, "bad args");
   MIA_CHECK_ARG(C > 0 && C <= 512 && Cr > 0 && Cr <= 64, "C ≤ 512, C/r ≤ 64");
-  hipLaunchKernelGGL(se_fwd_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, csum, w1, w2, u,
-                     s, C, Cr, inv_hw);
+  hipLaunchKernelGGL(se_fwd_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, part, nch, w1, w2,
+                     u, s, C, Cr, inv_hw);
   return check_launch("se_fwd");
 }
 
 extern "C" int mia_se_bwd(const float* gs, const float* s, const float* u, const float* w1,
                           const float* w2, float* gavg, int N, int C, int Cr, float inv_hw,
                           void* stream) {
-  MIA_CHECK_ARG(gs && s && u && w1 && w2 && gavg && N > 0, "bad args");
+  return mia_se_bwd_parts(gs, 0, s, u, w1, w2, gavg, N, C, Cr, inv_hw, stream);
+}
+
+extern "C" int mia_se_bwd_parts(const float* part, int nch, const float* s, const float* u,
+                                const float* w1, const float* w2, float* gavg, int N, int C,
+                                int Cr, float inv_hw, void* stream) {
+  MIA_CHECK_ARG(part && s && u && w1 && w2 && gavg && N > 0 && nch >= 0, "bad args");
   MIA_CHECK_ARG(C > 0 && C <= 512 && Cr > 0 && Cr <= 64, "C ≤ 512, C/r ≤ 64");
-  hipLaunchKernelGGL(se_bwd_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, gs, s, u, w1, w2,
-                     gavg, C, Cr, inv_hw);
+  hipLaunchKernelGGL(se_bwd_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, part, nch, s, u, w1,
+                     w2, gavg, C, Cr, inv_hw);
   return check_launch("se_bwd");
 }
 
@@ -486,7 +508,8 @@ extern "C" int mia_chan_sum_parts(int N, int HW) {
 
 extern "C" int mia_chan_sum(const void* a, const void* b, float* part, float* out, int N, int HW,
                             int C, int accumulate, int dtype, void* stream) {
-  MIA_CHECK_ARG(a && part && out && N > 0 && HW > 0, "bad args");
+  MIA_CHECK_ARG(a && part && N > 0 && HW > 0, "bad args");
+  MIA_CHECK_ARG(out || !accumulate, "accumulate needs out");
   ENC_CHECK_C(C);
   MIA_CHECK_ARG(C <= 2048, "C ≤ 2048");
   hipStream_t st = (hipStream_t)stream;
@@ -502,7 +525,7 @@ extern "C" int mia_chan_sum(const void* a, const void* b, float* part, float* ou
                          (const T*)a, (const T*)nullptr, part, HW, C, ppc);
   });
   const int rc = check_launch("chan_part");
-  if (rc) return rc;
+  if (rc || !out) return rc;  // out NULL: the partials only (mia_se_fwd_parts / mia_se_bwd_parts)
   hipLaunchKernelGGL(chan_fin_kernel, dim3((N * C + 255) / 256), dim3(256), 0, st, part, out, N, C,
                      nch, accumulate);
   return check_launch("chan_fin");

@@ -305,15 +305,15 @@ class E4EEncoder:
             ops.conv2d(xb, [_g3(U["w1"], h)], a1, (h, h), cout=d, act_out=ACT_PRELU,
                        act_slope=U["slope"])
             r = self._buf(ws, f"r_{i}", (N, ho, ho, d))
-            cs = self._buf(ws, f"cs_{i}", (N, d), f32)
             ops.conv2d(a1, [_g3(U["w2"], ho)], r, (ho, ho), cout=d, stride=s, bias=U["b2"])
             # the SE average pool's sum: an ordered two-pass reduction with per-image pixel
-            # chunks (mia_chan_sum), so the forward — and the PReLU / ReLU branches after it —
-            # reproduce bit for bit run to run and batch to batch
-            ops.chan_sum(r, None, self._chan_part(ws, N, ho * ho, d), cs)
+            # chunks (mia_chan_sum's partials, finished in chunk order inside the SE kernel), so
+            # the forward — and the PReLU / ReLU branches after it — reproduce bit for bit run to
+            # run and batch to batch
+            part = ops.chan_sum(r, None, self._chan_part(ws, N, ho * ho, d), None)
             u = self._buf(ws, f"u_{i}", (N, U["cr"]), f32)
             sv = self._buf(ws, f"s_{i}", (N, d), f32)
-            ops.se_fwd(cs, U["se_w1"], U["se_w2"], u, sv, ho * ho)
+            ops.se_fwd_parts(part, ho * ho, U["se_w1"], U["se_w2"], u, sv)
             if U["cin"] != d:
                 sc = self._buf(ws, f"sc_{i}", (N, ho, ho, d))
                 ops.conv2d(x, [_g1(U["wsc"], ho)], sc, (ho, ho), cout=d, stride=s, bias=U["bsc"])
@@ -502,10 +502,9 @@ class E4EEncoder:
             u = U[i]
             d, s, cin = u["depth"], u["stride"], u["cin"]
             h = u["_a1"].shape[1]
-            gs = ops.chan_sum(Gc, u["_r"], self._chan_part(ws, N, u["_hw"], d),
-                              self._buf(ws, "gs", (N, d), f32))
-            gavg = ops.se_bwd(gs, u["_s"], u["_u"], u["se_w1"], u["se_w2"],
-                              self._buf(ws, "gavg", (N, d), f32), u["_hw"])
+            part = ops.chan_sum(Gc, u["_r"], self._chan_part(ws, N, u["_hw"], d), None)
+            gavg = ops.se_bwd_parts(part, u["_hw"], u["_s"], u["_u"], u["se_w1"], u["se_w2"],
+                                    self._buf(ws, "gavg", (N, d), f32))
             g_r = ops.se_grad_scale(Gc, u["_s"], gavg, self._buf(ws, f"g_r{d}", Gc.shape))
             gp1 = self._buf(ws, f"gp1_{h}_{d}", (N, h, h, d))
             if s == 1:

@@ -896,6 +896,39 @@ def se_fwd(csum, w1, w2, u, s, hw):
     return s
 
 
+def _parts_ok(part, N, hw, C):
+    nch = chan_sum_parts(N, hw)
+    if part.dtype != torch.float32 or part.numel() < N * nch * C:
+        raise ValueError("SE partials: fp32 scratch of N · chan_sum_parts · C floats")
+    return nch
+
+
+def se_fwd_parts(part, hw, w1, w2, u, s):
+    """se_fwd from chan_sum's partials (chan_sum(..., out=None)): the pool sum is finished inside
+    the SE kernel in the same chunk order (mia_se_fwd_parts, bit-identical, one launch fewer)."""
+    N, C = s.shape
+    Cr = w1.shape[0]
+    _need(w1, (Cr, C), torch.float32, "w1")
+    _need(w2, (C, Cr), torch.float32, "w2")
+    _need(u, (N, Cr), torch.float32, "u")
+    nch = _parts_ok(part, N, hw, C)
+    call("mia_se_fwd_parts", ptr(part), nch, ptr(w1), ptr(w2), ptr(u), ptr(s), N, C, Cr, 1.0 / hw,
+         stream())
+    return s
+
+
+def se_bwd_parts(part, hw, s, u, w1, w2, gavg):
+    """se_bwd from chan_sum's partials of gs = Σ ∂out·r (mia_se_bwd_parts)."""
+    N, C = s.shape
+    Cr = w1.shape[0]
+    _need(u, (N, Cr), torch.float32, "u")
+    _need(gavg, (N, C), torch.float32, "gavg")
+    nch = _parts_ok(part, N, hw, C)
+    call("mia_se_bwd_parts", ptr(part), nch, ptr(s), ptr(u), ptr(w1), ptr(w2), ptr(gavg), N, C,
+         Cr, 1.0 / hw, stream())
+    return gavg
+
+
 def se_apply(r, s, sc, ss, out, g=None, b=None, xb=None):
     """out = r·s + sc (sc read at stride ss), xb = out·g + b (either output may be None)."""
     N, H, W, C = r.shape
@@ -929,16 +962,20 @@ def chan_sum_parts(N, HW):
 
 def chan_sum(a, b, part, out, accumulate=False):
     """mia_chan_sum: out (N, C) fp32 (+)= Σ_pixels a·b (b given) or Σ_pixels a, deterministic;
-    part: fp32 scratch of N · chan_sum_parts(N, H·W) · C floats."""
+    part: fp32 scratch of N · chan_sum_parts(N, H·W) · C floats. out None: only the ordered
+    per-chunk partials (for se_fwd_parts / se_bwd_parts); returns part then."""
     N, H, W, C = a.shape
     if b is not None:
         _need(b, a.shape, a.dtype, "b")
-    _need(out, (N, C), torch.float32, "out")
+    if out is not None:
+        _need(out, (N, C), torch.float32, "out")
+    elif accumulate:
+        raise ValueError("chan_sum: accumulate needs out")
     if part.dtype != torch.float32 or part.numel() < N * chan_sum_parts(N, H * W) * C:
         raise ValueError("chan_sum: part scratch too small")
     call("mia_chan_sum", ptr(a), ptr(b), ptr(part), ptr(out), N, H * W, C,
          int(bool(accumulate)), dt(a), stream())
-    return out
+    return out if out is not None else part
 
 
 def se_bwd(gs, s, u, w1, w2, gavg, hw):

@@ -453,6 +453,10 @@ int mia_repeat(const void* src, void* dst, int64_t bytes, int count, void* strea
  *                 (the next unit's BatchNorm, optional); out may be NULL when only xb is wanted.
  *   mia_chan_dot: gs[n][c] (+)= Σ_p a·b  (fp32 out)
  *   mia_se_bwd:  from gs = ∂L/∂s: gz = gs·s(1−s); gu = (W2ᵀ gz)·[u > 0]; gavg = W1ᵀ gu / hw
+ *   mia_se_fwd_parts / mia_se_bwd_parts: the same, with csum / gs given as mia_chan_sum's nch
+ *                 ordered pixel-chunk partials (mia_chan_sum with out NULL) and summed in chunk
+ *                 order inside the kernel: bit-identical to mia_chan_sum + mia_se_fwd / _bwd, one
+ *                 launch fewer per SE module
  *   mia_se_grad_scale: g_r = gamma[c]·(g_out·s[n][c] + gavg[n][c])  (gamma NULL → 1)
  *   mia_prelu_bwd_scale: g = g_a·(a > 0 ? 1 : slope[c])·gamma[c]  (gamma NULL → 1)
  *   mia_cast: y = scale·x converted between dtypes (x, y: flat, n elements)
@@ -470,12 +474,18 @@ int mia_chan_dot(const void* a, const void* b, float* gs, int N, int HW, int C, 
  * out[n][c] (+)= Σ_p a·b (b given: the SE gate gradient Σ ∂out·r, as mia_chan_dot) or Σ_p a
  * (b NULL: the SE average pool's sum, psp_encoders SEModule AdaptiveAvgPool2d, reached through
  * net.encoder at code/attack/attack_main2.py:597,622). Fixed-order reduction through `part`
- * (fp32 scratch of N · mia_chan_sum_parts(N, HW) · C floats): bit-reproducible run to run. */
+ * (fp32 scratch of N · mia_chan_sum_parts(N, HW) · C floats): bit-reproducible run to run.
+ * out NULL (accumulate 0): only the partials part[(n·nch + q)·C + c] are written. */
 int mia_chan_sum_parts(int N, int HW);
 int mia_chan_sum(const void* a, const void* b, float* part, float* out, int N, int HW, int C,
                  int accumulate, int dtype, void* stream);
 int mia_se_bwd(const float* gs, const float* s, const float* u, const float* w1, const float* w2,
                float* gavg, int N, int C, int Cr, float inv_hw, void* stream);
+int mia_se_fwd_parts(const float* part, int nch, const float* w1, const float* w2, float* u,
+                     float* s, int N, int C, int Cr, float inv_hw, void* stream);
+int mia_se_bwd_parts(const float* part, int nch, const float* s, const float* u, const float* w1,
+                     const float* w2, float* gavg, int N, int C, int Cr, float inv_hw,
+                     void* stream);
 int mia_se_grad_scale(const void* g_out, const float* s, const float* gavg, const float* gamma,
                       void* g_r, int N, int HW, int C, int dtype, void* stream);
 int mia_prelu_bwd_scale(const void* g_a, const void* a, const float* slope, const float* gamma,

@@ -267,6 +267,32 @@ def test_se_kernels_vs_autograd(cuda, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("N,H,C", [(3, 16, 256), (2, 7, 64), (1, 64, 512)])
+def test_se_from_partials_bit_identical(cuda, dtype, N, H, C):
+    """mia_se_fwd_parts / mia_se_bwd_parts (the e4e path: chan_sum's ordered chunk partials
+    finished inside the SE kernel) equal mia_chan_sum + mia_se_fwd / mia_se_bwd bit for bit."""
+    Cr = C // 16
+    rd = nhwc(rnd((N, C, H, H), 40), dtype, cuda)
+    god = nhwc(rnd((N, C, H, H), 41), dtype, cuda)
+    w1 = rnd((Cr, C), 42, 1 / math.sqrt(C)).float().to(cuda)
+    w2 = rnd((C, Cr), 43, 1 / math.sqrt(Cr)).float().to(cuda)
+    part = torch.empty(N * ops.chan_sum_parts(N, H * H) * C, device=cuda)
+    cs = ops.chan_sum(rd, None, part, torch.empty(N, C, device=cuda))
+    u0, s0 = torch.empty(N, Cr, device=cuda), torch.empty(N, C, device=cuda)
+    ops.se_fwd(cs, w1, w2, u0, s0, H * H)
+    u1, s1 = torch.full_like(u0, float("nan")), torch.full_like(s0, float("nan"))
+    ops.se_fwd_parts(ops.chan_sum(rd, None, part, None), H * H, w1, w2, u1, s1)
+    gs = ops.chan_sum(god, rd, part, torch.empty(N, C, device=cuda))
+    ga0 = ops.se_bwd(gs, s0, u0, w1, w2, torch.empty(N, C, device=cuda), H * H)
+    ga1 = ops.se_bwd_parts(ops.chan_sum(god, rd, part, None), H * H, s0, u0, w1, w2,
+                           torch.full_like(ga0, float("nan")))
+    torch.cuda.synchronize()
+    assert torch.equal(u0, u1) and torch.equal(s0, s1) and torch.equal(ga0, ga1)
+    with pytest.raises(ValueError):
+        ops.chan_sum(rd, None, part, None, accumulate=True)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("hi,ho", [(16, 32), (32, 64), (4, 9)])
 def test_bilinear_align_corners_fwd_bwd(cuda, dtype, hi, ho):
     N, C = 2, 64

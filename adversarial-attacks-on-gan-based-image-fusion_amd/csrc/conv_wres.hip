@@ -4,35 +4,45 @@
 // first IR-SE50 stage (Encoder4Editing body units 0-2 conv1/conv2 and their input gradients,
 // 256² / 128²; un-vendored, code/utils/model_utils.py:24). At Cout = 64 the tiled kernels pay the
 // per-K-step weight staging and barrier for half the MFMAs of a 128-channel tile (measured 375-
-// 440 TFLOP/s); here the whole weight matrix (K = 9·64 = 576 × 64 channels = 72 KB) is loaded
-// ONCE per wave into VGPRs as MFMA B fragments (288 registers, one wave per SIMD) and the block
-// is persistent over 16×16-pixel output patches:
+// 440 TFLOP/s); here the weights (K = 9·64 = 576) are loaded ONCE per wave into VGPRs as MFMA B
+// fragments and the block is persistent over a contiguous run of 16×16-pixel output patches:
+//   * 8 waves, two per SIMD: wave (wm, wn) owns patch rows 4·wm … 4·wm+3 (one 16-pixel MFMA
+//     fragment per row) × output channels 32·wn … 32·wn+31, and holds only those channels'
+//     weights (144 VGPRs). One wave's epilogue, DMA issue and LDS waits run under its partner's
+//     MFMAs (round 5: the first form, 4 waves × all 64 channels with 288 weight VGPRs and one
+//     wave per SIMD, ran 13–18 % slower per layer and is gone);
 //   * per patch the (16+2)×(16+2) input halo (one 64-channel block, 41 KB) is DMA'd into one of
 //     two LDS buffers a full patch ahead (global_load_lds, bank swizzle fsw() through the source
 //     chunk, zero page for the padding);
-//   * the main loop is 9 taps × 2 K-chunks of ds_read_b128 A fragments and 16 MFMAs each, with
+//   * the main loop is 9 taps × 2 K-chunks of ds_read_b128 A fragments and 8 MFMAs each, with
 //     no barrier and no weight traffic;
 //   * one barrier per patch (all waves finished the previous patch and waited for their DMA
 //     pieces) before the next halo is issued into the buffer just released; each wave drains its
 //     DMA (vmcnt(0)) AFTER its MFMAs and BEFORE its epilogue stores, so the wait never covers
 //     stores and the DMA had a whole patch to land;
 //   * the epilogue is halo_epilogue_f (registers, 16-byte stores); a single per-pixel operand
-//     (mask or old y) is DMA'd into LDS at the start of the patch (WresAux) and lands during the
-//     MFMAs instead of stalling the epilogue.
-// Wave w owns patch rows 4w … 4w+3 (one 16-pixel MFMA fragment per row) × all 64 channels.
+//     (mask or old y) of the wave's pixels and channels is DMA'd into LDS at the start of the
+//     patch (WresAux) and lands during the MFMAs instead of stalling the epilogue.
 #include "conv_common.h"
 #include "halo_epilogue.h"
 
 namespace mia {
 
-struct WresTile {
-  static constexpr int FM = 4, FN = 4, NW = 4, NT = 256;
+template <int NW_, int WN_>
+struct WresTileT {
+  // NW waves; WN channel halves: wave (wm, wn) owns patch rows wm·FM … +FM−1 × output channels
+  // 16·FN·wn … +16·FN−1, and holds only those channels' weights (FN = 4 / WN fragments)
+  static constexpr int NW = NW_, WN = WN_, WM = NW / WN, FM = 16 / WM, FN = 4 / WN, NT = 64 * NW;
   static constexpr int PH = 16, PW = 16, HSIDE = PW + 2, HROWS = (PH + 2) * HSIDE;  // 324
   static constexpr int HPIECES = (HROWS + 7) / 8;                                    // 41
   static constexpr int HBUF = HPIECES * 8 * ROWB;
-  static constexpr int H_INS = (HPIECES + NW - 1) / NW;                              // 11
-  static constexpr int AUXW = FM * 16 * ROWB;  // one per-pixel epilogue operand of a wave: 8 KB
+  static constexpr int H_INS = (HPIECES + NW - 1) / NW;
+  static constexpr int CPP = 2 * FN;            // 16-B chunks per pixel of a wave's channels
+  static constexpr int AUXW = FM * 16 * CPP * 16;  // one per-pixel epilogue operand of a wave
+  static_assert(WM * FM == PH && WN * FN == 4, "");
 };
+// two waves per SIMD, each 32 channels (144 weight VGPRs)
+typedef WresTileT<8, 2> WresTile;
 
 // Per-pixel epilogue operand prefetched into LDS (a wave's 64 pixels × 64 channels): MASK →
 // mask_a, ACC → old y. Register prefetch spills next to the 288 resident weight VGPRs; LDS-DMA
@@ -49,17 +59,19 @@ struct WresAux {
 };
 
 // bank swizzle of the prefetched operand rows (16-B chunk c of pixel q stored at c ^ asw(q)): a
-// ds_read_b64 of 16 pixels × one channel quad pair hits 16 distinct (pixel parity, chunk) slots
-__device__ __forceinline__ int asw(int q) { return (q >> 1) & 7; }
+// ds_read_b64 of 16 pixels × one channel quad pair hits 16 distinct (pixel parity, chunk) slots.
+// FN = 2 (64-B rows): chunk c ^ ((q >> 2) & 3), 16 pixels × 2 halves on 64 distinct dwords.
+template <int FN>
+__device__ __forceinline__ int asw(int q) { return FN == 4 ? (q >> 1) & 7 : (q >> 2) & 3; }
 
 // EPI: the epilogue feature mask (halo_epilogue.h, specialised only; see wres_mask_ok); wave wm
 // owns rows wm·FM …, wn = 0, n0 = 0
-template <typename T, int EPI>
-__global__ __launch_bounds__(256, 1) void conv_wres_kernel(const ConvK k) {
-  typedef WresTile TL;
+template <typename T, typename TL, int EPI>
+__global__ __launch_bounds__(TL::NT, 1) void conv_wres_kernel(const ConvK k) {
   typedef typename Vec<T>::type VT;
   constexpr int FM = TL::FM, FN = TL::FN, HSIDE = TL::HSIDE, HROWS = TL::HROWS;
   constexpr int HPIECES = TL::HPIECES, HBUF = TL::HBUF, H_INS = TL::H_INS, NW = TL::NW;
+  constexpr int WM = TL::WM, CPP = TL::CPP;
   constexpr int VEC = 8;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -67,6 +79,7 @@ __global__ __launch_bounds__(256, 1) void conv_wres_kernel(const ConvK k) {
   const mia_conv_args& p = k.a;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid % WM, wn = wid / WM;
   const int frow = lane & 15, fq = lane >> 4;
   const int H = p.H, W = p.W;
   const int ptx = W / TL::PW, pty = H / TL::PH;
@@ -77,7 +90,7 @@ __global__ __launch_bounds__(256, 1) void conv_wres_kernel(const ConvK k) {
   const T* zero = (const T*)g_zero16;
 
   // weights → VGPRs: B fragment (tap t, K-chunk h, channel fragment j) = 8 input channels
-  // (h·4 + fq)·8 … of output channel 16·j + frow
+  // (h·4 + fq)·8 … of output channel 16·(FN·wn + j) + frow
   VT wreg[9][2][FN];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -85,7 +98,7 @@ __global__ __launch_bounds__(256, 1) void conv_wres_kernel(const ConvK k) {
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int j = 0; j < FN; ++j)
-        wreg[t][h][j] = *(const VT*)(Wt + (size_t)(16 * j + frow) * kpad + t * 64 +
+        wreg[t][h][j] = *(const VT*)(Wt + (size_t)(16 * (FN * wn + j) + frow) * kpad + t * 64 +
                                      (h * 4 + fq) * VEC);
 
   auto tile_pos = [&](int tile, int& n, int& y0, int& x0) {
@@ -118,9 +131,10 @@ __global__ __launch_bounds__(256, 1) void conv_wres_kernel(const ConvK k) {
     }
   };
 
-  // wave wid DMAs the epilogue operands of its 4 output rows (pieces of 8 pixels = 1 KB)
+  // wave wid DMAs the epilogue operands of its FM output rows × its channels (1 KB pieces of
+  // 64 / CPP pixels)
   char* const auxw = smem + 2 * HBUF + wid * (AUX::N * TL::AUXW);  // this wave's operand slots
-  // sdot / q / csum pre-reduction of the 4 waves (each covers all 64 channels of its rows)
+  // sdot / q / csum pre-reduction of the WM wave rows (each covers its channels of its rows)
   float* const red = k.prered ? (float*)(smem + 2 * HBUF + NW * AUX::N * TL::AUXW) : nullptr;
   auto issue_aux = [&](int n, int y0, int x0) {
     int ln = lane;
@@ -129,29 +143,34 @@ __global__ __launch_bounds__(256, 1) void conv_wres_kernel(const ConvK k) {
 #pragma unroll
     for (int t = 0; t < AUX::N; ++t)
 #pragma unroll
-      for (int j = 0; j < FM * 2; ++j) {
-        const int q = j * 8 + (ln >> 3);  // wave-local pixel: row q / 16, column q % 16
-        const int y = y0 + wid * FM + (q >> 4), x = x0 + (q & 15);
-        const T* src = srcs[t] + ((size_t)(n * H + y) * W + x) * 64 + ((ln & 7) ^ asw(q)) * VEC;
+      for (int j = 0; j < FM * CPP / 4; ++j) {
+        const int q = j * (64 / CPP) + ln / CPP;  // wave-local pixel: row q / 16, column q % 16
+        const int y = y0 + wm * FM + (q >> 4), x = x0 + (q & 15);
+        const T* src = srcs[t] + ((size_t)(n * H + y) * W + x) * 64 + 16 * FN * wn +
+                       ((ln % CPP) ^ asw<FN>(q)) * VEC;
         __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(auxw + t * TL::AUXW + j * 1024),
                                          16, 0, 0);
         __builtin_amdgcn_sched_barrier(0);  // one address live at a time (weights fill the VGPRs)
       }
   };
 
-  int tile = blockIdx.x;
-  if (tile < ntiles) issue_halo(tile, 0);
+  // a contiguous run of patches per block (neighbouring halos overlap: L2 hits on its XCD)
+  const int per = (ntiles + gridDim.x - 1) / gridDim.x;
+  const int t_end = min((int)blockIdx.x * per + per, ntiles);
+  const int t_step = 1;
+  int tile = blockIdx.x * per;
+  if (tile < t_end) issue_halo(tile, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int buf = 0;
-  for (; tile < ntiles; tile += gridDim.x) {
+  for (; tile < t_end; tile += t_step) {
     // every wave finished the previous patch (buffer buf^1 is free) and drained its DMA pieces
     // of this patch (buffer buf is complete)
     __syncthreads();
-    const int next = tile + gridDim.x;
+    const int next = tile + t_step;
     int n, y0, x0;
     tile_pos(tile, n, y0, x0);
     if constexpr (AUX::N > 0) issue_aux(n, y0, x0);  // land during this patch's MFMAs
-    if (next < ntiles) issue_halo(next, buf ^ 1);
+    if (next < t_end) issue_halo(next, buf ^ 1);
     const char* ha = smem + buf * HBUF;
     // opaque pixel-row lane index: the 36 swizzled A-fragment addresses (lane-dependent XOR, no
     // immediate-offset form) are recomputed inside the patch, not held across it
@@ -171,7 +190,7 @@ __global__ __launch_bounds__(256, 1) void conv_wres_kernel(const ConvK k) {
         VT af[FM];
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
-          const int hr = (wid * FM + i + dy) * HSIDE + fr + dx;
+          const int hr = (wm * FM + i + dy) * HSIDE + fr + dx;
           af[i] = *(const VT*)(ha + hr * ROWB + ((ch ^ fsw(hr)) << 4));
         }
 #pragma unroll
@@ -196,24 +215,25 @@ __global__ __launch_bounds__(256, 1) void conv_wres_kernel(const ConvK k) {
 #pragma unroll
           for (int j = 0; j < FN; ++j) {
             // channels 16j + 4·lrow … +3: chunk 2j + lrow/2, byte 8·(lrow & 1) within it
-            const int off = q * ROWB + (((2 * j + (lrow >> 1)) ^ asw(q)) << 4) + ((lrow & 1) << 3);
+            const int off =
+                q * (CPP * 16) + (((2 * j + (lrow >> 1)) ^ asw<FN>(q)) << 4) + ((lrow & 1) << 3);
             if constexpr (AUX::MASK) R.rma[i][j] = *(const R4*)(auxw + off);
             if constexpr (AUX::ACC) R.ryo[i][j] = *(const R4*)(auxw + off);
           }
         }
-        halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, 0, wid, 0, lane, -1, -1, &R, red, NW, 64);
+        halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, 0, wm, wn, lane, -1, -1, &R, red, WM, 64);
       }
     } else {
-      halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, 0, wid, 0, lane, -1, -1, nullptr, red, NW,
+      halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, 0, wm, wn, lane, -1, -1, nullptr, red, WM,
                                   64);
     }
     buf ^= 1;
   }
 }
 
-template <typename T, int EPI>
+template <typename T, typename TL, int EPI>
 static int launch_wres_(ConvK& k, int grid, size_t lds, hipStream_t st) {
-  auto fn = conv_wres_kernel<T, EPI>;
+  auto fn = conv_wres_kernel<T, TL, EPI>;
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -223,9 +243,9 @@ static int launch_wres_(ConvK& k, int grid, size_t lds, hipStream_t st) {
   }
   RedQ r;
   int rc = conv_red_begin(k, r,
-                          halo_red_slots(k.a.H, k.a.W, WresTile::FM, WresTile::NW, k.prered), st);
+                          halo_red_slots(k.a.H, k.a.W, TL::FM, TL::WM, k.prered), st);
   if (rc != MIA_OK) return rc;
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(WresTile::NT), lds, st, k);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(TL::NT), lds, st, k);
   rc = check_launch("conv_wres");
   return rc != MIA_OK ? rc : red_finish(r, st);
 }
@@ -255,8 +275,8 @@ bool conv_wres_eligible(const ConvK& k, int dtype) {
          a.act_in == MIA_ACT_NONE && G.kpad >= 9 * 64 && wres_mask_ok(epi_mask(k));
 }
 
-int launch_conv_wres(ConvK& k, int dtype, hipStream_t st) {
-  typedef WresTile TL;
+template <typename TL>
+static int launch_conv_wres_t(ConvK& k, int dtype, hipStream_t st) {
   static int ncu = 0;
   if (!ncu) {
     int dev = 0;
@@ -265,30 +285,35 @@ int launch_conv_wres(ConvK& k, int dtype, hipStream_t st) {
       ncu = 256;
   }
   const int ntiles = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW);
-  const int grid = std::min(ntiles, ncu);
+  const int per = (ntiles + ncu - 1) / ncu;
+  const int grid = (ntiles + per - 1) / per;  // contiguous runs: every block gets a non-empty one
   k.nbn = 1;
   k.nblk = ntiles;
   using namespace epi;
   const int f = epi_mask(k);
   const int naux = (f & TAP) ? 0 : ((f & MASK) ? 1 : 0) + ((f & ACC) ? 1 : 0);
-  const size_t lds = 2 * (size_t)TL::HBUF + (size_t)TL::NW * naux * TL::AUXW + 3 * TL::NW * 64 * 4;
+  const size_t lds = 2 * (size_t)TL::HBUF + (size_t)TL::NW * naux * TL::AUXW + 3 * TL::WM * 64 * 4;
   k.prered = prered_enabled() && (f & CSUM);
   MIA_DISPATCH_DTYPE(dtype, T, {
     if constexpr (sizeof(T) == 2) {
       switch (f) {
-        case BIAS | RELU: return launch_wres_<T, BIAS | RELU>(k, grid, lds, st);
-        case TAP | MASK: return launch_wres_<T, TAP | MASK>(k, grid, lds, st);
-        case 0: return launch_wres_<T, 0>(k, grid, lds, st);
-        case PRELU: return launch_wres_<T, PRELU>(k, grid, lds, st);
-        case BIAS | CSUM: return launch_wres_<T, BIAS | CSUM>(k, grid, lds, st);
-        case MASK | MSL: return launch_wres_<T, MASK | MSL>(k, grid, lds, st);
-        case ACC: return launch_wres_<T, ACC>(k, grid, lds, st);
-        case BIAS: return launch_wres_<T, BIAS>(k, grid, lds, st);  // e4e conv2 (SE body)
+        case BIAS | RELU: return launch_wres_<T, TL, BIAS | RELU>(k, grid, lds, st);
+        case TAP | MASK: return launch_wres_<T, TL, TAP | MASK>(k, grid, lds, st);
+        case 0: return launch_wres_<T, TL, 0>(k, grid, lds, st);
+        case PRELU: return launch_wres_<T, TL, PRELU>(k, grid, lds, st);
+        case BIAS | CSUM: return launch_wres_<T, TL, BIAS | CSUM>(k, grid, lds, st);
+        case MASK | MSL: return launch_wres_<T, TL, MASK | MSL>(k, grid, lds, st);
+        case ACC: return launch_wres_<T, TL, ACC>(k, grid, lds, st);
+        case BIAS: return launch_wres_<T, TL, BIAS>(k, grid, lds, st);  // e4e conv2 (SE body)
         default: break;
       }
     }
   });
   return set_error("conv_wres: no specialisation for this launch (see conv_wres_eligible)");
+}
+
+int launch_conv_wres(ConvK& k, int dtype, hipStream_t st) {
+  return launch_conv_wres_t<WresTile>(k, dtype, st);
 }
 
 

@@ -934,11 +934,12 @@ def test_generic_tile_register_epilogues_stride2(cuda, tune, dtype, C, mode):
 def test_conv2d_register_epilogue_paths(cuda, tune, dtype, N, H, W, C, mode, spec):
     """Stride-1 C→C 3×3 convs with every epilogue feature set of the attack step (vgg.py, e4e
     IR-SE50 body). spec=1: the specialised register epilogues — at C = 64 the weights-resident
-    persistent kernel (conv_wres.hip; 192² = 288 patches > one per CU exercises the persistent
-    loop and the halo prefetch), at C = 128 the halo kernel; spec=0: generic tile at 64
-    (MIA_CONV_WRES=0) and the runtime-feature halo epilogue at 128 (MIA_HALO_EPI=2)."""
+    persistent kernel (conv_wres.hip, 8 waves × 32 channels; 192² = 288 patches > one per CU
+    exercises the persistent run and the halo prefetch), at C = 128 the halo kernel; spec=0:
+    generic tile at 64 (MIA_CONV_WRES=0) and the runtime-feature halo epilogue at 128
+    (MIA_HALO_EPI=2)."""
     tune("MIA_CONV_WRES", spec)
-    tune("MIA_HALO_EPI", "1" if spec == "1" else "2")
+    tune("MIA_HALO_EPI", "2" if spec == "0" else "1")
     g = torch.Generator().manual_seed(N * 11 + H + W + C + len(mode))
     x = torch.randn(N, C, H, W, generator=g)
     w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)

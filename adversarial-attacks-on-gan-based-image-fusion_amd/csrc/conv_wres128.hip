@@ -64,10 +64,21 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   using namespace epi;
   constexpr int FM = TL::FM, NW = TL::NW, NS = TL::NS, HBUF = TL::HBUF, NPIECE = TL::NPIECE;
   constexpr int GB = TL::GB, P_INS = TL::P_INS;
-  constexpr bool FWD = EPI == (NOISE | BIAS | LRELU);
+  constexpr bool FWD = EPI == (NOISE | BIAS | LRELU);  // StyledConv forward, per-image weights
   constexpr bool DG = EPI == (OSC | SDOT | BAB);
-  static_assert(FWD || DG, "the StyledConv forward / input-gradient epilogues");
-  constexpr int SLOTB = TL::CHB + TL::NZB + (DG ? TL::AXB : 0);  // per-wave epilogue operands
+  // shared-weight launches with a plain per-element epilogue (halo_epilogue_f's operations in
+  // its order): VGG forward BIAS | RELU and input gradient MASK; e4e IR-SE body (128 channels)
+  // conv1 PRELU, conv2 BIAS, the input gradients MASK | MSL (PReLU') and ACC (identity shortcut)
+  constexpr bool GEN = EPI == (BIAS | RELU) || EPI == MASK || EPI == PRELU || EPI == BIAS ||
+                       EPI == (MASK | MSL) || EPI == ACC;
+  static_assert(FWD || DG || GEN, "the StyledConv / VGG / e4e epilogues");
+  constexpr bool G_BIAS = GEN && (EPI & BIAS), G_MASK = GEN && (EPI & MASK);
+  constexpr bool G_MSL = GEN && (EPI & MSL), G_ACC = GEN && (EPI & ACC);
+  constexpr bool G_RELU = GEN && ((EPI >> 8) & 3) == MIA_ACT_RELU;
+  constexpr bool G_PRELU = GEN && ((EPI >> 8) & 3) == MIA_ACT_PRELU;
+  constexpr bool NZ = FWD || DG;              // noise rows DMA'd per patch
+  constexpr bool AUXX = DG || G_MASK || G_ACC;  // a 16-channel per-pixel operand DMA'd per patch
+  constexpr int SLOTB = TL::CHB + TL::NZB + (AUXX ? TL::AXB : 0);  // per-wave epilogue operands
   // DG: the next halo's DMA pieces are issued one per (dx, s) fragment group inside the MFMA loop
   // (868 → 906 TFLOP/s); the forward keeps them at the patch start (1207 vs 1182 spread;
   // profiles/r05_layers_fp16_{spread,nospread}.txt)
@@ -116,10 +127,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   char* const slot = smem + 2 * HBUF + wid * SLOTB;
   float* const chl = (float*)slot;
   auto load_chan = [&](int n) {
-    f32x4 c0, c1 = {0.f, 0.f, 0.f, 0.f}, c2 = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (FWD) {
+    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f}, c2 = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (FWD || G_BIAS) {
       c0 = *(const f32x4*)(p.bias + cl);
-    } else {
+    } else if constexpr (G_PRELU) {
+      c0 = *(const f32x4*)(p.act_slope + cl);
+    } else if constexpr (G_MSL) {
+      c0 = *(const f32x4*)(p.mask_slope + cl);
+    } else if constexpr (DG) {
       c0 = *(const f32x4*)(p.out_scale + (size_t)n * k.cout_mod + cl);
       c1 = *(const f32x4*)(p.bab_demod + (size_t)n * Cout + cl);
       c2 = *(const f32x4*)(p.bab_bias ? p.bab_bias + cl : (const float*)zero);
@@ -165,12 +180,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   auto issue_aux = [&](int n, int y0, int x0) {
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const float* nzp = FWD ? p.noise : p.bab_noise;
-    const float* src = ln < 32 && nzp ? nzp + (size_t)(y0 + (ln >> 2)) * W + x0 + 4 * (ln & 3)
-                                      : (const float*)zero;
-    __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)aux, 16, 0, 0);
-    if constexpr (DG) {
-      const T* AX = (const T*)p.aux_x;
+    if constexpr (NZ) {
+      const float* nzp = FWD ? p.noise : p.bab_noise;
+      const float* src = ln < 32 && nzp ? nzp + (size_t)(y0 + (ln >> 2)) * W + x0 + 4 * (ln & 3)
+                                        : (const float*)zero;
+      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)aux, 16, 0, 0);
+    }
+    if constexpr (AUXX) {  // DG: the stored activation aux_x; MASK: the mask operand; ACC: old y
+      const T* AX = (const T*)(DG ? p.aux_x : (G_MASK ? p.mask_a : p.y));
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int q = j * 32 + (ln >> 1), c = (ln & 1) ^ ((q >> 3) & 1);
@@ -263,10 +280,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     asm volatile("" ::: "memory");
     const int px = lane & 15, lrow = lane >> 4;
     const float* nz = (const float*)aux;
-    const float nzw = FWD ? p.noise_w : p.bab_noise_w;
+    const float nzw = FWD ? p.noise_w : (DG ? p.bab_noise_w : 0.f);
     // (DG: the per-channel constants are re-read from LDS per row pair below — held across the
     // epilogue they pushed the kernel past 256 VGPRs)
-    const f32x4 c0 = FWD ? *(const f32x4*)(chl + cl - cw0) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 c0 = FWD || GEN ? *(const f32x4*)(chl + cl - cw0) : f32x4{0.f, 0.f, 0.f, 0.f};
     float part[4] = {0.f, 0.f, 0.f, 0.f}, partq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < FM; i += 2) {
@@ -274,8 +291,25 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       float vo[2][4];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const float z = nzw * nz[(i + u) * 16 + px];
-        if constexpr (FWD) {
+        const float z = NZ ? nzw * nz[(i + u) * 16 + px] : 0.f;
+        typedef T t4 __attribute__((ext_vector_type(4)));
+        const int q = (i + u) * 16 + px;
+        if constexpr (GEN) {
+          t4 ar = {};
+          if constexpr (AUXX)
+            ar = *(const t4*)(aux + TL::NZB + q * 32 + ((((lrow >> 1) ^ (q >> 3)) & 1) << 4) +
+                              ((lrow & 1) << 3));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float v = acc[i + u][e];
+            if constexpr (G_BIAS) v += c0[e];
+            if constexpr (G_MASK) v = (float)ar[e] > 0.f ? v : (G_MSL ? c0[e] * v : 0.f);
+            if constexpr (G_RELU) v = v > 0.f ? v : 0.f;
+            if constexpr (G_PRELU) v = v > 0.f ? v : c0[e] * v;
+            if constexpr (G_ACC) v += (float)ar[e];
+            vo[u][e] = v;
+          }
+        } else if constexpr (FWD) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             float v = acc[i + u][e];
@@ -287,8 +321,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
           const f32x4 c0 = *(const f32x4*)(chl + cl - cw0);
           const f32x4 c1 = *(const f32x4*)(chl + 16 + cl - cw0);
           const f32x4 c2 = *(const f32x4*)(chl + 32 + cl - cw0);
-          const int q = (i + u) * 16 + px;
-          typedef T t4 __attribute__((ext_vector_type(4)));
           const t4 xr = *(const t4*)(aux + TL::NZB + q * 32 +
                                      ((((lrow >> 1) ^ (q >> 3)) & 1) << 4) + ((lrow & 1) << 3));
 #pragma unroll
@@ -333,11 +365,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         }
       }
     }
-    if (more) {
-      if (n1 != wimg) {  // block-uniform: the run reaches the next image. Its weights (per-image
-        if constexpr (FWD) load_w(n1);  // matrices) and constants are loaded and waited for here, so no
-        load_chan(n1);         // wait for them (which would also wait for the next halo, in
-        wimg = n1;             // flight behind them) lands in the next patch's MFMAs
+    // block-uniform: the run reaches the next image. Its weights (per-image matrices) and
+    // constants are loaded and waited for here, so no wait for them (which would also wait for
+    // the next halo, in flight behind them) lands in the next patch's MFMAs. (The VGG launches
+    // share their weights and bias over the images.)
+    if constexpr (FWD || DG) {
+      if (more && n1 != wimg) {
+        if constexpr (FWD) load_w(n1);
+        load_chan(n1);
+        wimg = n1;
         __builtin_amdgcn_s_waitcnt(0x0f70);
       }
     }
@@ -348,8 +384,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 template <typename T, int CIN, int EPI>
 static int launch_wres128_(ConvK& k, hipStream_t st) {
   typedef Wres128Tile<CIN> TL;
+  constexpr bool AUXX = (EPI & (epi::SDOT | epi::MASK | epi::ACC)) != 0;
   constexpr bool DG = (EPI & epi::SDOT) != 0;
-  constexpr int LDS = 2 * TL::HBUF + TL::NW * (TL::CHB + TL::NZB + (DG ? TL::AXB : 0));
+  constexpr int LDS = 2 * TL::HBUF + TL::NW * (TL::CHB + TL::NZB + (AUXX ? TL::AXB : 0));
   static_assert(LDS <= 160 * 1024, "LDS budget");
   auto fn = conv_wres128_kernel<T, CIN, EPI>;
   static int ncu = 0;
@@ -394,7 +431,15 @@ bool conv_wres128_eligible(const ConvK& k, int dtype) {
   const int f = epi_mask(k);
   if (f == (NOISE | BIAS | LRELU)) return a.noise && a.bias && k.wn > 0;
   if (f == (OSC | SDOT | BAB)) return k.wn == 0 && k.cout_mod == a.Cout;
-  return false;
+  if (k.wn != 0) return false;
+  switch (f) {
+    case BIAS | RELU: case BIAS: return a.bias != nullptr;     // VGG conv2_2 / e4e conv2 forward
+    case PRELU: return a.act_slope != nullptr;                 // e4e conv1 forward
+    case MASK: return a.mask_a != nullptr;                     // VGG input gradient (ReLU mask)
+    case MASK | MSL: return a.mask_a && a.mask_slope;          // e4e conv2 input gradient
+    case ACC: return true;                                     // e4e conv1 input gradient
+    default: return false;
+  }
 }
 
 int launch_conv_wres128(ConvK& k, int dtype, hipStream_t st) {
@@ -404,6 +449,15 @@ int launch_conv_wres128(ConvK& k, int dtype, hipStream_t st) {
     if constexpr (sizeof(T) == 2) {
       if (f == (NOISE | BIAS | LRELU)) return launch_wres128_<T, 128, NOISE | BIAS | LRELU>(k, st);
       if (f == (OSC | SDOT | BAB)) return launch_wres128_<T, 128, OSC | SDOT | BAB>(k, st);
+      switch (f) {
+        case BIAS | RELU: return launch_wres128_<T, 128, BIAS | RELU>(k, st);
+        case BIAS: return launch_wres128_<T, 128, BIAS>(k, st);
+        case PRELU: return launch_wres128_<T, 128, PRELU>(k, st);
+        case MASK: return launch_wres128_<T, 128, MASK>(k, st);
+        case MASK | MSL: return launch_wres128_<T, 128, MASK | MSL>(k, st);
+        case ACC: return launch_wres128_<T, 128, ACC>(k, st);
+        default: break;
+      }
     }
   });
   return set_error("conv_wres128: no specialisation for this launch");

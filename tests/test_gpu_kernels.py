@@ -1483,3 +1483,58 @@ def test_upconv_x6_two_block_form_bitwise(cuda, tune, R, cin, cout):
     xin = F.leaky_relu(x.double(), 0.2) * math.sqrt(2) * s.double().view(N, cin, 1, 1)
     ref = F.conv_transpose2d(xin, w.double().transpose(0, 1), stride=2)
     assert rel_err(nchw(t1), ref) < 3 * TOL[torch.float32]
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,R,W", [(6, 128, 128), (3, 40, 48)])
+@pytest.mark.parametrize("mode", ["bias_relu", "mask", "prelu", "bias", "mask_slope", "acc"])
+def test_wres128_shared_weight_epilogues(cuda, tune, dtype, N, R, W, mode):
+    """The weights-resident 128-channel kernel on the shared-weight launches: VGG conv2_2
+    forward (bias + ReLU) and input gradient (ReLU mask); the e4e IR-SE body at 128 channels,
+    conv1 (PReLU), conv2 (bias), the conv2 input gradient (PReLU' mask with slope) and the conv1
+    input gradient accumulated onto the identity shortcut's; against torch fp64 and against the
+    halo tile (MIA_CONV_WRES128=0; both accumulate in fp32, in different orders)."""
+    C = 128
+    g = torch.Generator().manual_seed(N * 7 + R + W + len(mode))
+    x = torch.randn(N, C, R, W, generator=g)
+    w = torch.randn(C, C, 3, 3, generator=g) / math.sqrt(9 * C)
+    xq, wq = x.to(dtype).double(), w.to(dtype).double()
+    wf = layouts.fwd_matrix(w, dtype).to(cuda)
+    grp = [dict(w=wf, kh=3, kw=3, pad=(1, 1), ho=R, wo=W)]
+    conv = F.conv2d(xq, wq, padding=1)
+    slope = torch.rand(C, generator=g) * 0.5 + 0.05
+    sl = slope.double().view(1, C, 1, 1)
+    y0 = torch.randn(N, C, R, W, generator=g)
+    b = torch.randn(C, generator=g) * 0.1
+    m = torch.randn(N, C, R, W, generator=g)
+    if mode == "bias_relu":
+        ref = F.relu(conv + b.double().view(1, C, 1, 1))
+        kw = dict(bias=b.to(cuda), act_out=ops.ACT_RELU)
+    elif mode == "mask":
+        ref = conv * (m.to(dtype).double() > 0)
+        kw = dict(mask_a=nhwc(m, dtype).to(cuda))
+    elif mode == "prelu":
+        ref = torch.where(conv > 0, conv, sl * conv)
+        kw = dict(act_out=ops.ACT_PRELU, act_slope=slope.to(cuda))
+    elif mode == "bias":
+        ref = conv + b.double().view(1, C, 1, 1)
+        kw = dict(bias=b.to(cuda))
+    elif mode == "mask_slope":
+        ref = torch.where(m.to(dtype).double() > 0, conv, sl * conv)
+        kw = dict(mask_a=nhwc(m, dtype).to(cuda), mask_slope=slope.to(cuda))
+    else:
+        ref = conv + y0.to(dtype).double()
+        kw = dict(accumulate=True)
+    xd = nhwc(x, dtype).to(cuda)
+    y = nhwc(y0, dtype).to(cuda)
+    ops.conv2d(xd, grp, y, (R, W), cout=C, **kw)
+    tune("MIA_CONV_WRES128", 0)
+    y_halo = nhwc(y0, dtype).to(cuda)
+    if R % 16 == 0:
+        ops.conv2d(xd, grp, y_halo, (R, W), cout=C, **kw)
+    torch.cuda.synchronize()
+    e = rel_err(nchw(y), ref)
+    print(f"wres128 shared-weight {mode} {dtype} {N}x{R}x{W}: rel err vs fp64 {e:.2e}")
+    assert e < 2 * TOL[dtype]
+    if R % 16 == 0:
+        assert rel_err(nchw(y), nchw(y_halo).double()) < 2 * TOL[dtype]

@@ -278,12 +278,18 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // LDS reads of the DMA'd operands below the wait
     __builtin_amdgcn_s_waitcnt(0x0f70);
     asm volatile("" ::: "memory");
-    const int px = lane & 15, lrow = lane >> 4;
+    // lane terms of the epilogue from an opaque copy of the lane id: held across the patch loop
+    // (8 aux row offsets + the channel slot) they were spilled, and each scratch reload's
+    // vmcnt(0) then waited for the epilogue's own stores (DG 2849 µs vs 2069 without its math)
+    int ln_e = lane;
+    asm volatile("" : "+v"(ln_e));
+    const int px = ln_e & 15, lrow = ln_e >> 4;
+    const int cle = (lrow << 2);  // this lane's channel quad within the wave's 16
     const float* nz = (const float*)aux;
     const float nzw = FWD ? p.noise_w : (DG ? p.bab_noise_w : 0.f);
     // (DG: the per-channel constants are re-read from LDS per row pair below — held across the
     // epilogue they pushed the kernel past 256 VGPRs)
-    const f32x4 c0 = FWD || GEN ? *(const f32x4*)(chl + cl - cw0) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 c0 = FWD || GEN ? *(const f32x4*)(chl + cle) : f32x4{0.f, 0.f, 0.f, 0.f};
     float part[4] = {0.f, 0.f, 0.f, 0.f}, partq[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < FM; i += 2) {
@@ -318,9 +324,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
             vo[u][e] = lrelu_s2(v);
           }
         } else {
-          const f32x4 c0 = *(const f32x4*)(chl + cl - cw0);
-          const f32x4 c1 = *(const f32x4*)(chl + 16 + cl - cw0);
-          const f32x4 c2 = *(const f32x4*)(chl + 32 + cl - cw0);
+          const f32x4 c0 = *(const f32x4*)(chl + cle);
+          const f32x4 c1 = *(const f32x4*)(chl + 16 + cle);
+          const f32x4 c2 = *(const f32x4*)(chl + 32 + cle);
           const t4 xr = *(const t4*)(aux + TL::NZB + q * 32 +
                                      ((((lrow >> 1) ^ (q >> 3)) & 1) << 4) + ((lrow & 1) << 3));
 #pragma unroll
@@ -360,8 +366,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       for (int e = 0; e < 4; ++e) {
         const float a = row16_sum(part[e]), b = row16_sum(partq[e]);
         if (px == 0) {
-          red_put(k, 0, slt, n * Cout + cl + e, a);
-          red_put(k, 1, slt, n * Cout + cl + e, b);
+          red_put(k, 0, slt, n * Cout + cw0 + cle + e, a);
+          red_put(k, 1, slt, n * Cout + cw0 + cle + e, b);
         }
       }
     }

@@ -31,6 +31,16 @@
 #include "conv_common.h"
 #include "halo_epilogue.h"
 
+// fragment reads issued this many fragments ahead of their MFMAs, as inline asm with counted
+// waits (tuning build flags; round 5: PF 3 asm vs 1 compiler-scheduled: 256² forward 2135 -> 2072,
+// input gradient 2404 -> 2366, VGG 128² 464 -> 455 µs, profiles/r05_layers_fp16_wres128_pf.txt)
+#ifndef MIA_WRES128_PF
+#define MIA_WRES128_PF 3
+#endif
+#ifndef MIA_WRES128_ASMREAD
+#define MIA_WRES128_ASMREAD 1
+#endif
+
 namespace mia {
 
 template <int CIN>
@@ -245,18 +255,49 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // the 120 fragment reads in (dx, s, q) order, each feeding the taps dy = 0, 1, 2 of output
     // row q − dy; the next read is issued before the current fragment's MFMAs
     const char* hd[3] = {hb + offa[0], hb + offa[1], hb + offa[2]};
-    VT cur = *(const VT*)hd[0];
+    // fragment f = (dx·NS + s)·(FM + 2) + q, read PF fragments ahead into a ring of PF + 1
+    constexpr int NQ = FM + 2, NF = 3 * NS * NQ, PF = MIA_WRES128_PF;
+#if MIA_WRES128_ASMREAD
+    // the reads as inline asm with explicit counted waits (the compiler's own waits were
+    // lgkmcnt(0) right after the next read's issue, exposing the LDS latency every few MFMAs).
+    // Safe beside the compiler's own LDS waits: an unknown younger read only makes them stricter;
+    // the MFMA loop issues no other LDS operation between a read and its wait.
+    unsigned hl[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) hl[d] = (unsigned)(size_t)(lptr_t)(hd[d]);
+    auto frag = [&](int f) {
+      const int dxf = f / (NS * NQ), rf = f % (NS * NQ);
+      VT v;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(hl[dxf] + (rf % NQ) * 5 * GB + (rf / NQ) * 256));
+      return v;
+    };
+#else
+    auto frag = [&](int f) {
+      const int dxf = f / (NS * NQ), rf = f % (NS * NQ);
+      return *(const VT*)(hd[dxf] + (rf % NQ) * 5 * GB + (rf / NQ) * 256);
+    };
+#endif
+    VT ring[PF + 1];
+#pragma unroll
+    for (int f = 0; f < PF; ++f) ring[f] = frag(f);
 #pragma unroll
     for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
       for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int q = 0; q < FM + 2; ++q) {
-          int q2 = q + 1, s2 = s, dx2 = dx;
-          if (q2 == FM + 2) { q2 = 0; ++s2; }
-          if (s2 == NS) { s2 = 0; ++dx2; }
-          VT nxt = cur;
-          if (dx2 < 3) nxt = *(const VT*)(hd[dx2] + q2 * 5 * GB + s2 * 256);
+        for (int q = 0; q < NQ; ++q) {
+          const int f = (dx * NS + s) * NQ + q;
+          if (f + PF < NF) ring[(f + PF) % (PF + 1)] = frag(f + PF);
+          VT cur = ring[f % (PF + 1)];
+#if MIA_WRES128_ASMREAD
+          {  // fragment f landed: at most the reads issued after it (f+1 … f+PF) outstanding
+            const int younger = NF - 1 - f < PF ? NF - 1 - f : PF;
+            if (younger >= 3) asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(cur));
+            else if (younger == 2) asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(cur));
+            else if (younger == 1) asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(cur));
+            else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur));
+          }
+#endif
 #pragma unroll
           for (int dy = 0; dy < 3; ++dy) {
             const int i = q - dy;
@@ -271,7 +312,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
               __builtin_amdgcn_sched_barrier(0);
             }
           }
-          cur = nxt;
         }
     // the next patch's halo and this patch's operands were issued during its MFMAs: drain them
     // before the epilogue's stores (vmcnt retires in order); the empty asm keeps the epilogue's

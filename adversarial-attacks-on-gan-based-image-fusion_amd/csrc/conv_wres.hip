@@ -44,17 +44,16 @@ struct WresTileT {
 // two waves per SIMD, each 32 channels (144 weight VGPRs)
 typedef WresTileT<8, 2> WresTile;
 
-// Per-pixel epilogue operand prefetched into LDS (a wave's 64 pixels × 64 channels): MASK →
-// mask_a, ACC → old y. Register prefetch spills next to the 288 resident weight VGPRs; LDS-DMA
-// costs no registers. The tap pair (TAP | MASK, VGG dgrad) still loads in the epilogue: with two
-// operands the epilogue's extra live registers spill the weights (measured in the ISA: reloads
-// with vmcnt(0) inside the MFMA loop).
+// Per-pixel epilogue operands prefetched into LDS (a wave's 64 pixels × its 32 channels): MASK →
+// mask_a, ACC → old y, TAP | MASK → the tap pair (tap_a, also the ReLU mask, and tap_t). LDS-DMA
+// costs no registers (a register prefetch spilled next to the resident weights).
 template <int EPI>
 struct WresAux {
   static constexpr bool TAP = EPI & epi::TAP, MASK = (EPI & epi::MASK) && !TAP;
   static constexpr bool ACC = EPI & epi::ACC;
-  static constexpr int N = TAP ? 0 : (MASK ? 1 : 0) + (ACC ? 1 : 0);
-  static_assert(N <= 1, "one prefetched operand per wave");
+  // TAP: the tap pair (tap_a, which is also the mask: conv_wres_eligible, and tap_t)
+  static constexpr int N = TAP ? 2 : (MASK ? 1 : 0) + (ACC ? 1 : 0);
+  static_assert(N <= 2 && (TAP || N <= 1), "prefetched operands per wave");
   static_assert(!(EPI & (epi::SDOT | epi::BAB | epi::NOISE)), "not a weights-resident epilogue");
 };
 
@@ -139,7 +138,8 @@ __global__ __launch_bounds__(TL::NT, 1) void conv_wres_kernel(const ConvK k) {
   auto issue_aux = [&](int n, int y0, int x0) {
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const T* srcs[1] = {AUX::MASK ? (const T*)p.mask_a : (const T*)p.y};
+    const T* srcs[2] = {AUX::TAP ? (const T*)p.tap_a : (AUX::MASK ? (const T*)p.mask_a : (const T*)p.y),
+                        (const T*)p.tap_t};
 #pragma unroll
     for (int t = 0; t < AUX::N; ++t)
 #pragma unroll
@@ -219,6 +219,10 @@ __global__ __launch_bounds__(TL::NT, 1) void conv_wres_kernel(const ConvK k) {
                 q * (CPP * 16) + (((2 * j + (lrow >> 1)) ^ asw<FN>(q)) << 4) + ((lrow & 1) << 3);
             if constexpr (AUX::MASK) R.rma[i][j] = *(const R4*)(auxw + off);
             if constexpr (AUX::ACC) R.ryo[i][j] = *(const R4*)(auxw + off);
+            if constexpr (AUX::TAP) {
+              R.rta[i][j] = *(const R4*)(auxw + off);
+              R.rtt[i][j] = *(const R4*)(auxw + TL::AUXW + off);
+            }
           }
         }
         halo_epilogue_f<T, TL, EPI>(k, acc, n, y0, x0, 0, wm, wn, lane, -1, -1, &R, red, WM, 64);
@@ -272,7 +276,8 @@ bool conv_wres_eligible(const ConvK& k, int dtype) {
          G.pad_y == 1 && G.pad_x == 1 && G.ho == a.H && G.wo == a.W && G.ay == 1 && G.ax == 1 &&
          G.by == 0 && G.bx == 0 && !a.shuffle_out && a.H % 16 == 0 && a.W % 16 == 0 &&
          a.Cin == 64 && a.Cout == 64 && k.HT == a.H && k.WT == a.W && !a.in_scale &&
-         a.act_in == MIA_ACT_NONE && G.kpad >= 9 * 64 && wres_mask_ok(epi_mask(k));
+         a.act_in == MIA_ACT_NONE && G.kpad >= 9 * 64 && wres_mask_ok(epi_mask(k)) &&
+         (!a.tap_a || a.mask_a == a.tap_a);
 }
 
 template <typename TL>
@@ -291,7 +296,7 @@ static int launch_conv_wres_t(ConvK& k, int dtype, hipStream_t st) {
   k.nblk = ntiles;
   using namespace epi;
   const int f = epi_mask(k);
-  const int naux = (f & TAP) ? 0 : ((f & MASK) ? 1 : 0) + ((f & ACC) ? 1 : 0);
+  const int naux = (f & TAP) ? 2 : ((f & MASK) ? 1 : 0) + ((f & ACC) ? 1 : 0);
   const size_t lds = 2 * (size_t)TL::HBUF + (size_t)TL::NW * naux * TL::AUXW + 3 * TL::WM * 64 * 4;
   k.prered = prered_enabled() && (f & CSUM);
   MIA_DISPATCH_DTYPE(dtype, T, {

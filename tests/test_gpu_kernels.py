@@ -218,7 +218,8 @@ def test_modconv_fwd_per_image_weights(cuda, dtype, N, cin, cout, R):
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("N,R,W,C", [(20, 64, 64, 128), (3, 256, 256, 128), (5, 40, 48, 128)])
+@pytest.mark.parametrize("N,R,W,C", [(20, 64, 64, 128), (3, 256, 256, 128), (5, 40, 48, 128),
+                                     (1, 8, 16, 128), (2, 16, 32, 128)])
 def test_wres128_modconv_fwd(cuda, tune, dtype, N, R, W, C):
     """The weights-resident StyledConv forward (conv_wres128.hip: 128 → 128, the 256² layer of the
     fp16 / bf16 synthesis) on per-image weights: persistent runs that cross image boundaries
@@ -272,7 +273,8 @@ def test_wres128_modconv_fwd(cuda, tune, dtype, N, R, W, C):
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 @pytest.mark.parametrize("N,R,W,with_noise", [(20, 64, 64, True), (2, 256, 256, True),
-                                               (3, 40, 48, False)])
+                                               (3, 40, 48, False), (1, 8, 16, True),
+                                               (2, 16, 16, False)])
 def test_wres128_dgrad_sdot_bab(cuda, tune, dtype, N, R, W, with_noise):
     """The weights-resident kernel's StyledConv input gradient (OSC | SDOT | BAB: the 256² block's
     dgrad with the style-gradient dot and the fused backward front of the layer below) against
@@ -1486,7 +1488,7 @@ def test_upconv_x6_two_block_form_bitwise(cuda, tune, R, cin, cout):
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("N,R,W", [(6, 128, 128), (3, 40, 48)])
+@pytest.mark.parametrize("N,R,W", [(6, 128, 128), (3, 40, 48), (1, 8, 16)])
 @pytest.mark.parametrize("mode", ["bias_relu", "mask", "prelu", "bias", "mask_slope", "acc"])
 def test_wres128_shared_weight_epilogues(cuda, tune, dtype, N, R, W, mode):
     """The weights-resident 128-channel kernel on the shared-weight launches: VGG conv2_2

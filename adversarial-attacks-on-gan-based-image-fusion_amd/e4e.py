@@ -50,9 +50,12 @@ BATCH_MAX = 16  # groups per mia_conv2d_batched launch
 # c3 heads (16² → 8², 256 tiles per head) 15.9 → 12.4 ms per step merged, the p2 heads (1024
 # tiles) 63.5 → 63.5, the p1 heads (4096 tiles) 461.7 → 476.4 (the merged launch's 28 column
 # tiles per row tile cycle 99 MB of pre-split weights through L2). 0 = never (A/B:
-# MIA_E4E_MERGE_HEADS).
+# MIA_E4E_MERGE_HEADS). fp16 / bf16 (round 5, profiles/r05_layers_fp16_merge_ab.txt): the p2
+# heads merged 18.7 → 15.2 ms per step, the p1 heads 112.0 → 111.5 (neutral): the 2-byte types
+# merge below 2048 tiles (p2 and c3).
 MERGE_HEADS = int(__import__("os").environ.get("MIA_E4E_MERGE_HEADS", "1"))
 MERGE_BELOW_TILES = 1024
+MERGE_BELOW_TILES_2B = 2048
 
 
 def _bn_fold(p, pre):
@@ -345,7 +348,8 @@ class E4EEncoder:
         # stacked level buffer, then one batched launch per resolution level
         merged = set()
         for src, (idx, k0, r) in self.src_fwd.items():
-            if -(-N * r * r // 128) * (STYLE_DIM // 128) >= MERGE_BELOW_TILES:
+            lim = MERGE_BELOW_TILES if self.dtype == torch.float32 else MERGE_BELOW_TILES_2B
+            if -(-N * r * r // 128) * (STYLE_DIM // 128) >= lim:
                 continue  # enough tiles per head: one launch per head
             merged.update(idx)
             if src not in self._src_cat:

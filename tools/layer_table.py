@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16", "fp32"])
     a = ap.parse_args()
+    if os.environ.get("E4E_MERGE_BELOW_TILES"):  # A/B of the merged first head convs (e4e.py)
+        import gfa_amd.e4e as e4e_mod
+        e4e_mod.MERGE_BELOW_TILES = int(os.environ["E4E_MERGE_BELOW_TILES"])
     dev = torch.device("cuda:0")
     T, S, B = bench.DT[a.dtype], a.size, a.batch
     enc = E4EEncoder(bench.encoder_weights("e4e", S), S, dtype=T, device=dev)

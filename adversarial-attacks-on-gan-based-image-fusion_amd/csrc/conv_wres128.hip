@@ -55,8 +55,8 @@ struct Wres128Tile {
   static constexpr int NZB = 1024;                      // per wave: the patch's noise rows
   static constexpr int AXB = FM * 16 * 32;              // per wave: 16 channels of aux_x (4 KB)
   static constexpr int CHB = 256;                       // per wave: 3 × 16 per-channel constants
-  static_assert(CIN == 128, "one DMA piece = one 4-pixel group (GB = 1 KB)");
-  static_assert(HBUF % 1024 == 0 && GB == 1024, "halo layout");
+  // a 1-KB DMA piece = 1024 / GB 4-pixel groups (Cin 128: one, Cin 64: two)
+  static_assert((CIN == 128 || CIN == 64) && HBUF % 1024 == 0, "halo layout");
 };
 
 __device__ __forceinline__ int sw128(int v) { return (v >> 1) & 3; }
@@ -165,10 +165,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // id, so the per-piece lane terms are recomputed per patch instead of hoisted (they spilled)
     int ln = lane;
     asm volatile("" : "+v"(ln));
-    const int ls = ln >> 4, lpp = (ln >> 2) & 3, lcs = ln & 3;
-    const int hy = pc / 5, c5 = pc - 5 * hy;
+    // LDS byte 16·lane of the piece: group gi, sub-plane ls, pixel lpp of the group, chunk lcs
+    constexpr int GPP = 1024 / GB;  // groups per piece
+    const int gi = (ln * 16) / GB, lb = (ln * 16) % GB;
+    const int ls = lb >> 8, lpp = (lb >> 6) & 3, lcs = (lb >> 4) & 3;
+    const int hp = (pc * GPP + gi) * 4 + lpp;  // padded halo pixel (rows of HS)
+    const int hy = hp / TL::HS, hx = hp - TL::HS * hy;
     const int y = y0 + hy - 1;
-    const int hx = 4 * c5 + lpp;
     const int x = x0 + hx - 1;
     const bool ok = y >= 0 && y < H && hx < TL::PW + 2 && x >= 0 && x < W;
     const int yc = ok ? y : 0, xc = ok ? x : 0;
@@ -458,9 +461,10 @@ static int launch_wres128_(ConvK& k, hipStream_t st) {
 }
 
 // Eligible: 2-byte type, Cin 128 → Cout 128, one group, stride 1, 3×3 pad 1, identity placement,
-// H % 8 == 0, W % 16 == 0, dense output rows, and either the StyledConv forward epilogue on
-// per-image weights (noise, bias, leaky ReLU; mia_conv3x3_wmod) or the StyledConv input gradient
-// with the style dot and the fused backward front (OSC | SDOT | BAB, shared weights).
+// H % 8 == 0, W % 16 == 0, dense output rows, and the StyledConv forward epilogue on per-image
+// weights (noise, bias, leaky ReLU; mia_conv3x3_wmod), the StyledConv input gradient with the
+// style dot and the fused backward front (OSC | SDOT | BAB, shared weights) or a shared-weight
+// plain epilogue (GEN); Cin 64 → Cout 128 for the forward BIAS | RELU and PRELU launches.
 // T_CONV_WRES128 = 0 disables.
 bool conv_wres128_eligible(const ConvK& k, int dtype) {
   if (tune(T_CONV_WRES128) == 0) return false;
@@ -470,11 +474,13 @@ bool conv_wres128_eligible(const ConvK& k, int dtype) {
   if (dtype == MIA_F32 || k.ng != 1 || k.stride != 1 || G.kh != 3 || G.kw != 3 ||
       G.pad_y != 1 || G.pad_x != 1 || G.ho != a.H || G.wo != a.W || G.ay != 1 || G.ax != 1 ||
       G.by != 0 || G.bx != 0 || a.shuffle_out || a.H % 8 != 0 || a.W % 16 != 0 ||
-      a.Cin != 128 || a.Cout != 128 || k.HT != a.H || k.WT != a.W || a.in_scale ||
-      a.act_in != MIA_ACT_NONE || G.kpad < 9 * 128 || !a.y || k.ystride != a.Cout ||
-      k.ysplit > 0)
+      (a.Cin != 128 && a.Cin != 64) || a.Cout != 128 || k.HT != a.H || k.WT != a.W ||
+      a.in_scale || a.act_in != MIA_ACT_NONE || G.kpad < 9 * a.Cin || !a.y ||
+      k.ystride != a.Cout || k.ysplit > 0)
     return false;
   const int f = epi_mask(k);
+  if (a.Cin == 64)  // (the 64 → 128 launches: VGG conv2_1 forward, the e4e stage-2 conv1)
+    return k.wn == 0 && ((f == (BIAS | RELU) && a.bias) || (f == PRELU && a.act_slope));
   if (f == (NOISE | BIAS | LRELU)) return a.noise && a.bias && k.wn > 0;
   if (f == (OSC | SDOT | BAB)) return k.wn == 0 && k.cout_mod == a.Cout;
   if (k.wn != 0) return false;
@@ -493,6 +499,11 @@ int launch_conv_wres128(ConvK& k, int dtype, hipStream_t st) {
   const int f = epi_mask(k);
   MIA_DISPATCH_DTYPE(dtype, T, {
     if constexpr (sizeof(T) == 2) {
+      if (k.a.Cin == 64) {
+        if (f == (BIAS | RELU)) return launch_wres128_<T, 64, BIAS | RELU>(k, st);
+        if (f == PRELU) return launch_wres128_<T, 64, PRELU>(k, st);
+        return set_error("conv_wres128: no Cin = 64 specialisation for this launch");
+      }
       if (f == (NOISE | BIAS | LRELU)) return launch_wres128_<T, 128, NOISE | BIAS | LRELU>(k, st);
       if (f == (OSC | SDOT | BAB)) return launch_wres128_<T, 128, OSC | SDOT | BAB>(k, st);
       switch (f) {

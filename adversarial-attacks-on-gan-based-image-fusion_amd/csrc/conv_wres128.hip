@@ -43,9 +43,12 @@
 
 namespace mia {
 
-template <int CIN>
+template <int CIN, int COUT = 128>
 struct Wres128Tile {
-  static constexpr int FM = 8, NW = 8, NT = 512, PH = 8, PW = 16, BN = 16 * NW;  // 128
+  // wave (row group wid / WNC, channel group wid % WNC): FM patch rows × 16 output channels
+  static constexpr int NW = 8, NT = 512, PH = 8, PW = 16, BN = COUT;
+  static constexpr int WNC = COUT / 16, WMR = NW / WNC, FM = PH / WMR;
+  static_assert((COUT == 128 || COUT == 64) && WMR * WNC == NW, "8 waves of 16 channels");
   static constexpr int HS = 20, HROWS = (PH + 2) * HS;  // 200 halo pixels
   static constexpr int PB = 2 * CIN, GB = 4 * PB;       // bytes per pixel / per 4-pixel group
   static constexpr int NS = CIN / 32;                   // K-chunks (32-channel sub-planes) per tap
@@ -67,9 +70,9 @@ __device__ __forceinline__ int sw128(int v) { return (v >> 1) & 3; }
 //   OSC | SDOT | BAB — the StyledConv input gradient of the 256² block with the style-gradient dot
 //     (sdot) and the fused backward front of the layer below (bab: its lrelu', demod scale and the
 //     q sum), on the shared dgrad matrix (k.wn = 0).
-template <typename T, int CIN, int EPI>
+template <typename T, int CIN, int EPI, int COUT = 128>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) void conv_wres128_kernel(const ConvK k) {
-  typedef Wres128Tile<CIN> TL;
+  typedef Wres128Tile<CIN, COUT> TL;
   typedef typename Vec<T>::type VT;
   using namespace epi;
   constexpr int FM = TL::FM, NW = TL::NW, NS = TL::NS, HBUF = TL::HBUF, NPIECE = TL::NPIECE;
@@ -79,8 +82,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // shared-weight launches with a plain per-element epilogue (halo_epilogue_f's operations in
   // its order): VGG forward BIAS | RELU and input gradient MASK; e4e IR-SE body (128 channels)
   // conv1 PRELU, conv2 BIAS, the input gradients MASK | MSL (PReLU') and ACC (identity shortcut)
-  constexpr bool GEN = EPI == (BIAS | RELU) || EPI == MASK || EPI == PRELU || EPI == BIAS ||
-                       EPI == (MASK | MSL) || EPI == ACC;
+  constexpr bool GEN = EPI == 0 || EPI == (BIAS | RELU) || EPI == MASK || EPI == PRELU ||
+                       EPI == BIAS || EPI == (MASK | MSL) || EPI == ACC;
+  static_assert(COUT == 128 || GEN, "Cout 64: the shared-weight plain epilogues");
   static_assert(FWD || DG || GEN, "the StyledConv / VGG / e4e epilogues");
   constexpr bool G_BIAS = GEN && (EPI & BIAS), G_MASK = GEN && (EPI & MASK);
   constexpr bool G_MSL = GEN && (EPI & MSL), G_ACC = GEN && (EPI & ACC);
@@ -110,7 +114,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const T* __restrict__ W0 = (const T*)k.g[0].w;
   const int kpad = k.g[0].kpad;
   T* __restrict__ Y = (T*)p.y;
-  const int cw0 = 16 * wid;  // this wave's first output channel
+  const int cw0 = 16 * (wid % TL::WNC);  // this wave's first output channel
+  const int row0 = FM * (wid / TL::WNC);  // and its first patch row
   const int cl = cw0 + ((lane >> 4) << 2);  // this lane's 4 channels (lane row r: cw0 + 4r …)
   // the zero page for padding lanes, loaded once (not rematerialised per DMA piece)
   const T* zero = (const T*)g_zero16;
@@ -202,9 +207,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if constexpr (AUXX) {  // DG: the stored activation aux_x; MASK: the mask operand; ACC: old y
       const T* AX = (const T*)(DG ? p.aux_x : (G_MASK ? p.mask_a : p.y));
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < FM / 2; ++j) {
         const int q = j * 32 + (ln >> 1), c = (ln & 1) ^ ((q >> 3) & 1);
-        const T* a = AX + ((size_t)(n * H + y0 + (q >> 4)) * W + x0 + (q & 15)) * Cout + cw0 + 8 * c;
+        const T* a =
+            AX + ((size_t)(n * H + y0 + row0 + (q >> 4)) * W + x0 + (q & 15)) * Cout + cw0 + 8 * c;
         __builtin_amdgcn_global_load_lds((gptr_t)a, (lptr_t)(aux + TL::NZB + j * 1024), 16, 0,
                                          0);
       }
@@ -257,7 +263,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int i = 0; i < FM; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     // the 120 fragment reads in (dx, s, q) order, each feeding the taps dy = 0, 1, 2 of output
     // row q − dy; the next read is issued before the current fragment's MFMAs
-    const char* hd[3] = {hb + offa[0], hb + offa[1], hb + offa[2]};
+    const char* hd[3] = {hb + offa[0] + row0 * 5 * GB, hb + offa[1] + row0 * 5 * GB,
+                         hb + offa[2] + row0 * 5 * GB};
     // fragment f = (dx·NS + s)·(FM + 2) + q, read PF fragments ahead into a ring of PF + 1
     constexpr int NQ = FM + 2, NF = 3 * NS * NQ, PF = MIA_WRES128_PF;
 #if MIA_WRES128_ASMREAD
@@ -340,7 +347,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       float vo[2][4];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const float z = NZ ? nzw * nz[(i + u) * 16 + px] : 0.f;
+        const float z = NZ ? nzw * nz[(row0 + i + u) * 16 + px] : 0.f;
         typedef T t4 __attribute__((ext_vector_type(4)));
         const int q = (i + u) * 16 + px;
         if constexpr (GEN) {
@@ -397,7 +404,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         a[h] = r[0];
         b[h] = r[1];
       }
-      const int m = (n * H + y0 + i + (lrow & 1)) * W + x0 + px;
+      const int m = (n * H + y0 + row0 + i + (lrow & 1)) * W + x0 + px;
       const int c = cw0 + 8 * (lrow >> 1);
       *(uint4*)(Y + (size_t)m * k.ystride + c) = make_uint4(a[0], a[1], b[0], b[1]);
     }
@@ -430,14 +437,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
 }
 
-template <typename T, int CIN, int EPI>
+template <typename T, int CIN, int EPI, int COUT = 128>
 static int launch_wres128_(ConvK& k, hipStream_t st) {
-  typedef Wres128Tile<CIN> TL;
+  typedef Wres128Tile<CIN, COUT> TL;
   constexpr bool AUXX = (EPI & (epi::SDOT | epi::MASK | epi::ACC)) != 0;
   constexpr bool DG = (EPI & epi::SDOT) != 0;
   constexpr int LDS = 2 * TL::HBUF + TL::NW * (TL::CHB + TL::NZB + (AUXX ? TL::AXB : 0));
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  auto fn = conv_wres128_kernel<T, CIN, EPI>;
+  auto fn = conv_wres128_kernel<T, CIN, EPI, COUT>;
   static int ncu = 0;
   if (!ncu) {
     if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS) !=
@@ -474,11 +481,15 @@ bool conv_wres128_eligible(const ConvK& k, int dtype) {
   if (dtype == MIA_F32 || k.ng != 1 || k.stride != 1 || G.kh != 3 || G.kw != 3 ||
       G.pad_y != 1 || G.pad_x != 1 || G.ho != a.H || G.wo != a.W || G.ay != 1 || G.ax != 1 ||
       G.by != 0 || G.bx != 0 || a.shuffle_out || a.H % 8 != 0 || a.W % 16 != 0 ||
-      (a.Cin != 128 && a.Cin != 64) || a.Cout != 128 || k.HT != a.H || k.WT != a.W ||
+      (a.Cin != 128 && a.Cin != 64) || (a.Cout != 128 && a.Cout != 64) || k.HT != a.H ||
+      k.WT != a.W ||
       a.in_scale || a.act_in != MIA_ACT_NONE || G.kpad < 9 * a.Cin || !a.y ||
       k.ystride != a.Cout || k.ysplit > 0)
     return false;
   const int f = epi_mask(k);
+  if (a.Cout == 64)  // (the 128 → 64 launches: VGG conv2_1 / e4e stage-2 input gradients)
+    return a.Cin == 128 && k.wn == 0 &&
+           (f == 0 || f == ACC || (f == (MASK | MSL) && a.mask_a && a.mask_slope));
   if (a.Cin == 64)  // (the 64 → 128 launches: VGG conv2_1 forward, the e4e stage-2 conv1)
     return k.wn == 0 && ((f == (BIAS | RELU) && a.bias) || (f == PRELU && a.act_slope));
   if (f == (NOISE | BIAS | LRELU)) return a.noise && a.bias && k.wn > 0;
@@ -499,6 +510,12 @@ int launch_conv_wres128(ConvK& k, int dtype, hipStream_t st) {
   const int f = epi_mask(k);
   MIA_DISPATCH_DTYPE(dtype, T, {
     if constexpr (sizeof(T) == 2) {
+      if (k.a.Cout == 64) {
+        if (f == 0) return launch_wres128_<T, 128, 0, 64>(k, st);
+        if (f == ACC) return launch_wres128_<T, 128, ACC, 64>(k, st);
+        if (f == (MASK | MSL)) return launch_wres128_<T, 128, MASK | MSL, 64>(k, st);
+        return set_error("conv_wres128: no Cout = 64 specialisation for this launch");
+      }
       if (k.a.Cin == 64) {
         if (f == (BIAS | RELU)) return launch_wres128_<T, 64, BIAS | RELU>(k, st);
         if (f == PRELU) return launch_wres128_<T, 64, PRELU>(k, st);

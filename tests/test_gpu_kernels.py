@@ -1578,3 +1578,43 @@ def test_wres128_cin64_forward(cuda, tune, dtype, N, R, W, mode):
     assert e < 2 * TOL[dtype]
     if R % 16 == 0:
         assert rel_err(nchw(y), nchw(y_halo).double()) < 2 * TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,R,W", [(4, 128, 128), (2, 24, 32), (1, 8, 16)])
+@pytest.mark.parametrize("mode", ["plain", "acc", "mask_slope"])
+def test_wres128_cout64(cuda, tune, dtype, N, R, W, mode):
+    """The weights-resident kernel with Cout = 64 (8 waves = 2 row groups × 4 channel groups of
+    16) on the 128 → 64 input gradients (VGG conv2_1, the e4e stage-2 conv1: plain, accumulated,
+    PReLU'-masked): against torch fp64 and the halo tile (MIA_CONV_WRES128=0)."""
+    cin, C = 128, 64
+    g = torch.Generator().manual_seed(N * 17 + R + W + len(mode))
+    x = torch.randn(N, cin, R, W, generator=g)
+    w = torch.randn(C, cin, 3, 3, generator=g) / math.sqrt(9 * cin)
+    xq, wq = x.to(dtype).double(), w.to(dtype).double()
+    wf = layouts.fwd_matrix(w, dtype).to(cuda)
+    grp = [dict(w=wf, kh=3, kw=3, pad=(1, 1), ho=R, wo=W)]
+    conv = F.conv2d(xq, wq, padding=1)
+    y0 = torch.randn(N, C, R, W, generator=g)
+    if mode == "plain":
+        ref, kw = conv, {}
+    elif mode == "acc":
+        ref, kw = conv + y0.to(dtype).double(), dict(accumulate=True)
+    else:
+        m = torch.randn(N, C, R, W, generator=g)
+        slope = torch.rand(C, generator=g) * 0.5 + 0.05
+        ref = torch.where(m.to(dtype).double() > 0, conv, slope.double().view(1, C, 1, 1) * conv)
+        kw = dict(mask_a=nhwc(m, dtype).to(cuda), mask_slope=slope.to(cuda))
+    xd = nhwc(x, dtype).to(cuda)
+    y = nhwc(y0, dtype).to(cuda)
+    ops.conv2d(xd, grp, y, (R, W), cout=C, **kw)
+    tune("MIA_CONV_WRES128", 0)
+    y_halo = nhwc(y0, dtype).to(cuda)
+    if R % 16 == 0:
+        ops.conv2d(xd, grp, y_halo, (R, W), cout=C, **kw)
+    torch.cuda.synchronize()
+    e = rel_err(nchw(y), ref)
+    print(f"wres128 Cout 64 {mode} {dtype} {N}x{R}x{W}: rel err vs fp64 {e:.2e}")
+    assert e < 2 * TOL[dtype]
+    if R % 16 == 0:
+        assert rel_err(nchw(y), nchw(y_halo).double()) < 2 * TOL[dtype]

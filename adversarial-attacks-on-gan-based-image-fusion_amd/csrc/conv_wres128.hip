@@ -107,14 +107,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int H = p.H, W = p.W, Cout = p.Cout;
   const int ptx = W / TL::PW, pty = H / TL::PH;
   const int ntiles = p.N * ptx * pty;
-  const int per = (ntiles + gridDim.x - 1) / gridDim.x;
-  const int t0 = blockIdx.x * per, t1 = min(t0 + per, ntiles);
+  // Cout = nct · BN: blocks [ct·runs, (ct+1)·runs) take output channels ct·BN … of every patch
+  const int nct = Cout / TL::BN, runs = gridDim.x / nct;
+  const int ct = blockIdx.x / runs, rb = blockIdx.x - ct * runs;
+  const int per = (ntiles + runs - 1) / runs;
+  const int t0 = rb * per, t1 = min(t0 + per, ntiles);
   if (t0 >= t1) return;
   const T* __restrict__ X = (const T*)p.x;
   const T* __restrict__ W0 = (const T*)k.g[0].w;
   const int kpad = k.g[0].kpad;
   T* __restrict__ Y = (T*)p.y;
-  const int cw0 = 16 * (wid % TL::WNC);  // this wave's first output channel
+  const int cw0 = TL::BN * ct + 16 * (wid % TL::WNC);  // this wave's first output channel
   const int row0 = FM * (wid / TL::WNC);  // and its first patch row
   const int cl = cw0 + ((lane >> 4) << 2);  // this lane's 4 channels (lane row r: cw0 + 4r …)
   // the zero page for padding lanes, loaded once (not rematerialised per DMA piece)
@@ -456,8 +459,10 @@ static int launch_wres128_(ConvK& k, hipStream_t st) {
       ncu = 256;
   }
   const int ntiles = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW);
-  const int per = (ntiles + ncu - 1) / ncu;
-  const int grid = (ntiles + per - 1) / per;  // every block has a non-empty run
+  // Cout = nct column tiles of BN channels, each over the CUs' share of contiguous patch runs
+  const int nct = k.a.Cout / TL::BN, share = std::max(1, ncu / nct);
+  const int per = (ntiles + share - 1) / share;
+  const int grid = nct * ((ntiles + per - 1) / per);  // every block has a non-empty run
   k.prered = 0;
   RedQ r;
   int rc = conv_red_begin(k, r, DG ? (k.a.H / TL::PH) * (k.a.W / TL::PW) : 1, st);
@@ -481,12 +486,15 @@ bool conv_wres128_eligible(const ConvK& k, int dtype) {
   if (dtype == MIA_F32 || k.ng != 1 || k.stride != 1 || G.kh != 3 || G.kw != 3 ||
       G.pad_y != 1 || G.pad_x != 1 || G.ho != a.H || G.wo != a.W || G.ay != 1 || G.ax != 1 ||
       G.by != 0 || G.bx != 0 || a.shuffle_out || a.H % 8 != 0 || a.W % 16 != 0 ||
-      (a.Cin != 128 && a.Cin != 64) || (a.Cout != 128 && a.Cout != 64) || k.HT != a.H ||
+      (a.Cin != 128 && a.Cin != 64) || (a.Cout != 128 && a.Cout != 64 && a.Cout != 256) ||
+      k.HT != a.H ||
       k.WT != a.W ||
       a.in_scale || a.act_in != MIA_ACT_NONE || G.kpad < 9 * a.Cin || !a.y ||
       k.ystride != a.Cout || k.ysplit > 0)
     return false;
   const int f = epi_mask(k);
+  if (a.Cout == 256)  // (two column tiles: VGG conv3_1 forward, the e4e stage-3 conv1, 64²)
+    return k.wn == 0 && ((f == (BIAS | RELU) && a.bias) || (f == PRELU && a.act_slope));
   if (a.Cout == 64)  // (the 128 → 64 launches: VGG conv2_1 / e4e stage-2 input gradients)
     return a.Cin == 128 && k.wn == 0 &&
            (f == 0 || f == ACC || (f == (MASK | MSL) && a.mask_a && a.mask_slope));

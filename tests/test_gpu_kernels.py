@@ -1618,3 +1618,40 @@ def test_wres128_cout64(cuda, tune, dtype, N, R, W, mode):
     assert e < 2 * TOL[dtype]
     if R % 16 == 0:
         assert rel_err(nchw(y), nchw(y_halo).double()) < 2 * TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("cin,N,R,W", [(128, 3, 64, 64), (64, 2, 32, 48), (128, 1, 8, 16)])
+@pytest.mark.parametrize("mode", ["bias_relu", "prelu"])
+def test_wres128_cout256_column_tiles(cuda, tune, dtype, cin, N, R, W, mode):
+    """The weights-resident kernel over two 128-channel column tiles (Cout = 256: VGG conv3_1
+    forward, the e4e stage-3 conv1): against torch fp64 and the halo tile (MIA_CONV_WRES128=0)."""
+    C = 256
+    g = torch.Generator().manual_seed(N * 19 + R + W + cin + len(mode))
+    x = torch.randn(N, cin, R, W, generator=g)
+    w = torch.randn(C, cin, 3, 3, generator=g) / math.sqrt(9 * cin)
+    xq, wq = x.to(dtype).double(), w.to(dtype).double()
+    wf = layouts.fwd_matrix(w, dtype).to(cuda)
+    grp = [dict(w=wf, kh=3, kw=3, pad=(1, 1), ho=R, wo=W)]
+    conv = F.conv2d(xq, wq, padding=1)
+    if mode == "bias_relu":
+        b = torch.randn(C, generator=g) * 0.1
+        ref = F.relu(conv + b.double().view(1, C, 1, 1))
+        kw = dict(bias=b.to(cuda), act_out=ops.ACT_RELU)
+    else:
+        slope = torch.rand(C, generator=g) * 0.5 + 0.05
+        ref = torch.where(conv > 0, conv, slope.double().view(1, C, 1, 1) * conv)
+        kw = dict(act_out=ops.ACT_PRELU, act_slope=slope.to(cuda))
+    xd = nhwc(x, dtype).to(cuda)
+    y = torch.full((N, R, W, C), float("nan"), dtype=dtype, device=cuda)
+    ops.conv2d(xd, grp, y, (R, W), cout=C, **kw)
+    tune("MIA_CONV_WRES128", 0)
+    y_halo = torch.full_like(y, float("nan"))
+    if R % 16 == 0:
+        ops.conv2d(xd, grp, y_halo, (R, W), cout=C, **kw)
+    torch.cuda.synchronize()
+    e = rel_err(nchw(y), ref)
+    print(f"wres128 Cout 256 (Cin {cin}) {mode} {dtype} {N}x{R}x{W}: rel err vs fp64 {e:.2e}")
+    assert e < 2 * TOL[dtype]
+    if R % 16 == 0:
+        assert rel_err(nchw(y), nchw(y_halo).double()) < 2 * TOL[dtype]

@@ -9,10 +9,13 @@
 //   * the weights live in VGPRs for the whole kernel (each wave loads them once);
 //   * a wave computes 16 consecutive pixels of one image row per step with MFMA 16×16×32,
 //     D[channel][pixel]; the pixel operand is gathered straight from global memory into VGPRs
-//     (one 16-B vector per lane per K-chunk, the neighbours' re-reads hit L1/L2), so there is no
-//     LDS traffic and no barrier;
-//   * forward stores: pairs of channel fragments are exchanged between lane rows
-//     (v_permlane16_swap) so every lane writes 8 consecutive channels with one 16-B store;
+//     (one 16-B vector per lane per K-chunk, the neighbours' re-reads hit L1/L2), and no block
+//     barrier;
+//   * forward stores (round 5): the 16 pixels × 64 channels of a group go through the wave's own
+//     LDS slice, so each non-temporal store instruction writes 8 whole pixels (1 KB contiguous);
+//     the round-4 form (lane-row swaps, each instruction writing half of 16 pixel rows) wrote at
+//     2.5 TB/s where a plain fill writes 6.6–6.9: 431 → 308 µs per 128 × 256² call
+//     (profiles/r05_thin_store_ab.txt);
 //   * the gradient kernel stages each input pixel once per wave work item in LDS (9 taps read it);
 //   * waves stride over the pixel groups / work items.
 #include <type_traits>
@@ -46,6 +49,7 @@ __global__ __launch_bounds__(256) void conv_thin_in_kernel(const T* __restrict__
                                                            T* __restrict__ y, int N, int H, int W) {
   typedef typename Vec<T>::type VT;
   constexpr int FN = COUT / 16;
+  __shared__ __attribute__((aligned(16))) char stage[4 * 16 * 144];  // per wave 16 pixels
   const int lane = threadIdx.x & 63, frow = lane & 15, fq = lane >> 4;
   const int wave = blockIdx.x * 4 + (threadIdx.x >> 6), nwaves = gridDim.x * 4;
   VT wr[FN][3];
@@ -83,39 +87,33 @@ __global__ __launch_bounds__(256) void conv_thin_in_kernel(const T* __restrict__
 #pragma unroll
       for (int m = 0; m < 3; ++m) acc[j] = mfma_chunk<T>(wr[j][m], af[m], acc[j]);
     }
-    // lane (frow = pixel, fq) holds channels 16j + 4fq … +3 of its pixel
-    T* yp = y + ((size_t)row * W + px) * COUT;
-    typedef T t2 __attribute__((ext_vector_type(2)));
+    // lane (frow = pixel, fq) holds channels 16j + 4fq … +3 of its pixel: staged through the
+    // wave's LDS slice so each store instruction writes 8 whole pixels (1 KB contiguous)
+    static_assert(COUT == 64, "the staged store covers 16 pixels x 128 B");
+    constexpr int PITCH = 144;  // bytes per staged pixel (36 dwords: conflict-free b64 writes)
+    char* const sw = stage + (threadIdx.x >> 6) * 16 * PITCH;
+    typedef T t4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-    for (int q = 0; q < FN / 2; ++q) {
-      unsigned a[2], b[2];
+    for (int j = 0; j < FN; ++j) {
+      float v[4];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        float va[2], vb[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          va[e] = acc[2 * q][2 * h + e] + bs[2 * q][2 * h + e];
-          vb[e] = acc[2 * q + 1][2 * h + e] + bs[2 * q + 1][2 * h + e];
-          if (act == MIA_ACT_PRELU) {
-            va[e] = va[e] > 0.f ? va[e] : sl[2 * q][2 * h + e] * va[e];
-            vb[e] = vb[e] > 0.f ? vb[e] : sl[2 * q + 1][2 * h + e] * vb[e];
-          } else {
-            va[e] = apply_act(va[e], act);
-            vb[e] = apply_act(vb[e], act);
-          }
-        }
-        const t2 ta = {(T)va[0], (T)va[1]};
-        const t2 tb = {(T)vb[0], (T)vb[1]};
-        const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, ta),
-                                                        __builtin_bit_cast(unsigned, tb), false,
-                                                        false);
-        a[h] = r[0];
-        b[h] = r[1];
+      for (int r = 0; r < 4; ++r) {
+        v[r] = acc[j][r] + bs[j][r];
+        if (act == MIA_ACT_PRELU) v[r] = v[r] > 0.f ? v[r] : sl[j][r] * v[r];
+        else v[r] = apply_act(v[r], act);
       }
-      // after the swap lane row fq holds channels [16·(2q + (fq & 1)) + 8·(fq >> 1), +8)
-      const int c = 16 * (2 * q + (fq & 1)) + 8 * (fq >> 1);
-      *(uint4*)(yp + c) = make_uint4(a[0], a[1], b[0], b[1]);
+      *(t4*)(sw + frow * PITCH + (16 * j + 4 * fq) * 2) = t4{(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
     }
+    asm volatile("" ::: "memory");  // a wave's LDS accesses execute in order: no barrier needed
+    T* yg = y + ((size_t)row * W + xg) * COUT;
+    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int p = 8 * i + (lane >> 3), c = lane & 7;
+      const u4v v = *(const u4v*)(sw + p * PITCH + 16 * c);
+      __builtin_nontemporal_store(v, (u4v*)(yg + p * COUT + 8 * c));
+    }
+    asm volatile("" ::: "memory");
   }
 }
 
@@ -522,7 +520,8 @@ __device__ __forceinline__ void thin_in_f32_body(const float* __restrict__ x,
         if (act == MIA_ACT_PRELU) o[e] = o[e] > 0.f ? o[e] : sl[e] * o[e];
         else o[e] = apply_act(o[e], act);
       }
-      *(f32x4*)(y + (size_t)(pix0 + p) * COUT + c0) = o;
+      // non-temporal: the 2.15 GB output streams past L2 / MALL (−9 % per call)
+      __builtin_nontemporal_store(o, (f32x4*)(y + (size_t)(pix0 + p) * COUT + c0));
     }
   }
 }

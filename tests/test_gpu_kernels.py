@@ -780,9 +780,8 @@ def test_conv_thin_vgg_input_layer(cuda, tune, dtype, N, H, W, thin, e4e):
     implicit-GEMM tiles), against torch fp64 on the same rounded operands. e4e: the encoder's
     input layer — bias + PReLU forward, gradient accumulated into an existing one (mia_conv2d).
     fp32 runs on the VALU kernels (the padded channels skipped by their zero weights); 9 × 256²
-    pixels exceed one pass of their persistent grid."""
-    if (N, H, W) == (9, 256, 256) and dtype != torch.float32:
-        pytest.skip("the persistent-loop shape is checked for the fp32 VALU kernels")
+    pixels exceed one pass of their persistent grid (and, at 2-byte types, give every wave of
+    the grid-strided MFMA kernels several pixel groups)."""
     tune("MIA_CONV_THIN", thin)
     if e4e:
         return _thin_e4e_input_layer(cuda, dtype, N, H, W)

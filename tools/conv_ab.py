@@ -46,6 +46,7 @@ SHAPES = [
     ("up 64²→128² 512→256", 64, 512, 256, "up"),
     ("up 32²→64² 512→512", 32, 512, 512, "up"),
     # e4e IR-SE50 body (mia_conv2d epilogue features)
+    ("e4e in prelu 256² 8→64", 256, 8, 64, "prelu"),
     ("e4e prelu 256² 64→64", 256, 64, 64, "prelu"),
     ("e4e bias+csum 128² 64→64", 128, 64, 64, "csum"),
     ("e4e mask+slope 128² 64→64", 128, 64, 64, "mslope"),

@@ -94,6 +94,8 @@ SIGNATURES = {
                                       P]),
     "mia_vgg_conv_dgrad": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P,
                                    c_float, P, c_int, P]),
+    "mia_vgg_conv_relu_dgrad": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P,
+                                        P, c_float, P, c_int, P]),
     "mia_upconv_kpad": (c_int, [c_int, c_int, c_int]),
     "mia_upconv_fwd": (c_int, [P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, P]),
     "mia_upconv_fwd_halo": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, P, c_int, P]),
@@ -127,6 +129,7 @@ SIGNATURES = {
     "mia_image_to_nhwc": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_mse_sum": (c_int, [P, P, P, c_int, c_int64, c_float, c_int, P]),
     "mia_mse_grad_f32": (c_int, [P, P, P, c_int64, c_float, c_int, P]),
+    "mia_mse_fwd_bwd": (c_int, [P, P, P, P, c_int, c_int64, c_float, c_float, c_int, c_int, P]),
     "mia_tap_grad": (c_int, [P, P, P, c_int64, c_float, c_int, c_int, P]),
     "mia_image_grad": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_float, c_int, P]),
     "mia_pgd_update": (c_int, [P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, c_float,

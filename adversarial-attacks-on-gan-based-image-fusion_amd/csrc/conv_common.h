@@ -110,8 +110,6 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
 // tap-shifted reads do not respect).
 __device__ __forceinline__ int fsw(int row) { return ((row >> 1) & 3) << 1; }
 
-// the register epilogues' LDS pre-reduction of the channel sums (T_EPI_PRERED, default on)
-inline int prered_enabled() { return tune(T_EPI_PRERED) != 0; }
 
 __device__ __forceinline__ int div_kw(int t, int kw) {
   return kw == 3 ? (t * 11) >> 5 : (kw == 2 ? t >> 1 : t);  // exact for t < 9

@@ -475,14 +475,8 @@ static int launch_halo_tile_(ConvK& k, hipStream_t st) {
   if (TL::NHBUF == 1 && k.a.Cin != ROWB / (int)sizeof(T))
     return set_error("conv_halo: single-buffer tile needs Cin = one channel block");
   auto fn = conv_halo_kernel<T, TL, PRO, EPI>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
-      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-    attr_set = true;
-  }
-  k.prered = prered_enabled() && EPI >= 0 && (EPI & epi::CSUM);
+  if (const int rc = ensure_dyn_lds((const void*)fn, 160 * 1024); rc != MIA_OK) return rc;
+  k.prered = EPI >= 0 && (EPI & epi::CSUM);
   const int H = k.a.H, W = k.a.W;
   const int nslots = EPI >= 0    ? halo_red_slots(H, W, TL::FM, TL::WM, k.prered)
                      : EPI == -1 ? halo_red_slots(H, W, TL::FM, TL::WM, false)

@@ -452,14 +452,8 @@ static int launch_x6_e(ConvK& k, hipStream_t st) {
   lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
   lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
   auto fn = conv_halo_x6_kernel<BN_, PRO, EPI, EARLY, PRIO, UNR, TPS>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
-      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-    attr_set = true;
-  }
-  k.prered = prered_enabled() && EPI >= 0 && (EPI & epi::CSUM);
+  if (const int rc = ensure_dyn_lds((const void*)fn, 160 * 1024); rc != MIA_OK) return rc;
+  k.prered = EPI >= 0 && (EPI & epi::CSUM);
   const int H = k.a.H, W = k.a.W;
   const int nslots = EPI >= 0    ? halo_red_slots(H, W, TL::FM, TL::WM, k.prered)
                      : EPI == -1 ? halo_red_slots(H, W, TL::FM, TL::WM, false)
@@ -711,14 +705,8 @@ static int launch_x6s_(ConvK& k, hipStream_t st) {
   lds = std::max(lds, (size_t)TL::EROWS * TL::ES * 4);
   lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
   auto fn = conv_halo_x6s_kernel<PRO, EPI>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            80 * 1024) != hipSuccess)
-      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-    attr_set = true;
-  }
-  k.prered = prered_enabled() && (EPI & epi::CSUM);
+  if (const int rc = ensure_dyn_lds((const void*)fn, 80 * 1024); rc != MIA_OK) return rc;
+  k.prered = (EPI & epi::CSUM);
   const int nslots = halo_red_slots(k.a.H, k.a.W, TL::FM, TL::WM, k.prered);
   RedQ r;
   int rc = conv_red_begin(k, r, nslots, st);

@@ -346,14 +346,8 @@ static int launch_tile(ConvK& k, hipStream_t st) {
   lds = std::max(lds, (size_t)TL::NW * TL::BN * 4);
   if (lds > 160 * 1024) return set_error("conv: LDS budget exceeded");
   auto fn = conv_kernel<T, TL, PRO, SMALLC, EPI, X6B>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
-      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-    attr_set = true;
-  }
-  k.prered = prered_enabled() && EPI >= 0 && (EPI & epi::CSUM);
+  if (const int rc = ensure_dyn_lds((const void*)fn, 160 * 1024); rc != MIA_OK) return rc;
+  k.prered = EPI >= 0 && (EPI & epi::CSUM);
   // X6B: s_setprio(1) around the MFMA blocks measured 1-2 % slower on this 2-blocks-per-CU tile
   k.prio = 0;
   // deterministic sums: contributor slots per (image, channel) (sums need one group, identity
@@ -912,4 +906,12 @@ extern "C" int mia_vgg_conv_dgrad(const void* g, const void* w_t, void* gx, int 
   a.N = N; a.H = H; a.W = W; a.Cin = Cin_g; a.Cout = Cout_g; a.Kpad = Kpad;
   a.tap_a = tap_a; a.tap_t = tap_t; a.tap_coef = tap_coef; a.mask_a = mask_a;
   return mia_conv3x3(&a, dtype, stream);
+}
+
+extern "C" int mia_vgg_conv_relu_dgrad(const void* g, const void* w_t, void* gx, int N, int H,
+                                       int W, int Cin_g, int Cout_g, int Kpad, const void* tap_a,
+                                       const void* tap_t, float tap_coef, const void* mask_a,
+                                       int dtype, void* stream) {
+  return mia_vgg_conv_dgrad(g, w_t, gx, N, H, W, Cin_g, Cout_g, Kpad, tap_a, tap_t, tap_coef,
+                            mask_a, dtype, stream);
 }

@@ -118,105 +118,14 @@ __global__ __launch_bounds__(256) void conv_thin_in_kernel(const T* __restrict__
 }
 
 // ---- input gradient, CIN = 64 channels → 8 output channels (store, or accumulate into y) -------
-// Every input pixel feeds 9 taps, so the pixel operand is staged per wave in LDS: a work item is
-// RS = 2 output rows × 16 pixels; its (RS+2) × 18 input pixels (72 rows of 128 B, 9 LDS-DMA pieces
-// of 1 KB, bank-swizzled through the source chunk as in conv_halo.hip) are DMA'd once, then read
-// by the 9 taps × 2 K-chunks as MFMA B fragments. Each wave owns two such buffers and prefetches
-// its next item while computing the current one; no block barrier (a wave reads only what its own
-// DMA wrote, after its own vmcnt).
-// D[channel][pixel] with channel rows 0 … 15 (rows ≥ COUT zero weights); K = 9 taps × 64 in
-// chunks of 32: chunk s = (tap s / 2, channels 32·(s & 1) + 8·fq …).
-constexpr int THIN_RS = 2, THIN_HW = 18, THIN_ROWS = (THIN_RS + 2) * THIN_HW;  // 72
-constexpr int THIN_PIECES = (THIN_ROWS + 7) / 8;                               // 9
-constexpr int THIN_WBUF = THIN_PIECES * 1024;
-
-template <typename T, int COUT>
-__global__ __launch_bounds__(256) void conv_thin_out_kernel(const T* __restrict__ g,
-                                                            const T* __restrict__ w, int kpad,
-                                                            T* __restrict__ y, int accumulate,
-                                                            int N, int H, int W) {
-  typedef typename Vec<T>::type VT;
-  constexpr int CIN = 64, S = 18;
-  static_assert(COUT == 8, "");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63, frow = lane & 15, fq = lane >> 4;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  char* const wbuf = smem + wid * 2 * THIN_WBUF;
-  const int wave = blockIdx.x * 4 + wid, nwaves = gridDim.x * 4;
-  VT wr[S];
-#pragma unroll
-  for (int s = 0; s < S; ++s)
-    wr[s] = ld16_or_zero<T>(w + (size_t)(frow < COUT ? frow : 0) * kpad + 32 * s + 8 * fq,
-                            frow < COUT);
-  const T* zero = (const T*)g_zero16;
-  const int gpr = W / 16, rpi = (H + THIN_RS - 1) / THIN_RS, nitems = N * rpi * gpr;
-
-  auto issue = [&](int it, int buf) {  // the input window of item it into buffer buf
-    const int row = it / gpr, x0 = (it - row * gpr) * 16;
-    const int n = row / rpi, y0 = (row - n * rpi) * THIN_RS;
-#pragma unroll
-    for (int q = 0; q < THIN_PIECES; ++q) {
-      const int r = q * 8 + (lane >> 3);
-      const int hy = r / THIN_HW, hx = r - (r / THIN_HW) * THIN_HW;
-      const int sy = y0 + hy - 1, sx = x0 + hx - 1;
-      const bool ok = r < THIN_ROWS && sy >= 0 && sy < H && sx >= 0 && sx < W;
-      const T* src = ok ? g + ((size_t)(n * H + sy) * W + sx) * CIN + ((lane & 7) ^ fsw(r)) * 8
-                        : zero;
-      __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)(wbuf + buf * THIN_WBUF + q * 1024),
-                                       16, 0, 0);
-    }
-  };
-
-  int it = wave, buf = 0;
-  if (it < nitems) issue(it, 0);
-  for (; it < nitems; it += nwaves, buf ^= 1) {
-    const int nxt = it + nwaves;
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): reads of the other buffer are done
-    if (nxt < nitems) {
-      issue(nxt, buf ^ 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(THIN_PIECES) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    const char* hb = wbuf + buf * THIN_WBUF;
-    const int row = it / gpr, x0 = (it - row * gpr) * 16;
-    const int n = row / rpi, y0 = (row - n * rpi) * THIN_RS;
-#pragma unroll
-    for (int ry = 0; ry < THIN_RS; ++ry) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int r = (ry + t / 3) * THIN_HW + frow + t % 3;
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const VT bf = *(const VT*)(hb + r * ROWB + (((4 * c + fq) ^ fsw(r)) << 4));
-          acc = mfma_chunk<T>(wr[2 * t + c], bf, acc);
-        }
-      }
-      // lane (frow = pixel, fq) holds output channels 4fq … 4fq+3; channels < 8 are real
-      const int yy = y0 + ry;
-      if (fq < COUT / 4 && yy < H) {
-        float v[4] = {acc[0], acc[1], acc[2], acc[3]};
-        T* yp = y + ((size_t)(n * H + yy) * W + x0 + frow) * COUT + 4 * fq;
-        if (accumulate) {  // the e4e input layer's gradient adds into the VGG input-path gradient
-          float yo[4];
-          load4<T>(yp, yo);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += yo[e];
-        }
-        store4<T>(yp, v);
-      }
-    }
-  }
-}
-
-// Round 4: the same input gradient on sliding-window row strips (the fp32 kernel's round-3 scheme
-// on the MFMA form above): a work item is a 16-pixel column strip × THIN_SR output rows; the wave
-// keeps a ring of 4 input rows (18 pixels × 128 B, 3 LDS-DMA pieces each) and per output row DMAs
-// only the next input row, so each input row comes from L2 / HBM about once instead of twice
-// (rocprof: 2.24 GB fetched per 1.07 GB gradient with the 2-row items). Same MFMAs in the same
-// order per output (bit-identical). A/B build: MIA_THIN_OUT_RS2 keeps the 2-row items.
-constexpr int THIN_SR = 16, THIN_SLOT = 3 * 1024, THIN_RING = 4;
+// On sliding-window row strips: a work item is a 16-pixel column strip × THIN_SR output rows; the
+// wave keeps a ring of 4 input rows (18 pixels × 128 B, 3 LDS-DMA pieces each, bank-swizzled
+// through the source chunk as in conv_halo.hip) and per output row DMAs only the next input row,
+// so each input row comes from L2 / HBM about once (rocprof: 2.24 → 1.27 GB fetched per 1.07 GB
+// gradient against round 3's 2-row items, which were removed in round 6). The 9 taps × 2 K-chunks
+// read the rows as MFMA B fragments; D[channel][pixel] with channel rows 0 … 15 (rows ≥ COUT zero
+// weights); K = 9 taps × 64 in chunks of 32: chunk s = (tap s / 2, channels 32·(s & 1) + 8·fq …).
+constexpr int THIN_SR = 16, THIN_HW = 18, THIN_SLOT = 3 * 1024, THIN_RING = 4;
 
 template <typename T, int COUT>
 __global__ __launch_bounds__(256) void conv_thin_out_strip_kernel(const T* __restrict__ g,
@@ -414,13 +323,7 @@ __global__ __launch_bounds__(256) void conv_thin32_kernel(const ConvK k) {
 }
 
 static int grid_for(int64_t groups, int waves_per_cu = 32) {
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      ncu = 256;
-  }
+  const int ncu = device_cu_count();
   const int64_t waves = std::min<int64_t>(groups, (int64_t)ncu * waves_per_cu);
   return (int)std::max<int64_t>(1, (waves + 3) / 4);
 }
@@ -449,8 +352,9 @@ __device__ __forceinline__ int64_t thin_seg_origin(int64_t seg, int H, int W, in
 // weights are transposed into LDS as [k][64] (one 16-B read per (tap, channel) serves the
 // segment's 4 pixels × 4 channels). CM: the real input channels as a compile-time mask (0x07, the
 // RGB image), or 0xff with the runtime mask cmask.
-// HOIST (T_THIN_F32 = 2): the segment's 3 × 6 input pixels are all loaded before the first FMA
-// (one exposed load latency per segment instead of one per tap row); same FMA order.
+// HOIST (the RGB-mask instance): the segment's 3 × 6 input pixels are all loaded before the first
+// FMA (one exposed load latency per segment instead of one per tap row; round 3, 1.10 → 0.90 ms per
+// 128 × 256² call); the runtime-mask instance loads per tap row.
 template <int CM, bool HOIST>
 __device__ __forceinline__ void thin_in_f32_body(const float* __restrict__ x,
                                                  const float* __restrict__ wl, int cmask,
@@ -526,7 +430,6 @@ __device__ __forceinline__ void thin_in_f32_body(const float* __restrict__ x,
   }
 }
 
-template <bool HOIST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv_thin_in_f32_kernel(
     const float* __restrict__ x, const float* __restrict__ w, int kpad,
     const float* __restrict__ bias, int act, const float* __restrict__ slope,
@@ -552,7 +455,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   if (bias) bs = *(const f32x4*)(bias + c0);
   if (act == MIA_ACT_PRELU) sl = *(const f32x4*)(slope + c0);
   if (cmask == 0x07) {
-    thin_in_f32_body<0x07, HOIST>(x, wl, cmask, bs, sl, act, y, N, H, W);
+    thin_in_f32_body<0x07, true>(x, wl, cmask, bs, sl, act, y, N, H, W);
   } else {
     thin_in_f32_body<0xff, false>(x, wl, cmask, bs, sl, act, y, N, H, W);
   }
@@ -563,20 +466,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 // in VGPRs; the segment's 4 pixels × 4 output channels are reduced over the 16 lanes by DPP.
 // Real output channels ≥ 4 (never the case for an RGB image) take a slower path with the weights
 // as wave-uniform scalar loads, one pixel per lane.
-// LDSW (T_THIN_F32 ≥ 1): the 144 weights a lane needs are read from LDS per tap instead of held in
-// VGPRs (209 → ~80 VGPRs: 2 → 6 waves per SIMD to cover the 2.1 GB gradient read); LDS layout
-// [tap][e][q][co], so the 16 lanes of a group read 256 contiguous bytes (no bank conflict). Same
-// FMA order either way (bit-identical).
-// STRIP (T_THIN_F32 = 3, with LDSW): sliding-window row strips (below); the grid-strided
-// 4-pixel segments re-read each input row for 3 output rows from L2 / HBM (rocprof: 5.5 GB
-// fetched per 2.15 GB gradient).
+// The 144 weights a lane needs are read from LDS per tap (held in VGPRs they took 209 VGPRs and
+// 2 waves per SIMD); LDS layout [tap][e][q][co], so the 16 lanes of a group read 256 contiguous
+// bytes (no bank conflict). Sliding-window row strips (below): a grid-strided 4-pixel segment
+// loop re-read each input row for 3 output rows from L2 / HBM (rocprof: 5.5 GB fetched per
+// 2.15 GB gradient; 2.5 GB with the strips). Round 6: the round-2 / round-3 launch modes
+// (MIA_THIN_F32 0–2, bit-identical and slower) were removed.
 constexpr int THIN_STRIP = 16;
-template <bool ACC, bool LDSW, bool STRIP = false>
+template <bool ACC>
 __global__ __launch_bounds__(256) void conv_thin_out_f32_kernel(
     const float* __restrict__ g, const float* __restrict__ w, int kpad, float* __restrict__ y,
     int N, int H, int W, int gen_blocks) {
   constexpr int CIN = 64, COUT = 8, K = 9 * CIN;
-  __shared__ __attribute__((aligned(16))) float wl[LDSW ? 9 * 4 * 16 * 4 : 4];
+  __shared__ __attribute__((aligned(16))) float wl[9 * 4 * 16 * 4];
   __shared__ int cmask_s;
   const int tid = threadIdx.x;
   if (tid == 0) cmask_s = 0;
@@ -623,173 +525,94 @@ __global__ __launch_bounds__(256) void conv_thin_out_f32_kernel(
     return;
   }
   const int q = tid & 15;
-  float wv[LDSW ? 1 : 9][4][4];  // [tap][input channel 4q + e][output channel]
-  if constexpr (LDSW) {
-    for (int i = tid; i < 9 * 4 * 16 * 4; i += 256) {  // i = ((t·4 + e)·16 + q')·4 + co
-      const int co = i & 3, qq = (i >> 2) & 15, te = i >> 6, t = te >> 2, e = te & 3;
-      wl[i] = w[(size_t)co * kpad + t * CIN + 4 * qq + e];
-    }
-    __syncthreads();
-  } else {
-#pragma unroll
-    for (int t = 0; t < 9; ++t)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-#pragma unroll
-        for (int co = 0; co < 4; ++co) wv[t][e][co] = w[(size_t)co * kpad + t * CIN + 4 * q + e];
+  for (int i = tid; i < 9 * 4 * 16 * 4; i += 256) {  // i = ((t·4 + e)·16 + q')·4 + co
+    const int co = i & 3, qq = (i >> 2) & 15, te = i >> 6, t = te >> 2, e = te & 3;
+    wl[i] = w[(size_t)co * kpad + t * CIN + 4 * qq + e];
   }
-  if constexpr (STRIP) {
-    // a 16-lane group walks THIN_STRIP output rows of one 4-pixel column segment with a sliding
-    // window of 3 input rows in VGPRs: one new input row (6 pixel records) per output row instead
-    // of 3. The 16 groups of a block take 16 adjacent segments of the same strip. Per output
-    // pixel the FMAs run in the same order as the segment loop below (bit-identical).
-    const int spr = W / 4, nsy = (H + THIN_STRIP - 1) / THIN_STRIP;
-    const int64_t nitems = (int64_t)N * nsy * spr;
-    auto load_row = [&](int n, int sy, int x0, f32x4 (&dst)[6]) __attribute__((always_inline)) {
-      const bool oky = sy >= 0 && sy < H;
+  __syncthreads();
+  // a 16-lane group walks THIN_STRIP output rows of one 4-pixel column segment with a sliding
+  // window of 3 input rows in VGPRs: one new input row (6 pixel records) per output row instead
+  // of 3. The 16 groups of a block take 16 adjacent segments of the same strip. Per output
+  // pixel the FMAs run in the same order as the segment loop below (bit-identical).
+  const int spr = W / 4, nsy = (H + THIN_STRIP - 1) / THIN_STRIP;
+  const int64_t nitems = (int64_t)N * nsy * spr;
+  auto load_row = [&](int n, int sy, int x0, f32x4 (&dst)[6]) __attribute__((always_inline)) {
+    const bool oky = sy >= 0 && sy < H;
 #pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        const int sx = x0 + c - 1;
-        const bool ok = oky && sx >= 0 && sx < W;
-        dst[c] = ok ? *(const f32x4*)(g + ((size_t)(n * H + sy) * W + sx) * CIN + 4 * q)
-                    : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    };
-    // NCO = 3 when output channel 3 is padding too (cmask 0x07, an RGB image): its FMAs are
-    // skipped and it stores +0, what the four-channel form computes from zero weights
-    auto strip = [&](auto nco_c) __attribute__((always_inline)) {
-    constexpr int NCO = decltype(nco_c)::value;
-    for (int64_t it = (int64_t)blockIdx.x * 16 + (tid >> 4); it < nitems;
-         it += (int64_t)gridDim.x * 16) {
-      const int xs = (int)(it % spr);
-      const int64_t r = it / spr;
-      const int n = (int)(r / nsy), y0 = (int)(r - (int64_t)n * nsy) * THIN_STRIP;
-      const int x0 = xs * 4, y1 = min(y0 + THIN_STRIP, H);
-      f32x4 win[3][6];
-      load_row(n, y0 - 1, x0, win[0]);
-      load_row(n, y0, x0, win[1]);
-      for (int yy = y0; yy < y1; ++yy) {
-        load_row(n, yy + 1, x0, win[2]);
-        float acc[4][4];
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-#pragma unroll
-          for (int co = 0; co < 4; ++co) acc[p][co] = 0.f;
-#pragma unroll
-        for (int ty = 0; ty < 3; ++ty) {
-          const int sy = yy + ty - 1;
-          if (sy < 0 || sy >= H) continue;
-#pragma unroll
-          for (int tx = 0; tx < 3; ++tx) {
-            f32x4 wt[4];
-            int off = (((3 * ty + tx) * 4) * 16 + q) * 4;
-            asm volatile("" : "+v"(off));
-#pragma unroll
-            for (int e = 0; e < 4; ++e) wt[e] = *(const f32x4*)(wl + off + e * 64);
-#pragma unroll
-            for (int p = 0; p < 4; ++p)
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-#pragma unroll
-                for (int co = 0; co < NCO; ++co)
-                  acc[p][co] = fmaf(win[ty][p + tx][e], wt[e][co], acc[p][co]);
-          }
-        }
-        f32x4 o = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-#pragma unroll
-          for (int co = 0; co < NCO; ++co) {
-            const float sm = row16_sum(acc[p][co]);
-            if (q == 2 * p) o[co] = sm;
-          }
-        if (q < 8) {
-          float* yp = y + ((size_t)(n * H + yy) * W + x0 + (q >> 1)) * COUT + 4 * (q & 1);
-          if constexpr (ACC) {
-            const f32x4 a = *(const f32x4*)yp;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] += a[e];
-          }
-          *(f32x4*)yp = o;
-        }
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-          win[0][c] = win[1][c];
-          win[1][c] = win[2][c];
-        }
-      }
+    for (int c = 0; c < 6; ++c) {
+      const int sx = x0 + c - 1;
+      const bool ok = oky && sx >= 0 && sx < W;
+      dst[c] = ok ? *(const f32x4*)(g + ((size_t)(n * H + sy) * W + sx) * CIN + 4 * q)
+                  : f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    };
-    if (cmask == 0x07) strip(std::integral_constant<int, 3>{});
-    else strip(std::integral_constant<int, 4>{});
-    return;
-  }
-  const int64_t nseg = (int64_t)N * H * (W / 4);
-  for (int64_t seg = (int64_t)blockIdx.x * 16 + (tid >> 4); seg < nseg;
-       seg += (int64_t)gridDim.x * 16) {
-    int n, yy, x0;
-    const int64_t pix0 = thin_seg_origin(seg, H, W, n, yy, x0);
-    float acc[4][4];
+  };
+  // NCO = 3 when output channel 3 is padding too (cmask 0x07, an RGB image): its FMAs are
+  // skipped and it stores +0, what the four-channel form computes from zero weights
+  auto strip = [&](auto nco_c) __attribute__((always_inline)) {
+  constexpr int NCO = decltype(nco_c)::value;
+  for (int64_t it = (int64_t)blockIdx.x * 16 + (tid >> 4); it < nitems;
+       it += (int64_t)gridDim.x * 16) {
+    const int xs = (int)(it % spr);
+    const int64_t r = it / spr;
+    const int n = (int)(r / nsy), y0 = (int)(r - (int64_t)n * nsy) * THIN_STRIP;
+    const int x0 = xs * 4, y1 = min(y0 + THIN_STRIP, H);
+    f32x4 win[3][6];
+    load_row(n, y0 - 1, x0, win[0]);
+    load_row(n, y0, x0, win[1]);
+    for (int yy = y0; yy < y1; ++yy) {
+      load_row(n, yy + 1, x0, win[2]);
+      float acc[4][4];
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+      for (int p = 0; p < 4; ++p)
 #pragma unroll
-      for (int co = 0; co < 4; ++co) acc[p][co] = 0.f;
+        for (int co = 0; co < 4; ++co) acc[p][co] = 0.f;
 #pragma unroll
-    for (int ty = 0; ty < 3; ++ty) {
-      const int sy = yy + ty - 1;
-      if (sy < 0 || sy >= H) continue;
-      f32x4 gr[6];
+      for (int ty = 0; ty < 3; ++ty) {
+        const int sy = yy + ty - 1;
+        if (sy < 0 || sy >= H) continue;
 #pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        const int sx = x0 + c - 1;
-        const bool ok = sx >= 0 && sx < W;
-        gr[c] = ok ? *(const f32x4*)(g + ((size_t)(n * H + sy) * W + sx) * CIN + 4 * q)
-                   : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int tx = 0; tx < 3; ++tx) {
-        f32x4 wt[4];  // this tap's weights [e][co]
-        if constexpr (LDSW) {
-          // an opaque lane offset per tap keeps the reads inside the segment loop (hoisted out of
-          // it they would be the 144 VGPRs again)
+        for (int tx = 0; tx < 3; ++tx) {
+          f32x4 wt[4];
           int off = (((3 * ty + tx) * 4) * 16 + q) * 4;
           asm volatile("" : "+v"(off));
 #pragma unroll
           for (int e = 0; e < 4; ++e) wt[e] = *(const f32x4*)(wl + off + e * 64);
-        } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            wt[e] = f32x4{wv[3 * ty + tx][e][0], wv[3 * ty + tx][e][1], wv[3 * ty + tx][e][2],
-                          wv[3 * ty + tx][e][3]};
+          for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+              for (int co = 0; co < NCO; ++co)
+                acc[p][co] = fmaf(win[ty][p + tx][e], wt[e][co], acc[p][co]);
         }
-#pragma unroll
-        for (int p = 0; p < 4; ++p)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int co = 0; co < 4; ++co)
-              acc[p][co] = fmaf(gr[p + tx][e], wt[e][co], acc[p][co]);
       }
-    }
-    // lanes 2p, 2p + 1 of the group write pixel p's channels 0–3 / 4–7 (zero, or unchanged)
-    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+      f32x4 o = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+      for (int p = 0; p < 4; ++p)
 #pragma unroll
-      for (int co = 0; co < 4; ++co) {
-        const float s = row16_sum(acc[p][co]);
-        if (q == 2 * p) o[co] = s;
+        for (int co = 0; co < NCO; ++co) {
+          const float sm = row16_sum(acc[p][co]);
+          if (q == 2 * p) o[co] = sm;
+        }
+      if (q < 8) {
+        float* yp = y + ((size_t)(n * H + yy) * W + x0 + (q >> 1)) * COUT + 4 * (q & 1);
+        if constexpr (ACC) {
+          const f32x4 a = *(const f32x4*)yp;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[e] += a[e];
+        }
+        *(f32x4*)yp = o;
       }
-    if (q < 8) {
-      float* yp = y + (size_t)(pix0 + (q >> 1)) * COUT + 4 * (q & 1);
-      if constexpr (ACC) {
-        const f32x4 a = *(const f32x4*)yp;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] += a[e];
+      for (int c = 0; c < 6; ++c) {
+        win[0][c] = win[1][c];
+        win[1][c] = win[2][c];
       }
-      *(f32x4*)yp = o;
     }
   }
+  };
+  if (cmask == 0x07) strip(std::integral_constant<int, 3>{});
+  else strip(std::integral_constant<int, 4>{});
 }
 
 // 32 → 32 layers: 2-byte type, one group, stride 1, 3×3 pad 1, identity placement, W % 16 == 0,
@@ -880,49 +703,23 @@ int launch_conv_thin(ConvK& k, int dtype, hipStream_t st) {
   const int grid = grid_for((int64_t)a.N * a.H * (a.W / 16));  // ≤ 8 waves per SIMD
   if (dtype == MIA_F32) {  // the fp32 VALU kernels (one pixel per thread / per 16 threads)
     const int64_t npix = (int64_t)a.N * a.H * a.W;
-    // T_THIN_F32: 0 = the round-2 launches (8 waves per CU, gradient weights in VGPRs); 1 =
-    // 16 waves per CU for the forward (112 VGPRs: 4 per SIMD fit), LDS weights + 20 waves per CU (82 VGPRs: 5 per SIMD)
-    // for the gradient; 2 = mode 1 with the forward's loads hoisted (thin_in_f32_body HOIST, held
-    // to 128 VGPRs: 16 waves per CU); 3 = mode 2 with the gradient's sliding-window row strips
-    const int mode = tune(T_THIN_F32);
-    const int wpc_in = mode ? 16 : 8, wpc_out = mode ? 20 : 8;
-    const int grid_out = grid_for(npix / 16, mode == 3 ? 12 : wpc_out);  // 3: 144 VGPRs
-    const int gen_blocks = std::min(grid_out, grid_for(npix / 16, 8));  // the general path's grid
+    // the forward at 16 waves per CU (held to 128 VGPRs: 4 per SIMD), the gradient strips at
+    // 12 (144 VGPRs); the gradient's general path (real output channels ≥ 4) runs on the first
+    // gen_blocks blocks only
+    const int grid_out = grid_for(npix / 16, 12);
+    const int gen_blocks = std::min(grid_out, grid_for(npix / 16, 8));
     if (a.Cin == 8) {
-      if (mode >= 2)
-        hipLaunchKernelGGL(conv_thin_in_f32_kernel<true>, dim3(grid_for(npix / 16, 16)), dim3(256),
-                           0, st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, a.bias,
-                           a.act_out, a.act_slope, (float*)a.y, a.N, a.H, a.W);
-      else
-        hipLaunchKernelGGL(conv_thin_in_f32_kernel<false>, dim3(grid_for(npix / 16, wpc_in)),
-                           dim3(256), 0, st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad,
-                           a.bias, a.act_out, a.act_slope, (float*)a.y, a.N, a.H, a.W);
+      hipLaunchKernelGGL(conv_thin_in_f32_kernel, dim3(grid_for(npix / 16, 16)), dim3(256), 0, st,
+                         (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, a.bias,
+                         a.act_out, a.act_slope, (float*)a.y, a.N, a.H, a.W);
     } else if (a.accumulate) {
-      if (mode == 3)
-        hipLaunchKernelGGL((conv_thin_out_f32_kernel<true, true, true>), dim3(grid_out), dim3(256),
-                           0, st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad,
-                           (float*)a.y, a.N, a.H, a.W, gen_blocks);
-      else if (mode)
-        hipLaunchKernelGGL((conv_thin_out_f32_kernel<true, true>), dim3(grid_out), dim3(256), 0, st,
-                           (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
-                           a.N, a.H, a.W, gen_blocks);
-      else
-        hipLaunchKernelGGL((conv_thin_out_f32_kernel<true, false>), dim3(grid_out), dim3(256), 0,
-                           st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
-                           a.N, a.H, a.W, gen_blocks);
+      hipLaunchKernelGGL(conv_thin_out_f32_kernel<true>, dim3(grid_out), dim3(256), 0, st,
+                         (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
+                         a.N, a.H, a.W, gen_blocks);
     } else {
-      if (mode == 3)
-        hipLaunchKernelGGL((conv_thin_out_f32_kernel<false, true, true>), dim3(grid_out), dim3(256),
-                           0, st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad,
-                           (float*)a.y, a.N, a.H, a.W, gen_blocks);
-      else if (mode)
-        hipLaunchKernelGGL((conv_thin_out_f32_kernel<false, true>), dim3(grid_out), dim3(256), 0,
-                           st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
-                           a.N, a.H, a.W, gen_blocks);
-      else
-        hipLaunchKernelGGL((conv_thin_out_f32_kernel<false, false>), dim3(grid_out), dim3(256), 0,
-                           st, (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
-                           a.N, a.H, a.W, gen_blocks);
+      hipLaunchKernelGGL(conv_thin_out_f32_kernel<false>, dim3(grid_out), dim3(256), 0, st,
+                         (const float*)a.x, (const float*)k.g[0].w, k.g[0].kpad, (float*)a.y,
+                         a.N, a.H, a.W, gen_blocks);
     }
     return check_launch("conv_thin_f32");
   }
@@ -933,19 +730,11 @@ int launch_conv_thin(ConvK& k, int dtype, hipStream_t st) {
                            (const T*)a.x, (const T*)k.g[0].w, k.g[0].kpad, a.bias, a.act_out,
                            a.act_slope, (T*)a.y, a.N, a.H, a.W);
       } else {
-#ifdef MIA_THIN_OUT_RS2
-        const int64_t items = (int64_t)a.N * ((a.H + THIN_RS - 1) / THIN_RS) * (a.W / 16);
-        const int lds = 4 * 2 * THIN_WBUF;
-        hipLaunchKernelGGL((conv_thin_out_kernel<T, 8>), dim3(grid_for(items, 16)), dim3(256),
-                           lds, st, (const T*)a.x, (const T*)k.g[0].w, k.g[0].kpad, (T*)a.y,
-                           a.accumulate, a.N, a.H, a.W);
-#else
         const int64_t items = (int64_t)a.N * ((a.H + THIN_SR - 1) / THIN_SR) * (a.W / 16);
         const int lds = 4 * THIN_RING * THIN_SLOT;  // 48 KB: 3 blocks per CU
         hipLaunchKernelGGL((conv_thin_out_strip_kernel<T, 8>), dim3(grid_for(items, 12)),
                            dim3(256), lds, st, (const T*)a.x, (const T*)k.g[0].w, k.g[0].kpad,
                            (T*)a.y, a.accumulate, a.N, a.H, a.W);
-#endif
       }
       return check_launch("conv_thin");
     }

@@ -357,13 +357,7 @@ static int launch_upconv_halo(UpK& k, hipStream_t st) {
   if (PRO) lds += (size_t)k.Cin * sizeof(T);
   if (lds > 160 * 1024) return set_error("upconv_halo: LDS budget exceeded");
   auto fn = upconv_halo_kernel<T, PRO, DG, BN_>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
-      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-    attr_set = true;
-  }
+  if (const int rc = ensure_dyn_lds((const void*)fn, 160 * 1024); rc != MIA_OK) return rc;
   hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), lds, st, k);
   return check_launch("upconv_halo");
 }
@@ -933,13 +927,7 @@ static int launch_upconv_x6s(UpK& k, hipStream_t st) {
   k.nbn = k.Cout / TL::BN;
   k.nblk = k.N * (k.R / TL::PH) * (k.R / TL::PW) * k.nbn;
   auto fn = upconv_x6s_kernel<DG, PRO>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            80 * 1024) != hipSuccess)
-      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-    attr_set = true;
-  }
+  if (const int rc = ensure_dyn_lds((const void*)fn, 80 * 1024); rc != MIA_OK) return rc;
   hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), TL::LDS, st, k);
   return check_launch("upconv_x6s");
 }
@@ -950,13 +938,7 @@ static int launch_upconv_x6_e(UpK& k, hipStream_t st) {
   k.nbn = k.Cout / TL::BN;
   k.nblk = k.N * (k.R / TL::PH) * (k.R / TL::PW) * k.nbn;
   auto fn = upconv_x6_kernel<DG, PRO, EARLY, PRIO>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
-      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-    attr_set = true;
-  }
+  if (const int rc = ensure_dyn_lds((const void*)fn, 160 * 1024); rc != MIA_OK) return rc;
   hipLaunchKernelGGL(fn, dim3(k.nblk), dim3(TL::NT), TL::LDS, st, k);
   return check_launch("upconv_x6");
 }

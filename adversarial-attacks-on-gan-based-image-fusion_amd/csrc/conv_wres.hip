@@ -238,13 +238,7 @@ __global__ __launch_bounds__(TL::NT, 1) void conv_wres_kernel(const ConvK k) {
 template <typename T, typename TL, int EPI>
 static int launch_wres_(ConvK& k, int grid, size_t lds, hipStream_t st) {
   auto fn = conv_wres_kernel<T, TL, EPI>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024) != hipSuccess)
-      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-    attr_set = true;
-  }
+  if (const int rc = ensure_dyn_lds((const void*)fn, 160 * 1024); rc != MIA_OK) return rc;
   RedQ r;
   int rc = conv_red_begin(k, r,
                           halo_red_slots(k.a.H, k.a.W, TL::FM, TL::WM, k.prered), st);
@@ -282,13 +276,7 @@ bool conv_wres_eligible(const ConvK& k, int dtype) {
 
 template <typename TL>
 static int launch_conv_wres_t(ConvK& k, int dtype, hipStream_t st) {
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      ncu = 256;
-  }
+  const int ncu = device_cu_count();
   const int ntiles = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW);
   const int per = (ntiles + ncu - 1) / ncu;
   const int grid = (ntiles + per - 1) / per;  // contiguous runs: every block gets a non-empty one
@@ -298,7 +286,7 @@ static int launch_conv_wres_t(ConvK& k, int dtype, hipStream_t st) {
   const int f = epi_mask(k);
   const int naux = (f & TAP) ? 2 : ((f & MASK) ? 1 : 0) + ((f & ACC) ? 1 : 0);
   const size_t lds = 2 * (size_t)TL::HBUF + (size_t)TL::NW * naux * TL::AUXW + 3 * TL::WM * 64 * 4;
-  k.prered = prered_enabled() && (f & CSUM);
+  k.prered = (f & CSUM);
   MIA_DISPATCH_DTYPE(dtype, T, {
     if constexpr (sizeof(T) == 2) {
       switch (f) {
@@ -620,23 +608,21 @@ template <typename T, bool PRO, int EPI>
 static int launch_wres32_(ConvK& k, hipStream_t st) {
   typedef Wres32Tile TL;
   auto fn = conv_wres32_kernel<T, PRO, EPI>;
-  static int per_cu = 0;
-  if (!per_cu) {
-    int dev = 0, ncu = 0, occ = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      ncu = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void*)fn, TL::NT, TL::LDS) !=
-            hipSuccess || occ < 1)
-      occ = 1;
-    per_cu = ncu * occ;
-  }
+  // blocks per CU of this instantiation (a thread-safe function-local static), × the device's CUs
+  static const int occ = [&] {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, (const void*)fn, TL::NT, TL::LDS) !=
+            hipSuccess || o < 1)
+      o = 1;
+    return o;
+  }();
+  const int per_cu = device_cu_count() * occ;
   const int ntiles = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW);
   const int grid = std::min(ntiles, per_cu);
   k.nbn = 1;
   k.nblk = ntiles;
   constexpr bool RED = (EPI & (epi::SDOT | epi::BAB | epi::CSUM)) != 0;
-  k.prered = RED && prered_enabled();
+  k.prered = RED;
   RedQ r;
   int rc = conv_red_begin(k, r, halo_red_slots(k.a.H, k.a.W, TL::FM, TL::NW, k.prered), st);
   if (rc != MIA_OK) return rc;

@@ -448,16 +448,8 @@ static int launch_wres128_(ConvK& k, hipStream_t st) {
   constexpr int LDS = 2 * TL::HBUF + TL::NW * (TL::CHB + TL::NZB + (AUXX ? TL::AXB : 0));
   static_assert(LDS <= 160 * 1024, "LDS budget");
   auto fn = conv_wres128_kernel<T, CIN, EPI, COUT>;
-  static int ncu = 0;
-  if (!ncu) {
-    if (hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, LDS) !=
-        hipSuccess)
-      return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      ncu = 256;
-  }
+  if (const int rc = ensure_dyn_lds((const void*)fn, LDS); rc != MIA_OK) return rc;
+  const int ncu = device_cu_count();
   const int ntiles = k.a.N * (k.a.H / TL::PH) * (k.a.W / TL::PW);
   // Cout = nct column tiles of BN channels, each over the CUs' share of contiguous patch runs
   const int nct = k.a.Cout / TL::BN, share = std::max(1, ncu / nct);

@@ -71,6 +71,12 @@ __device__ __forceinline__ float wave_sum(float v) {
 int set_error(const std::string& msg);
 int check_launch(const char* what);
 
+// Per-device launch facts, thread-safe (reduce.hip): the current device's CU count (cached per
+// device), and hipFuncSetAttribute(MaxDynamicSharedMemorySize, bytes) applied once per (kernel,
+// device) — the launchers' lazy initialisation, safe for several host threads and devices.
+int device_cu_count();
+int ensure_dyn_lds(const void* fn, int bytes);
+
 // Kernel-variant switches (tests' bitwise A/B comparisons and the tuning tools; the product path
 // never changes them): read ONCE from the environment (MIA_<NAME>=value) at first use, then only
 // through mia_set_tuning() — no getenv on the launch path. The defaults are the measured-best
@@ -90,12 +96,8 @@ enum TuneKey {
   T_S2DG_HALO,       // 0: the stride-2 input gradients as 4 sub-pixel phase GEMMs
   T_UPCONV_X6,       // 0: the fp32 up-conv forward on the on-the-fly split kernel
   T_UPCONV_HALO,     // 0: the up-conv forward as 4 sub-pixel phase GEMMs
-  T_EPI_PRERED,      // 0: no LDS pre-reduction of the channel sums in the register epilogues
   T_CONV_WRES32,     // 0: the 32 → 32 layers on the global-gather kernel (conv_thin32)
   T_HALO_C64,        // Cout = 64 (2-byte types) on the 64-channel halo tile: 1 (default), 0 never
-  T_THIN_F32,        // fp32 thin layers: 3 (default) + sliding-window gradient strips, 2 hoisted
-                     // forward loads, 1 more waves + LDS gradient weights, 0 round 2
-                     // (profiles/r03_thin_f32_ab.txt)
   T_X6_64S,          // fp32 Cout = 64: 1 (default) the two-blocks-per-CU x6 tile (conv_halo_x6.hip
                      // HaloX6S, also the VGG tap-pair gradient), 0 the 8-wave 64-column tile
   T_UPCONV_X6S,      // fp32 split-once stride-2 input gradient with Cin ≤ 512: 1 (default) the

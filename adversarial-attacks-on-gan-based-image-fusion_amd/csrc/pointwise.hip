@@ -1192,6 +1192,23 @@ extern "C" int mia_tap_grad(const void* a, const void* t, void* g, int64_t len, 
   return MIA_OK;
 }
 
+extern "C" int mia_mse_fwd_bwd(const void* a, const void* b, float* loss, void* g, int n,
+                               int64_t len, float coef_loss, float coef_grad, int accumulate,
+                               int dtype, void* stream) {
+  MIA_CHECK_ARG(a && b && (loss || g) && n > 0 && len > 0, "bad args");
+  MIA_CHECK_ARG(!g || dtype == MIA_F32 || !accumulate,
+                "accumulating gradient is fp32 only (mia_mse_grad_f32)");
+  if (loss) {
+    const int rc = mia_mse_sum(a, b, loss, n, len, coef_loss, dtype, stream);
+    if (rc != MIA_OK) return rc;
+  }
+  if (!g) return MIA_OK;
+  if (dtype == MIA_F32)
+    return mia_mse_grad_f32((const float*)a, (const float*)b, (float*)g, (int64_t)n * len,
+                            coef_grad, accumulate, stream);
+  return mia_tap_grad(a, b, g, (int64_t)n * len, coef_grad, 0, dtype, stream);
+}
+
 extern "C" int mia_image_grad(const float* rec, const float* t, const void* g_vgg, float* g_img,
                               int N, int S, int pf, int cpad, float coef, int dtype, void* stream) {
   MIA_CHECK_ARG(rec && t && g_img && pf >= 1 && S % pf == 0, "bad args");

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
+#include <vector>
 
 #include "mia_common.h"
 
@@ -33,8 +34,8 @@ TuneDef g_tune[T_NKEYS] = {
     {"MIA_CONV_THIN", 1}, {"MIA_CONV_THIN32", 1},   {"MIA_CONV_WRES", 1},
     {"MIA_CONV_REGEPI", 1},   {"MIA_CONV_SMALLTILE", 512},
     {"MIA_S2DG_X6", 1},   {"MIA_S2DG_HALO", 1},     {"MIA_UPCONV_X6", 1},   {"MIA_UPCONV_HALO", 1},
-    {"MIA_EPI_PRERED", 1},    {"MIA_CONV_WRES32", 1},
-    {"MIA_HALO_C64", 1},  {"MIA_THIN_F32", 3},      {"MIA_X6_64S", 1},
+    {"MIA_CONV_WRES32", 1},
+    {"MIA_HALO_C64", 1},  {"MIA_X6_64S", 1},
     {"MIA_UPCONV_X6S", 1}, {"MIA_CONV_WRES128", 1}};
 std::once_flag g_tune_once;
 void tune_init() {
@@ -48,6 +49,41 @@ void tune_init() {
 int tune(TuneKey key) {
   std::call_once(g_tune_once, tune_init);
   return g_tune[key].value;
+}
+
+namespace {
+std::mutex g_dev_mu;
+std::unordered_map<int, int> g_ncu;                           // device → CU count
+std::unordered_map<const void*, std::vector<int>> g_lds_set;  // kernel → devices configured
+int current_device() {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  return dev;
+}
+}  // namespace
+
+int device_cu_count() {
+  const int dev = current_device();
+  std::lock_guard<std::mutex> lock(g_dev_mu);
+  auto it = g_ncu.find(dev);
+  if (it != g_ncu.end()) return it->second;
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      ncu <= 0)
+    ncu = 256;  // MI355X
+  g_ncu[dev] = ncu;
+  return ncu;
+}
+
+int ensure_dyn_lds(const void* fn, int bytes) {
+  const int dev = current_device();
+  std::lock_guard<std::mutex> lock(g_dev_mu);
+  std::vector<int>& done = g_lds_set[fn];
+  if (std::find(done.begin(), done.end(), dev) != done.end()) return MIA_OK;
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
+    return set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+  done.push_back(dev);
+  return MIA_OK;
 }
 
 float* red_scratch(hipStream_t st, size_t bytes) {

@@ -96,6 +96,17 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def _die_with_parent():
+    """preexec_fn of the launcher child: PR_SET_PDEATHSIG(SIGTERM), so a SIGKILL of this process
+    (a `timeout -k` escalation skips the signal forwarding below) still ends the launcher, which
+    then terminates its ranks. Runs between fork and exec in the child; no GPU is involved."""
+    import ctypes
+    import signal
+    libc = ctypes.CDLL(None, use_errno=True)
+    PR_SET_PDEATHSIG = 1
+    libc.prctl(PR_SET_PDEATHSIG, int(signal.SIGTERM), 0, 0, 0)
+
+
 def spawn_workers(n, argv):
     """`--gpus N` without a launcher: start the N one-process-per-GPU ranks as ONE child
     (`python -m torch.distributed.run --nproc-per-node N … bench.py <same args>`) and return its
@@ -103,7 +114,8 @@ def spawn_workers(n, argv):
     from an initialised process; the ranks' rank 0 prints the JSON line on the shared stdout.
     The rendezvous store binds its own free port (c10d endpoint 127.0.0.1:0: no probe-then-bind
     race), and SIGTERM / SIGINT to this process are forwarded to the child's process group, so a
-    `timeout` around the bench also ends the launcher and its ranks."""
+    `timeout` around the bench also ends the launcher and its ranks; a SIGKILL of this process
+    reaches the launcher as SIGTERM through its parent-death signal (_die_with_parent)."""
     import signal
     import subprocess
     import uuid
@@ -113,7 +125,7 @@ def spawn_workers(n, argv):
            os.path.abspath(__file__), *argv]
     log(f"spawning {n} ranks: {' '.join(cmd[1:5])} …")
     child = subprocess.Popen(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"),
-                             start_new_session=True)
+                             start_new_session=True, preexec_fn=_die_with_parent)
 
     def forward(signum, _frame):
         try:

@@ -239,6 +239,13 @@ int mia_vgg_conv_relu_fwd(const void* x, const void* w, const float* bias, void*
 int mia_vgg_conv_dgrad(const void* g, const void* w_t, void* gx, int N, int H, int W, int Cin_g,
                        int Cout_g, int Kpad, const void* tap_a, const void* tap_t,
                        float tap_coef, const void* mask_a, int dtype, void* stream);
+/* The SURVEY.md §8(b) name of mia_vgg_conv_dgrad (same arguments, same result): the input
+ * gradient of a VGG conv3x3 + bias + ReLU block, the ReLU mask of the layer below (mask_a, its
+ * stored post-ReLU output) and the tap-MSE term (tap_a, tap_t, tap_coef) fused in the epilogue.
+ * Replaces: autograd through code/vgg.py:45-62 and interpolation.py:786-817. */
+int mia_vgg_conv_relu_dgrad(const void* g, const void* w_t, void* gx, int N, int H, int W,
+                            int Cin_g, int Cout_g, int Kpad, const void* tap_a, const void* tap_t,
+                            float tap_coef, const void* mask_a, int dtype, void* stream);
 
 /* Up-sampling StyledConv [ext] as conv_transpose2d(stride 2, pad 0) → Blur (algorithmic FLOPs:
  * 9·Cin·Cout MACs per INPUT pixel). The transposed conv runs as four sub-pixel phase GEMMs in one
@@ -348,6 +355,13 @@ int mia_mse_sum(const void* a, const void* b, float* loss, int n, int64_t len, f
 /* K10 gradient for flat fp32 tensors: g (+)= coef·(a − b). */
 int mia_mse_grad_f32(const float* a, const float* b, float* g, int64_t len, float coef,
                      int accumulate, void* stream);
+/* The SURVEY.md §8(b) K10 pair in one call: loss[i] (+)= coef_loss·Σ_j (a − b)[i][j]² over the n
+ * rows of len elements (mia_mse_sum; loss may be NULL) and g (+)= coef_grad·(a − b) (g may be
+ * NULL; fp32: mia_mse_grad_f32, accumulate allowed; fp16 / bf16: mia_tap_grad without a mask,
+ * accumulate = 0 only, else MIA_ERR_ARG). Replaces: F.mse_loss(reduction='mean') and its autograd
+ * backward (interpolation.py:786-817; coef_loss = 1/len, coef_grad = 2/len for a mean). */
+int mia_mse_fwd_bwd(const void* a, const void* b, float* loss, void* g, int n, int64_t len,
+                    float coef_loss, float coef_grad, int accumulate, int dtype, void* stream);
 /* Tap-MSE seed for the deepest VGG tap: g = coef·(a − t)·[a > 0 if mask] (dtype, flat). */
 int mia_tap_grad(const void* a, const void* t, void* g, int64_t len, float coef, int mask,
                  int dtype, void* stream);

@@ -13,14 +13,20 @@ class StubEngine:
     bench.py reports."""
 
     def __init__(self, rank):
+        import os
         self.rank = rank
+        pid_dir = os.environ.get("STUB_PID_DIR")
+        if pid_dir:  # test_bench_parent_sigkill_ends_ranks: which processes must not outlive it
+            with open(os.path.join(pid_dir, f"rank{rank}.pid"), "w") as f:
+                f.write(f"{os.getpid()} {os.getppid()}\n")
+        self.sleep = float(os.environ.get("STUB_SLEEP_S", "0"))
         self.status_rounds = 0
         self.G = types.SimpleNamespace(flops_fwd_per_image=10.0)
         self.V = types.SimpleNamespace(flops_fwd_per_image=1.0)
         self.E = types.SimpleNamespace(flops_fwd_per_image=3.0)
 
     def run(self, x0, t, steps, eps, alpha, group=None):
-        time.sleep(0.05 * (1 + self.rank))
+        time.sleep(self.sleep or 0.05 * (1 + self.rank))
         if group is not None:
             import gfa_import  # noqa: F401
             from gfa_amd import pgd

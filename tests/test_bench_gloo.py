@@ -122,3 +122,58 @@ def test_bench_rejects_world_mismatch():
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=240,
                        cwd=ROOT)
     assert p.returncode != 0 and "WORLD_SIZE=1" in p.stderr
+
+
+def _alive(pid):
+    """True while `pid` exists and is not a zombie (a container's PID 1 may never reap it)."""
+    try:
+        with open(f"/proc/{pid}/status") as f:
+            for ln in f:
+                if ln.startswith("State:"):
+                    return "Z" not in ln.split()[1]
+    except OSError:
+        return False
+    return False
+
+
+def test_bench_parent_sigkill_ends_ranks(tmp_path):
+    """advisor r05: `python bench.py --gpus 2` puts its launcher child in a session of its own,
+    so a SIGKILL of the parent (`timeout -k`) skips the signal forwarding. The launcher's
+    parent-death signal must still end it and every rank."""
+    import signal
+    import time
+    env = _clean_env()
+    env.update(STUB_PID_DIR=str(tmp_path), STUB_SLEEP_S="120")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "cpu",
+           "--engine-factory", "bench_stub:make_engine", "--steps", "1", "--warmup", "1",
+           "--batch", "2", "--size", "16", "--no-roofline", "--no-cpu-baseline"]
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                         cwd=ROOT)
+    pids = []
+    try:
+        t0 = time.time()
+        while time.time() - t0 < 120:
+            files = sorted(tmp_path.glob("rank*.pid"))
+            if len(files) == 2 and all(f.read_text().endswith("\n") for f in files):
+                break
+            assert p.poll() is None, "bench exited before its ranks started"
+            time.sleep(0.2)
+        else:
+            raise AssertionError("ranks did not start")
+        for f in files:
+            pid, ppid = map(int, f.read_text().split())
+            pids += [pid, ppid]  # the rank and its launcher (torch.distributed.run)
+        pids = sorted(set(pids))
+        assert all(_alive(q) for q in pids)
+        p.send_signal(signal.SIGKILL)
+        p.wait(timeout=30)
+        t0 = time.time()
+        while time.time() - t0 < 60 and any(_alive(q) for q in pids):
+            time.sleep(0.2)
+        assert not any(_alive(q) for q in pids), [q for q in pids if _alive(q)]
+    finally:
+        for q in pids:
+            if _alive(q):
+                os.kill(q, signal.SIGKILL)
+        if p.poll() is None:
+            p.kill()

@@ -812,13 +812,12 @@ def test_conv_thin_vgg_input_layer(cuda, tune, dtype, N, H, W, thin, e4e):
 
 @pytest.mark.parametrize("N,H,W", [(2, 32, 48), (1, 17, 16), (9, 256, 256)])
 @pytest.mark.parametrize("creal", [3, 8])
-def test_conv_thin_f32_launch_modes_bitwise(cuda, tune, N, H, W, creal):
-    """The fp32 VALU thin kernels' launch modes (MIA_THIN_F32: 3 = mode 2 with the gradient's
-    sliding-window row strips, 2 = mode 1 with the forward's input
-    loads hoisted, 1 = 16 / 20 waves per CU with the gradient weights in LDS, 0 = the round-2
-    launches) run the same FMAs in the same order: the forward, the plain gradient and the
-    accumulating gradient are bit-identical. creal = 8: every padded channel real (the general
-    gradient path, one pixel per thread)."""
+def test_conv_thin_f32_vs_fp64(cuda, N, H, W, creal):
+    """The fp32 VALU thin kernels (forward 8 → 64 + bias + ReLU; the 64 → 8 input gradient on
+    row strips, plain and accumulating) against fp64 torch: fp32 FMAs, so ≤ 1e-5 norm-relative;
+    the accumulating form equals base + the plain gradient bit for bit (one fp32 add). creal = 8:
+    every padded channel real (the gradient's general path, one pixel per thread). Round 6
+    replaces the bitwise comparison of the removed launch modes (MIA_THIN_F32 0–2)."""
     g = torch.Generator().manual_seed(7 * N + H + W)
     x = torch.zeros(N, 8, H, W)
     x[:, :creal] = torch.rand(N, creal, H, W, generator=g) * 2 - 1
@@ -829,20 +828,20 @@ def test_conv_thin_f32_launch_modes_bitwise(cuda, tune, N, H, W, creal):
     xin, gin = nhwc(x, torch.float32).to(cuda), nhwc(gout, torch.float32).to(cuda)
     wf = layouts.fwd_matrix(w, torch.float32, cin_pad=8).to(cuda)
     wd = layouts.dgrad_matrix(w, torch.float32, cin_pad=8).to(cuda)
-    outs = []
-    for mode in ("0", "1", "2", "3"):
-        tune("MIA_THIN_F32", mode)
-        y = torch.empty(N, H, W, 64, device=cuda)
-        ops.conv3x3(xin, wf, y, cout=64, bias=b.to(cuda), act_out=ops.ACT_RELU)
-        gx = torch.empty(N, H, W, 8, device=cuda)
-        ops.conv3x3(gin, wd, gx, cout=8)
-        ga = base.clone()
-        ops.conv3x3(gin, wd, ga, cout=8, accumulate=True)
-        torch.cuda.synchronize()
-        outs.append((y, gx, ga))
-    for other in outs[1:]:
-        for a, b_ in zip(outs[0], other):
-            assert torch.equal(a, b_)
+    y = torch.empty(N, H, W, 64, device=cuda)
+    ops.conv3x3(xin, wf, y, cout=64, bias=b.to(cuda), act_out=ops.ACT_RELU)
+    gx = torch.empty(N, H, W, 8, device=cuda)
+    ops.conv3x3(gin, wd, gx, cout=8)
+    ga = base.clone()
+    ops.conv3x3(gin, wd, ga, cout=8, accumulate=True)
+    torch.cuda.synchronize()
+    wp = torch.zeros(64, 8, 3, 3, dtype=torch.float64)
+    wp[:, :creal] = w.double()
+    y_ref = torch.relu(F.conv2d(x.double(), wp, b.double(), padding=1))
+    gx_ref = F.conv_transpose2d(gout.double(), wp, padding=1)
+    assert rel_err(nchw(y), y_ref) < 1e-5
+    assert rel_err(nchw(gx), gx_ref) < 1e-5
+    assert torch.equal(ga, base + gx)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
@@ -1654,3 +1653,59 @@ def test_wres128_cout256_column_tiles(cuda, tune, dtype, cin, N, R, W, mode):
     assert e < 2 * TOL[dtype]
     if R % 16 == 0:
         assert rel_err(nchw(y), nchw(y_halo).double()) < 2 * TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_survey_named_aliases(cuda, dtype):
+    """The SURVEY.md §8(b) names (round 6): mia_vgg_conv_relu_dgrad equals mia_vgg_conv_dgrad bit
+    for bit and both match fp64 torch (conv_transpose + tap-MSE term + ReLU mask of the layer
+    below); mia_mse_fwd_bwd equals mia_mse_sum + mia_mse_grad_f32 / mia_tap_grad bit for bit."""
+    g = torch.Generator().manual_seed(61)
+    N, H, W, cin, cout = 2, 16, 32, 64, 128
+    w = torch.randn(cout, cin, 3, 3, generator=g) / math.sqrt(9 * cin)
+    gy = torch.randn(N, cout, H, W, generator=g)
+    tap_a = torch.relu(torch.randn(N, cin, H, W, generator=g))  # the layer below's post-ReLU
+    tap_t = torch.randn(N, cin, H, W, generator=g)
+    coef = 0.37
+    wd = layouts.dgrad_matrix(w, dtype).to(cuda)
+    kpad = wd.shape[1]
+    gin, ta, tt = (nhwc(t, dtype).to(cuda) for t in (gy, tap_a, tap_t))
+    outs = []
+    for name in ("mia_vgg_conv_dgrad", "mia_vgg_conv_relu_dgrad"):
+        gx = torch.empty(N, H, W, cin, dtype=dtype, device=cuda)
+        ops.call(name, ops.ptr(gin), ops.ptr(wd), ops.ptr(gx), N, H, W, cout, cin, kpad,
+                 ops.ptr(ta), ops.ptr(tt), coef, ops.ptr(ta), ops.dt(dtype), ops.stream())
+        outs.append(gx)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    rd = lambda t: t.to(dtype).double()  # noqa: E731  (the operands as the device holds them)
+    ref = F.conv_transpose2d(rd(gy), rd(w), padding=1) + coef * (rd(tap_a) - rd(tap_t))
+    ref = ref * (rd(tap_a) > 0)
+    assert rel_err(nchw(outs[1]), ref) < (2e-5 if dtype == torch.float32 else 2e-2)
+
+    n, L = 3, 5000
+    a = torch.randn(n, L, generator=g).to(dtype).to(cuda)
+    b = torch.randn(n, L, generator=g).to(dtype).to(cuda)
+    base = torch.randn(n, L, generator=g).to(dtype).to(cuda)
+    l1 = torch.full((n,), 0.5, device=cuda)
+    l2 = l1.clone()
+    g1, g2 = base.clone(), base.clone()
+    acc = int(dtype == torch.float32)
+    ops.call("mia_mse_fwd_bwd", ops.ptr(a), ops.ptr(b), ops.ptr(l1), ops.ptr(g1), n, L,
+             1.0 / L, 2.0 / L, acc, ops.dt(dtype), ops.stream())
+    ops.call("mia_mse_sum", ops.ptr(a), ops.ptr(b), ops.ptr(l2), n, L, 1.0 / L, ops.dt(dtype),
+             ops.stream())
+    if dtype == torch.float32:
+        ops.call("mia_mse_grad_f32", ops.ptr(a), ops.ptr(b), ops.ptr(g2), n * L, 2.0 / L, 1,
+                 ops.stream())
+    else:
+        ops.call("mia_tap_grad", ops.ptr(a), ops.ptr(b), ops.ptr(g2), n * L, 2.0 / L, 0,
+                 ops.dt(dtype), ops.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(l1, l2) and torch.equal(g1, g2)
+    ref_l = 0.5 + ((a.double() - b.double()) ** 2).mean(dim=1)
+    assert torch.allclose(l1.double(), ref_l, rtol=1e-5)
+    if dtype != torch.float32:  # a 2-byte gradient cannot accumulate (fp32 only)
+        with pytest.raises(_lib.MiaError, match="fp32 only"):
+            ops.call("mia_mse_fwd_bwd", ops.ptr(a), ops.ptr(b), ops.ptr(l1), ops.ptr(g1), n, L,
+                     1.0 / L, 2.0 / L, 1, ops.dt(dtype), ops.stream())

@@ -35,8 +35,8 @@ int main() {
   const char* keys[] = {"MIA_CONV_HALO", "MIA_CONV_X6", "MIA_HALO_EPI", "MIA_X6_UNR",
                         "MIA_CONV_WRES128", "MIA_CONV_THIN", "MIA_CONV_THIN32", "MIA_CONV_WRES",
                         "MIA_CONV_REGEPI", "MIA_CONV_SMALLTILE", "MIA_S2DG_X6",
-                        "MIA_S2DG_HALO", "MIA_UPCONV_X6", "MIA_UPCONV_HALO", "MIA_EPI_PRERED",
-                        "MIA_CONV_WRES32", "MIA_HALO_C64", "MIA_THIN_F32", "MIA_X6_64S", "MIA_UPCONV_X6S"};
+                        "MIA_S2DG_HALO", "MIA_UPCONV_X6", "MIA_UPCONV_HALO",
+                        "MIA_CONV_WRES32", "MIA_HALO_C64", "MIA_X6_64S", "MIA_UPCONV_X6S"};
   for (const char* k : keys) {
     int v = -1, w = -1;
     EXPECT(mia_get_tuning(k, &v) == MIA_OK, k);
@@ -45,6 +45,8 @@ int main() {
   }
   int v = 0;
   expect_error(mia_get_tuning("MIA_NO_SUCH_SWITCH", &v), "unknown switch");
+  expect_error(mia_get_tuning("MIA_THIN_F32", &v), "removed switch");  // round 6
+  expect_error(mia_get_tuning("MIA_EPI_PRERED", &v), "removed switch");
   expect_error(mia_set_tuning(nullptr, 1), "null switch");
   expect_error(mia_get_tuning("MIA_CONV_X6", nullptr), "null out");
   std::string longname(5000, 'x');  // the error string grows to hold it
@@ -96,6 +98,11 @@ int main() {
   expect_error(mia_ssim2(dummy, dummy, 4, 64, 64, 2.f, (double*)dummy, 8 * 4, dummy, nullptr),
                "ssim work size");  // the round-3 contract (N doubles) is rejected
   expect_error(mia_gemm_f32_grouped(nullptr, 0, nullptr), "gemm groups");
+  // the §8(b)-named K10 pair (round 6): nothing to write, or a 2-byte accumulating gradient
+  expect_error(mia_mse_fwd_bwd(dummy, dummy, nullptr, nullptr, 1, 64, 1.f, 1.f, 0, MIA_F32,
+                               nullptr), "mse_fwd_bwd no output");
+  expect_error(mia_mse_fwd_bwd(dummy, dummy, dummy, dummy, 1, 64, 1.f, 1.f, 1, MIA_F16, nullptr),
+               "mse_fwd_bwd fp16 accumulate");
   expect_error(mia_reserve_reduction_scratch(-1, nullptr), "scratch negative");
   EXPECT(mia_reserve_reduction_scratch(0, nullptr) == MIA_OK, "scratch zero");
 

@@ -31,8 +31,12 @@ def main():
     ap.add_argument("--dtype", default="fp16", choices=["fp16", "bf16", "fp32"])
     a = ap.parse_args()
     if os.environ.get("E4E_MERGE_BELOW_TILES"):  # A/B of the merged first head convs (e4e.py)
+        # the threshold of the dtype being run (fp32 reads MERGE_BELOW_TILES, 2-byte types
+        # MERGE_BELOW_TILES_2B); "1e9" (merge every head) parses as well as an integer
         import gfa_amd.e4e as e4e_mod
-        e4e_mod.MERGE_BELOW_TILES = int(os.environ["E4E_MERGE_BELOW_TILES"])
+        lim = int(float(os.environ["E4E_MERGE_BELOW_TILES"]))
+        setattr(e4e_mod, "MERGE_BELOW_TILES" if a.dtype == "fp32" else "MERGE_BELOW_TILES_2B",
+                lim)
     dev = torch.device("cuda:0")
     T, S, B = bench.DT[a.dtype], a.size, a.batch
     enc = E4EEncoder(bench.encoder_weights("e4e", S), S, dtype=T, device=dev)

@@ -19,7 +19,8 @@
 //     per patch), so no patch waits for HBM;
 //   * every wave computes all 128 patch pixels × its 16 channels (acc 8 fragments). The A
 //     fragment of halo row q, column shift dx and K-chunk s feeds the three taps (dy = 0, 1, 2)
-//     of output rows q − dy: 120 ds_read_b128 per wave per patch for 288 MFMAs, read two ahead;
+//     of output rows q − dy: 120 ds_read_b128 per wave per patch for 288 MFMAs, read three ahead
+//     (MIA_WRES128_PF) as inline-asm ds_read_b128 with counted lgkmcnt waits;
 //   * the epilogue (noise, bias, leaky ReLU · √2) runs in registers; the patch's noise rows are
 //     DMA'd into LDS with the halo and the bias sits in VGPRs, so it waits on nothing.
 // Halo LDS image (2-byte types, PB = 2·Cin bytes per pixel): halo rows padded to HS = 20 pixels

@@ -177,6 +177,7 @@ SIGNATURES = {
     "mia_se_bwd_parts": (c_int, [P, c_int, P, P, P, P, P, c_int, c_int, c_int, c_float, P]),
     "mia_se_grad_scale": (c_int, [P, P, P, P, P, c_int, c_int, c_int, c_int, P]),
     "mia_prelu_bwd_scale": (c_int, [P, P, P, P, P, c_int64, c_int, c_int, P]),
+    "mia_prelu_fwd": (c_int, [P, P, P, c_int64, c_int, c_int, P]),
     "mia_subsample_add": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, P]),
     "mia_cast": (c_int, [P, c_int, P, c_int, c_int64, c_float, P]),
     "mia_bilinear_fwd": (c_int, [P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

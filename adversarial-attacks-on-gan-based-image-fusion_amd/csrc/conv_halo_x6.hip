@@ -248,6 +248,14 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
         ol[q][c] = vl;
       }
     int st = 0;
+#ifdef MIA_PROBE_MFMA32
+    typedef __attribute__((ext_vector_type(16))) float f32x16;
+    f32x16 acc32[FM / 2][FN / 2];
+#pragma unroll
+    for (int i = 0; i < FM / 2; ++i)
+#pragma unroll
+      for (int j = 0; j < FN / 2; ++j) acc32[i][j] = f32x16{};
+#endif
     for (int cb = 0; cb < ncb; ++cb) {
 #pragma unroll
       for (int tg = 0; tg < NG; ++tg) {
@@ -289,11 +297,35 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
               blo[j] = *(const u32x2*)(sb + TL::BHM + row * TL::LROWB + ((ch ^ lsw(row)) << 3));
             }
             __builtin_amdgcn_s_setprio(1);
+#ifdef MIA_PROBE_MFMA32
+            // TIMING PROBE ONLY (wrong numerics; round 6, verdict r05 item 2): the same fragment
+            // reads and FLOPs as 32×32×16 MFMAs — 6 per (row pair, channel pair) of 16×16 tiles
+            // instead of 3 × 4 16×16×32 ones
+#pragma unroll
+            for (int i = 0; i < FM / 2; ++i)
+#pragma unroll
+              for (int j = 0; j < FN / 2; ++j)
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                  const bf16x8 AHM = __builtin_bit_cast(bf16x8, ahm[2 * i + u]);
+                  const bf16x8 BHM = __builtin_bit_cast(bf16x8, bhm[2 * j + u]);
+                  const bf16x8 ALH = __builtin_bit_cast(
+                      bf16x8, u32x4{al[2 * i + u][0], al[2 * i + u][1], ahm[2 * i + u][0],
+                                    ahm[2 * i + u][1]});
+                  const bf16x8 BLH = __builtin_bit_cast(
+                      bf16x8, u32x4{blo[2 * j + u][0], blo[2 * j + u][1], bhm[2 * j + u][0],
+                                    bhm[2 * j + u][1]});
+                  acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(BLH, AHM, acc32[i][j], 0, 0, 0);
+                  acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(BHM, ALH, acc32[i][j], 0, 0, 0);
+                  acc32[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(BHM, AHM, acc32[i][j], 0, 0, 0);
+                }
+#else
 #pragma unroll
             for (int i = 0; i < FM; ++i)
 #pragma unroll
               for (int j = 0; j < FN; ++j)
                 acc[i][j] = mfma_x6(bhm[j], blo[j], ahm[i], al[i], acc[i][j]);  // D[ch][px]
+#endif
             __builtin_amdgcn_s_setprio(0);
           }
         }
@@ -320,6 +352,17 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
         st ^= 1;
       }
     }
+#ifdef MIA_PROBE_MFMA32
+#pragma unroll
+    for (int i = 0; i < FM / 2; ++i)
+#pragma unroll
+      for (int j = 0; j < FN / 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          acc[2 * i + q / 2][2 * j + q % 2] =
+              f32x4{acc32[i][j][4 * q], acc32[i][j][4 * q + 1], acc32[i][j][4 * q + 2],
+                    acc32[i][j][4 * q + 3]};
+#endif
   } else {
   int st = 0, cb = 0, t = 0;
   for (int s = 0; s < nk; ++s) {

@@ -288,6 +288,28 @@ __global__ __launch_bounds__(256) void prelu_bwd_scale_kernel(const T* __restric
   }
 }
 
+// ---- a = pre > 0 ? pre : slope·pre (PReLU forward from a stored pre-activation) -------------------
+// Round 6: the e4e units whose PReLU has a negative slope keep the conv output (pre) for the
+// backward's branch mask — the stored activation's sign no longer tells the branch — and take
+// their activation from this pass (same single rounding of slope·pre as the conv epilogue's
+// MIA_ACT_PRELU at fp32).
+template <typename T>
+__global__ __launch_bounds__(256) void prelu_fwd_kernel(const T* __restrict__ pre,
+                                                        const float* __restrict__ slope,
+                                                        T* __restrict__ a, int C, int64_t total) {
+  const int cv = C / 8;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % cv) * 8;
+    const int64_t pix = i / cv;
+    float v[8], sl[8];
+    load8<T>(pre + pix * C + c, v);
+    load8f(slope + c, sl);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : sl[e] * v[e];
+    store8<T>(a + pix * C + c, v);
+  }
+}
+
 // ---- gx[n][2y][2x] += g[n][y][x] -----------------------------------------------------------------
 template <typename T>
 __global__ __launch_bounds__(256) void subsample_add_kernel(const T* __restrict__ g, T* gx, int N,
@@ -555,6 +577,17 @@ extern "C" int mia_prelu_bwd_scale(const void* g_a, const void* a, const float* 
                                                   (hipStream_t)stream, (const T*)g_a, (const T*)a,
                                                   slope, gamma, (T*)g, C, total));
   return check_launch("prelu_bwd_scale");
+}
+
+extern "C" int mia_prelu_fwd(const void* pre, const float* slope, void* a, int64_t pixels, int C,
+                             int dtype, void* stream) {
+  MIA_CHECK_ARG(pre && slope && a && pixels > 0, "bad args");
+  ENC_CHECK_C(C);
+  const int64_t total = pixels * (C / 8);
+  MIA_DISPATCH_DTYPE(dtype, T, hipLaunchKernelGGL(prelu_fwd_kernel<T>, dim3(ew_grid(total)),
+                                                  dim3(256), 0, (hipStream_t)stream,
+                                                  (const T*)pre, slope, (T*)a, C, total));
+  return check_launch("prelu_fwd");
 }
 
 extern "C" int mia_subsample_add(const void* g, void* gx, int N, int H, int W, int C, int dtype,

@@ -1009,6 +1009,15 @@ def prelu_bwd_scale(g_a, a, slope, g, gamma=None):
     return g
 
 
+def prelu_fwd(pre, slope, a):
+    """a = pre > 0 ? pre : slope[c]·pre (NHWC, per-channel fp32 slope)."""
+    C = pre.shape[-1]
+    _need(a, pre.shape, pre.dtype, "a")
+    _numel_ok(slope, C, torch.float32, "slope")
+    call("mia_prelu_fwd", ptr(pre), ptr(slope), ptr(a), pre.numel() // C, C, dt(pre), stream())
+    return a
+
+
 def subsample_add(g, gx):
     N, H, W, C = g.shape
     _need(gx, (N, 2 * H, 2 * W, C), g.dtype, "gx")

@@ -472,7 +472,10 @@ int mia_repeat(const void* src, void* dst, int64_t bytes, int count, void* strea
  *                 order inside the kernel: bit-identical to mia_chan_sum + mia_se_fwd / _bwd, one
  *                 launch fewer per SE module
  *   mia_se_grad_scale: g_r = gamma[c]·(g_out·s[n][c] + gavg[n][c])  (gamma NULL → 1)
- *   mia_prelu_bwd_scale: g = g_a·(a > 0 ? 1 : slope[c])·gamma[c]  (gamma NULL → 1)
+ *   mia_prelu_bwd_scale: g = g_a·(a > 0 ? 1 : slope[c])·gamma[c]  (gamma NULL → 1); `a` is the
+ *                 stored activation when every slope is ≥ 0, else the pre-activation
+ *   mia_prelu_fwd: a = pre > 0 ? pre : slope[c]·pre (the e4e units with a negative PReLU slope,
+ *                 whose conv writes pre for the backward's branch mask; round 6)
  *   mia_cast: y = scale·x converted between dtypes (x, y: flat, n elements)
  *   mia_subsample_add: gx[n][2y][2x][c] += g[n][y][x][c]   (MaxPool2d(1,2) adjoint)
  *   mia_bilinear_fwd/bwd: F.interpolate(mode='bilinear', align_corners=True) (N,Hi,Wi,C) →
@@ -504,6 +507,8 @@ int mia_se_grad_scale(const void* g_out, const float* s, const float* gavg, cons
                       void* g_r, int N, int HW, int C, int dtype, void* stream);
 int mia_prelu_bwd_scale(const void* g_a, const void* a, const float* slope, const float* gamma,
                         void* g, int64_t pixels, int C, int dtype, void* stream);
+int mia_prelu_fwd(const void* pre, const float* slope, void* a, int64_t pixels, int C, int dtype,
+                  void* stream);
 int mia_subsample_add(const void* g, void* gx, int N, int H, int W, int C, int dtype,
                       void* stream);
 int mia_cast(const void* x, int xdtype, void* y, int ydtype, int64_t n, float scale,

@@ -42,12 +42,13 @@ def to64(params):
 
 
 def e4e_masks(enc):
-    """The device run's PReLU / LeakyReLU branch per activation (sign of the stored activation =
-    sign of the pre-activation, slopes > 0), keyed as oracle.encoder_ref.forced_masks expects.
-    Reflects the encoder's most recent forward."""
-    m = {"in": nchw(enc._a0) > 0}
+    """The device run's PReLU / LeakyReLU branch per activation (the sign of the tensor the
+    backward masks with: the stored activation, whose sign is the pre-activation's for slopes ≥ 0,
+    or — a layer with a negative PReLU slope, round 6 — the stored pre-activation), keyed as
+    oracle.encoder_ref.forced_masks expects. Reflects the encoder's most recent forward."""
+    m = {"in": nchw(enc._m0) > 0}
     for i, U in enumerate(enc.units):
-        m[f"body.{i}"] = nchw(U["_a1"]) > 0
+        m[f"body.{i}"] = nchw(U["_m1"]) > 0
         m[f"body.{i}.se"] = (U["_u"] > 0).cpu()[:, :, None, None]  # relu(fc1(avg)), (N, C/16)
     for i, hd in enumerate(enc.heads):
         for j, a in enumerate(hd["_acts"]):

@@ -5,7 +5,7 @@ the oracle / the fp32 device path:
 * cfg2 — PGD-10 L∞ ε=8/255, batch 32 at 256², fp32: ε-ball / range / finite; two runs
   bit-identical; three images' whole trajectories bit-identical to their own batch-1 runs
   (ordered reductions); image 0's gradient against the mask-forced fp64 oracle.
-* cfg3 — PGD-40 at 1024², bf16 (N=2): ε-ball / range / finite; gradient sign agreement with the
+* cfg3 — PGD-40 at 1024², bf16 (N=8): ε-ball / range / finite; gradient sign agreement with the
   fp32 device path (itself oracle-checked at 1024² in test_gpu_networks).
 * cfg4 per-GPU share — PGD-20, 128 images at 256², fp16: ε-ball / range / finite; gradient sign
   agreement with the fp32 device path on 8 of the images.
@@ -103,7 +103,8 @@ def _sign_agreement(size, dtype, N, cuda, s0, zeros=False):
 
 
 def test_cfg3_pgd40_1024_bf16(cuda):
-    size, N, steps = 1024, 2, 40
+    """N = 8 (cfg3 at N = 8–16; round 6, verdict r05 item 4)."""
+    size, N, steps = 1024, 8, 40
     eng, _ = engine(size, torch.bfloat16, cuda)
     x0, t = _pair(N, size, 300)
     adv = eng.run(x0.to(cuda), t.to(cuda), steps, EPS, ALPHA).cpu()

@@ -458,3 +458,65 @@ def test_style_head_first_convs_merged_per_source(cuda, dtype):
     for p in range(P):
         assert rel_err(nchw(y[p * N:(p + 1) * N]), ref[:, p * C:(p + 1) * C]) < TOL[dtype]
     enc.src_fwd = saved
+
+
+def _with_negative_slopes(p, frac=0.1, seed=77):
+    """A copy of e4e weights with about `frac` of every PReLU's slopes made negative (−|s|, up to
+    −0.45) and one slope per layer exactly 0: the slopes a trained pSp / e4e checkpoint may hold
+    (nn.PReLU is unconstrained; code/utils/model_utils.py:7-18 loads it as is)."""
+    g = torch.Generator().manual_seed(seed)
+    q = dict(p)
+    keys = ["input_layer.2.weight"] + [k for k in p if k.endswith("res_layer.2.weight")]
+    for k in keys:
+        s = p[k].clone()
+        flip = torch.rand(s.shape, generator=g) < frac
+        s[flip] = -(s[flip].abs() + 0.2 * torch.rand(int(flip.sum()), generator=g))
+        s[int(torch.randint(0, s.numel(), (1,), generator=g))] = 0.0
+        q[k] = s
+    return q
+
+
+def test_e4e_negative_prelu_slopes_vs_forced_oracle(cuda):
+    """verdict r05 item 3: an encoder whose PReLU slopes are partly negative (≈ 10 %) or zero is
+    accepted (the units keep their pre-activation as the backward's branch mask, mia_prelu_fwd
+    makes the activation), and at fp32 its latents match the fp64 oracle and its input gradient
+    matches the oracle forced onto the device's branches to < 1e-4 (norm), with every forced
+    disagreement a near-tie."""
+    from oracle import forcing
+    from gpu_helpers import e4e_masks
+    p = _with_negative_slopes(make_e4e_weights(256, seed=3))
+    enc = e4e.E4EEncoder(p, 256, dtype=torch.float32, device=cuda)
+    assert enc.in_neg and sum(U["neg"] for U in enc.units) >= 20
+    N, R = 2, 256
+    x = rnd((N, 3, R, R), 50).clamp(-1, 1) * 0.9
+    xin = torch.zeros(N, R, R, CPAD, dtype=torch.float32, device=cuda)
+    xin[..., :3] = x.permute(0, 2, 3, 1).to(cuda)
+    x64 = xin[..., :3].permute(0, 3, 1, 2).double().cpu()
+    p64 = {k: (v.double() if torch.is_tensor(v) else v) for k, v in p.items()}
+    ws = Workspace(cuda)
+    lat = enc.forward_nhwc(xin, ws)
+    # the activation of a negative-slope unit is PReLU(pre) of the kept pre-activation
+    U = enc.units[5]
+    want = torch.where(U["_m1"] > 0, U["_m1"], U["slope"] * U["_m1"])
+    assert torch.equal(U["_a1"], want)
+    gl = rnd((N, 14, 512), 51)
+    gx = torch.zeros_like(xin)
+    enc.backward_nhwc(gl.float().to(cuda), ws, gx, accumulate=True)
+    got = nchw(gx[..., :3].contiguous())
+    xx = x64.clone().requires_grad_(True)
+    ref_free = encoder_ref.e4e_encode(p64, x64, 14)
+    assert rel_err(lat, ref_free) < 1e-4
+    with forcing.audit() as au, encoder_ref.forced_masks(e4e_masks(enc)):
+        ref = encoder_ref.e4e_encode(p64, xx, 14)
+        (gref,) = torch.autograd.grad(ref, xx, gl)
+    flips, sites, worst, key = au.summary()
+    print(f"negative-slope e4e: forced flips {flips} of {sites} sites (max gap {worst:.2e}, "
+          f"{key}); gradient norm-rel {((got - gref).norm() / gref.norm()).item():.2e}")
+    assert sites > 0 and flips <= 1e-4 * sites
+    assert all(r["rel_gap"] <= 1e-5 for r in au.records if r["flips"])
+    assert ((got - gref).norm() / gref.norm()).item() < 1e-4
+    # the same weights with every negative slope clamped to 0 take other branches: the mask is
+    # what makes the gradient right (a sign-of-activation backward would follow the clamped net)
+    prelu_keys = [k for k in p64 if k == "input_layer.2.weight" or k.endswith("res_layer.2.weight")]
+    clamped = {k: (v.clamp_min(0) if k in prelu_keys else v) for k, v in p64.items()}
+    assert rel_err(lat, encoder_ref.e4e_encode(clamped, x64, 14)) > 1e-3

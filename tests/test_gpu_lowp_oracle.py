@@ -94,3 +94,48 @@ def test_cfg1_fgsm_vs_oracle(cuda, dtype):
         assert torch.equal(adv[stable], ref[stable])
     else:
         assert eq >= 0.999 and eq_ref >= 0.999
+
+
+# (dtype, size, PGD iterations, bound on the equal fraction over sign-stable pixels)
+OUT_CASES = [(torch.bfloat16, 1024, 3, 0.999), (torch.float16, 256, 4, 0.999)]
+
+
+@pytest.mark.parametrize("dtype,size,k,eq_tol", OUT_CASES)
+def test_lowp_pgd_output_vs_oracle(cuda, dtype, size, k, eq_tol):
+    """verdict r05 item 4: the reduced-precision PGD-k OUTPUT against the oracle's PGD-k, unforced.
+    The device runs attack steps 1…k on its own; the oracle runs the same k steps with fp64
+    gradients (interpolation.py:786-818 objective, :62-96 rule; attack_ref.project_step at fp32).
+    On every pixel whose oracle gradient exceeds 1e-3 of its max at EVERY one of the k steps
+    (sign-stable), the device's final value must equal the oracle's bit for bit on ≥ eq_tol of
+    them (a pixel differs only where some step's sign differed). The forced-branch audit of the
+    device's first-step gradient is printed alongside (its flips are what the unforced run lives
+    with)."""
+    eng, params = engine(size, dtype, cuda)
+    x0, t = seeded(640 + size, (1, 3, size, size)), seeded(641 + size, (1, 3, size, size))
+    adv = eng.run(x0.to(cuda), t.to(cuda), k, EPS, 2 / 255).cpu()
+    # the forced audit at x0 (the first step's gradient)
+    eng.prepare(x0.to(cuda), t.to(cuda))
+    with capture_vgg(eng.V, n=1) as cap:
+        eng.full_gradient(x0.to(cuda))
+    p64 = to64(params)
+    refs = attack_ref.Refs(*p64, x0.double(), t.double(), size)
+    fa = forced_all(eng, cap, n=1)
+    with fa:
+        attack_ref.loss_grad(*p64, x0.double(), refs, size)
+    report = fa.report()
+    del eng
+    free()
+    e, a = 2 * EPS, 2 * 2 / 255
+    x = x0.clone()
+    stable = torch.ones_like(x0, dtype=torch.bool)
+    for _ in range(k):
+        _, g = attack_ref.loss_grad(*p64, x.double(), refs, size)
+        stable &= g.abs() > 1e-3 * g.abs().max()
+        x = attack_ref.project_step(x, x0, g.float(), e, a)
+    eq = (adv[stable] == x[stable]).float().mean().item()
+    eq_all = (adv == x).float().mean().item()
+    print(f"{dtype} {size}² PGD-{k} output vs the oracle's PGD-{k}: equal on {eq:.5f} of "
+          f"{int(stable.sum())} sign-stable pixels ({eq_all:.5f} of all {adv.numel()}); "
+          f"first-step audit: {report}")
+    assert ((adv - x0).abs() <= float(np.float32(2 * EPS)) + 1e-6).all()
+    assert eq >= eq_tol

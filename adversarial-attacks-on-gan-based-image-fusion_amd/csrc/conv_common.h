@@ -218,21 +218,6 @@ __device__ __forceinline__ f32x4 mfma_x6(const u32x4& ahm, const u32x2& al, cons
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(AHM, BHM, c, 0, 0, 0);  // hh + mm
 }
 
-// The same six products on v_mfma_f32_32x32x16_bf16 (round 6 A/B, conv_halo_x6.hip MIA_X6_M32):
-// a lane holds 8 consecutive k slots of one row of each 32-row operand, so the (hi,mid) / (lo,hi)
-// windows are the 16×16×32 ones; D[32][32]: lane l holds column l % 32, rows
-// 8·(v / 4) + 4·(l / 32) + v % 4 for element v.
-typedef __attribute__((ext_vector_type(16))) float f32x16;
-__device__ __forceinline__ f32x16 mfma_x6_32(const u32x4& ahm, const u32x2& al, const u32x4& bhm,
-                                             const u32x2& bl, f32x16 c) {
-  const bf16x8 AHM = __builtin_bit_cast(bf16x8, ahm), BHM = __builtin_bit_cast(bf16x8, bhm);
-  const bf16x8 ALH = __builtin_bit_cast(bf16x8, u32x4{al[0], al[1], ahm[0], ahm[1]});
-  const bf16x8 BLH = __builtin_bit_cast(bf16x8, u32x4{bl[0], bl[1], bhm[0], bhm[1]});
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(AHM, BLH, c, 0, 0, 0);  // hl + mh
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ALH, BHM, c, 0, 0, 0);  // lh + hm
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(AHM, BHM, c, 0, 0, 0);  // hh + mm
-}
-
 #ifdef MIA_F32_NATIVE
 // A/B build (MIA_F32_ARITH=native): the fp32 convs on the native fp32 matrix instruction
 template <>

@@ -37,10 +37,6 @@
 #include "conv_common.h"
 #include "halo_epilogue.h"
 
-#ifndef MIA_X6_M32
-#define MIA_X6_M32 0  // round 6 A/B: the 128-channel unrolled loop on 32×32×16 MFMAs
-#endif
-
 namespace mia {
 
 #ifdef MIA_STAMPS
@@ -87,7 +83,6 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
   static_assert(UNR || TPS == 1, "several taps per K-step: the unrolled loop only");
   typedef HaloX6<BN_, TPS> TL;
   constexpr int NG = TL::NG;
-  constexpr bool M32 = MIA_X6_M32 && UNR && BN_ == 128 && TPS == 1;
   constexpr int FM = TL::FM, FN = TL::FN, WN = TL::WN, NT = TL::NT, BN = TL::BN, BK = TL::BK;
   constexpr int HSIDE = TL::HSIDE, HROWS = TL::HROWS, HPIECES = TL::HPIECES, HBUF = TL::HBUF;
   constexpr int H_INS = TL::H_INS, HPS = TL::H_PER_STEP, HWAVES = TL::HWAVES;
@@ -235,112 +230,7 @@ __global__ __launch_bounds__(HaloX6<BN_>::NT, 2) void conv_halo_x6_kernel(const 
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int frow = lane & 15, fq = lane >> 4;
-  if constexpr (M32) {
-    // Round 6 A/B (MIA_X6_M32, verdict r05 item 2): the unrolled loop on v_mfma_f32_32x32x16_bf16.
-    // A wave's 4 patch rows × 16 pixels are 2 fragments of 32 pixels (row pairs), its 64
-    // channels 2 fragments of 32; a K-step's 32 k are 4 sub-steps of 8 (two 4-k quads: chunks
-    // 2s + (lane >> 5)). Same fragment bytes per MFMA FLOP as the 16×16×32 loop, half the MFMA
-    // instructions (each holds vector issue for 8 of its 32 cycles instead of 8 of 16).
-    const int p = lane & 31, kq = lane >> 5;
-    int oh[FM + 1][3], ol[FM + 1][3];  // pixel fragments: row shift q2 = 2I + dy, column shift dx
-#pragma unroll
-    for (int q = 0; q < FM + 1; ++q)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const int hr = (wm * FM + q + (p >> 4)) * HSIDE + (p & 15) + c;
-        int vh = hr * ROWB + ((kq ^ fsw(hr)) << 4), vl = hr * TL::LROWB + ((kq ^ lsw(hr)) << 3);
-        asm volatile("" : "+v"(vh), "+v"(vl));
-        oh[q][c] = vh;
-        ol[q][c] = vl;
-      }
-    int ow[2], owl[2];  // weight fragments: channel rows wn·64 + 32·J + p
-#pragma unroll
-    for (int J = 0; J < 2; ++J) {
-      const int row = wn * FN * 16 + 32 * J + p;
-      ow[J] = row * ROWB + ((kq ^ fsw(row)) << 4);
-      owl[J] = TL::BHM + row * TL::LROWB + ((kq ^ lsw(row)) << 3);
-    }
-    f32x16 acc32[FM / 2][2];
-#pragma unroll
-    for (int I = 0; I < FM / 2; ++I)
-#pragma unroll
-      for (int J = 0; J < 2; ++J) acc32[I][J] = f32x16{};
-    int st = 0;
-    for (int cb = 0; cb < ncb; ++cb) {
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int s = cb * 9 + t;
-        // opaque per step (as the loop below): keeps (table ^ sub-step) from being hoisted out of
-        // the unrolled taps as 90 more live registers
-        int hoff = (cb & 1) * HBUF, x1 = 32, x2 = 16;
-        asm volatile("" : "+s"(hoff), "+s"(x1), "+s"(x2));
-        const char* ha = hbuf + hoff;
-        const char* sb = bring + st * BSTAGE;
-        if (bwave && s + 1 < nk) issue_b(s + 1, st ^ 1);
-        if (!bwave && cb + 1 < ncb && t < (H_INS + HPS - 1) / HPS) {
-#pragma unroll
-          for (int q = 0; q < HPS; ++q) {
-            const int j = t * HPS + q;
-            if (j < H_INS && j < my_pieces) issue_h(cb + 1, j, (cb + 1) & 1);
-          }
-        }
-        const int dy = t / 3, dx = t % 3;
-#pragma unroll
-        for (int ss = 0; ss < 4; ++ss) {
-          const int xh = ss * x1, xl = ss * x2;  // chunk 2·ss + kq: byte offset ^ (2·ss)·16 / ·8
-          u32x4 ahm[FM / 2], bhm[2];
-          u32x2 al[FM / 2], blo[2];
-#pragma unroll
-          for (int I = 0; I < FM / 2; ++I) {
-            ahm[I] = *(const u32x4*)(ha + (oh[2 * I + dy][dx] ^ xh));
-            al[I] = *(const u32x2*)(lbuf + (ol[2 * I + dy][dx] ^ xl));
-          }
-#pragma unroll
-          for (int J = 0; J < 2; ++J) {
-            bhm[J] = *(const u32x4*)(sb + (ow[J] ^ xh));
-            blo[J] = *(const u32x2*)(sb + (owl[J] ^ xl));
-          }
-          __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-          for (int I = 0; I < FM / 2; ++I)
-#pragma unroll
-            for (int J = 0; J < 2; ++J)
-              acc32[I][J] = mfma_x6_32(bhm[J], blo[J], ahm[I], al[I], acc32[I][J]);  // D[ch][px]
-          __builtin_amdgcn_s_setprio(0);
-        }
-        if (bwave || t == 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        if (t == 8 && cb + 1 < ncb) {
-          convert(cb + 1, (cb + 1) & 1);
-          __syncthreads();
-        }
-        st ^= 1;
-      }
-    }
-    // back to the 16×16 fragment layout the epilogues take: acc[i][j] lane (fq, frow) = channel
-    // 16j + 4fq + e at pixel (row i, column frow) = acc32[i/2][j/2] element 4·(2·(j%2) + fq/2) + e
-    // of lane 32·(fq%2) + 16·(i%2) + frow
-    // (one 32×32 tile at a time, so that each dies as its four 16×16 tiles are built)
-#pragma unroll
-    for (int I = 0; I < FM / 2; ++I)
-#pragma unroll
-      for (int J = 0; J < 2; ++J)
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj) {
-            const int src = 32 * (fq & 1) + 16 * r + frow;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float v0 = __shfl(acc32[I][J][8 * jj + e], src, 64);
-              const float v1 = __shfl(acc32[I][J][8 * jj + 4 + e], src, 64);
-              acc[2 * I + r][2 * J + jj][e] = (fq >> 1) ? v1 : v0;
-            }
-          }
-    __builtin_amdgcn_sched_barrier(0);  // the remap completes before the epilogue's loads
-  } else if constexpr (UNR) {
+  if constexpr (UNR) {
     // The taps unrolled: every fragment address is a lane-constant LDS offset chosen at compile
     // time — for the A fragments one per (row shift q = i + dy, column shift dx), computed once
     // here (the swizzle is not linear in the row, so per step it cost ≈ 8 VALU per fragment); the

@@ -1,3 +1,4 @@
+# Reproduce at commit 245ea98 (the MIA_X6_M32 variant was removed from the source after this A/B).
 # round 6 A/B (verdict r05 item 2): the fp32 x6 halo kernel's 128-channel unrolled loop on
 # v_mfma_f32_32x32x16_bf16 (libmiattack_m32.so: make variant VARIANT=m32 VARIANT_FLAGS=-DMIA_X6_M32=1)
 # against the product library (16x16x32). First the variant's numerics (the x6 kernel tests and the

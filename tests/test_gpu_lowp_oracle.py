@@ -96,24 +96,35 @@ def test_cfg1_fgsm_vs_oracle(cuda, dtype):
         assert eq >= 0.999 and eq_ref >= 0.999
 
 
-# (dtype, size, PGD iterations, bound on the equal fraction over sign-stable pixels)
-OUT_CASES = [(torch.bfloat16, 1024, 3, 0.999), (torch.float16, 256, 4, 0.999)]
+# (dtype, size, PGD iterations, sign-stable threshold as a fraction of max|g|, bound on the
+# unforced equal fraction). A pixel's sign is "stable" where the oracle gradient exceeds the dtype's
+# measured max gradient error against the forced oracle at every step (bf16 3.5e-2, fp16 4.0e-3
+# of max|g|: profiles/r05_lowp_oracle.log; fp32 ≈ 1e-5). The teacher-forced steps must agree on
+# ≥ 0.999 of the stable pixels at every dtype. The UNFORCED bound is lower at bf16 / fp16 because
+# the trajectories decouple: pixels below the threshold take the other sign at step 1, the images
+# then differ by 2α there, and every later gradient differs through the networks (measured round 6,
+# profiles/r06_lowp_oracle.log). That decoupling is PGD's, not the kernels': the fp32 device run
+# (gradient within 1e-5 of fp64, 125 forced flips in 93 M sites) and the oracle itself run with
+# fp32 instead of fp64 gradients (the reference's own CPU precision) leave the fp64 trajectory on
+# the same order of pixels — the sign of a near-zero gradient is arbitrary, and a pixel that moved
+# the other way changes every later gradient through the networks.
+OUT_CASES = [(torch.float32, 256, 4, 1e-2, 0.95), (torch.bfloat16, 1024, 3, 5e-2, 0.9),
+             (torch.float16, 256, 4, 1e-2, 0.9)]
 
 
-@pytest.mark.parametrize("dtype,size,k,eq_tol", OUT_CASES)
-def test_lowp_pgd_output_vs_oracle(cuda, dtype, size, k, eq_tol):
-    """verdict r05 item 4: the reduced-precision PGD-k OUTPUT against the oracle's PGD-k, unforced.
-    The device runs attack steps 1…k on its own; the oracle runs the same k steps with fp64
-    gradients (interpolation.py:786-818 objective, :62-96 rule; attack_ref.project_step at fp32).
-    On every pixel whose oracle gradient exceeds 1e-3 of its max at EVERY one of the k steps
-    (sign-stable), the device's final value must equal the oracle's bit for bit on ≥ eq_tol of
-    them (a pixel differs only where some step's sign differed). The forced-branch audit of the
-    device's first-step gradient is printed alongside (its flips are what the unforced run lives
-    with)."""
+@pytest.mark.parametrize("dtype,size,k,thr,eq_tol", OUT_CASES)
+def test_lowp_pgd_output_vs_oracle(cuda, dtype, size, k, thr, eq_tol):
+    """verdict r05 item 4: the PGD-k OUTPUT against the oracle's PGD-k (interpolation.py:786-818
+    objective, :62-96 rule; fp64 gradients, attack_ref.project_step at fp32).
+    * unforced: the device runs attack steps 1…k on its own; on the pixels whose oracle gradient
+      exceeds `thr` of its max at EVERY step its final value must equal the oracle's bit for bit
+      on ≥ eq_tol of them (equal fractions at other thresholds printed);
+    * teacher-forced per step: at each oracle iterate x_i the device's gradient, projected, must
+      give the oracle's x_{i+1} bit for bit on ≥ 0.999 of the pixels with |g_i| > thr.
+    The forced-branch audit of the device's first-step gradient is printed alongside."""
     eng, params = engine(size, dtype, cuda)
     x0, t = seeded(640 + size, (1, 3, size, size)), seeded(641 + size, (1, 3, size, size))
     adv = eng.run(x0.to(cuda), t.to(cuda), k, EPS, 2 / 255).cpu()
-    # the forced audit at x0 (the first step's gradient)
     eng.prepare(x0.to(cuda), t.to(cuda))
     with capture_vgg(eng.V, n=1) as cap:
         eng.full_gradient(x0.to(cuda))
@@ -123,19 +134,45 @@ def test_lowp_pgd_output_vs_oracle(cuda, dtype, size, k, eq_tol):
     with fa:
         attack_ref.loss_grad(*p64, x0.double(), refs, size)
     report = fa.report()
-    del eng
-    free()
     e, a = 2 * EPS, 2 * 2 / 255
     x = x0.clone()
-    stable = torch.ones_like(x0, dtype=torch.bool)
+    thrs = sorted({1e-3, 1e-2, thr, 1e-1})
+    stable = {c: torch.ones_like(x0, dtype=torch.bool) for c in thrs}
+    forced = []
     for _ in range(k):
         _, g = attack_ref.loss_grad(*p64, x.double(), refs, size)
-        stable &= g.abs() > 1e-3 * g.abs().max()
-        x = attack_ref.project_step(x, x0, g.float(), e, a)
-    eq = (adv[stable] == x[stable]).float().mean().item()
-    eq_all = (adv == x).float().mean().item()
-    print(f"{dtype} {size}² PGD-{k} output vs the oracle's PGD-{k}: equal on {eq:.5f} of "
-          f"{int(stable.sum())} sign-stable pixels ({eq_all:.5f} of all {adv.numel()}); "
-          f"first-step audit: {report}")
+        big = g.abs() > thr * g.abs().max()
+        for c in thrs:
+            stable[c] &= g.abs() > c * g.abs().max()
+        x_next = attack_ref.project_step(x, x0, g.float(), e, a)
+        gd = eng.full_gradient(x.to(cuda)).cpu()  # the device's gradient at the oracle's iterate
+        xd = attack_ref.project_step(x, x0, gd, e, a)
+        forced.append((xd[big] == x_next[big]).float().mean().item())
+        x = x_next
+    del eng
+    free()
+    own = ""
+    if dtype == torch.float32:  # the oracle's own fp32-vs-fp64 divergence over the same k steps
+        p32 = ({kk: vv.float() for kk, vv in p64[0].items()},
+               {kk: (w.float(), b.float()) for kk, (w, b) in p64[1].items()},
+               {kk: (vv.float() if torch.is_tensor(vv) else vv) for kk, vv in p64[2].items()})
+        refs32 = attack_ref.Refs(*p32, x0, t, size)
+        x32 = x0.clone()
+        for _ in range(k):
+            _, g32 = attack_ref.loss_grad(*p32, x32, refs32, size)
+            x32 = attack_ref.project_step(x32, x0, g32, e, a)
+        m = stable[thr]
+        own = (f"; the oracle at fp32 vs fp64: {(x32[m] == x[m]).float().mean().item():.5f} of the "
+               f"same stable pixels, {(x32 == x).float().mean().item():.5f} of all")
+    fr = {c: (adv[m] == x[m]).float().mean().item() for c, m in stable.items()}
+    eq = fr[thr]
+    print(f"{dtype} {size}² PGD-{k} vs the oracle's PGD-{k}: teacher-forced steps equal on "
+          + "/".join(f"{f:.5f}" for f in forced) + f" of the pixels with |g_i| > {thr:g}·max; "
+          f"unforced output equal on {eq:.5f} of {int(stable[thr].sum())} pixels stable at every "
+          f"step (" + ", ".join(f"> {c:g}·max: {fr[c]:.5f} of {int(stable[c].sum())}"
+                                for c in thrs)
+          + f"; all pixels {(adv == x).float().mean().item():.5f}){own}; first-step audit: "
+          f"{report}")
     assert ((adv - x0).abs() <= float(np.float32(2 * EPS)) + 1e-6).all()
+    assert min(forced) >= 0.999
     assert eq >= eq_tol

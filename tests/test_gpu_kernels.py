@@ -1709,3 +1709,39 @@ def test_survey_named_aliases(cuda, dtype):
         with pytest.raises(_lib.MiaError, match="fp32 only"):
             ops.call("mia_mse_fwd_bwd", ops.ptr(a), ops.ptr(b), ops.ptr(l1), ops.ptr(g1), n, L,
                      1.0 / L, 2.0 / L, 1, ops.dt(dtype), ops.stream())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("N,R,C", [(2, 16, 128), (1, 24, 64), (2, 32, 512), (1, 40, 256),
+                                   (2, 8, 128), (1, 16, 32)])
+def test_upconv_blur_fwd_bwd_vs_fp64(cuda, dtype, N, R, C):
+    """mia_upconv_blur_fwd / _bwd (the up-sampling StyledConv's Blur, rosinality upfirdn2d with
+    [1,3,3,1]⊗[1,3,3,1]/64·4, pad (1,1), + demod + noise + bias + lrelu·√2; and its adjoint)
+    against fp64 on the device's own (rounded) inputs. Round 6: the row-walking LDS kernel takes
+    every launch with C a multiple of 8 vectors and 2R ≥ 32 (here R = 16, 24, 32, 40; a partial
+    last column tile at R = 24 / 40 and the 2R + 1 adjoint rows / columns); the strip kernel the
+    rest (R = 8, fp16 / bf16 C = 32)."""
+    g = torch.Generator().manual_seed(R * 7 + C)
+    S = 2 * R + 1
+    t = torch.randn(N, S, S, C, generator=g).to(dtype)
+    demod = (0.5 + torch.rand(N, C, generator=g))
+    noise = torch.randn(2 * R, 2 * R, generator=g)
+    bias = 0.1 * torch.randn(C, generator=g)
+    gy = torch.randn(N, 2 * R, 2 * R, C, generator=g).to(dtype)
+    k = stylegan2_ref.make_kernel([1, 3, 3, 1], torch.float64) * 4
+    blur = stylegan2_ref.upfirdn2d(t.permute(0, 3, 1, 2).double(), k, pad=(1, 1))
+    pre = blur * demod.double().view(N, C, 1, 1) + 0.1 * noise.double() + bias.double().view(1, -1, 1, 1)
+    ref = F.leaky_relu(pre, 0.2) * math.sqrt(2)
+    # the adjoint: autograd of the same linear map
+    tt = t.permute(0, 3, 1, 2).double().requires_grad_(True)
+    (gt_ref,) = torch.autograd.grad(stylegan2_ref.upfirdn2d(tt, k, pad=(1, 1)),
+                                    tt, gy.permute(0, 3, 1, 2).double())
+    out = torch.empty(N, 2 * R, 2 * R, C, dtype=dtype, device=cuda)
+    ops.upconv_blur_fwd(t.to(cuda), out, demod.to(cuda), noise.reshape(-1).to(cuda), 0.1,
+                        bias.to(cuda), act_out=ops.ACT_LRELU_S2)
+    gt = torch.empty(N, S, S, C, dtype=dtype, device=cuda)
+    ops.upconv_blur_bwd(gy.to(cuda), gt)
+    torch.cuda.synchronize()
+    tol = {torch.float32: 2e-6, torch.float16: 2e-3, torch.bfloat16: 1.5e-2}[dtype]
+    assert rel_err(nchw(out), ref) < tol
+    assert rel_err(nchw(gt), gt_ref) < tol

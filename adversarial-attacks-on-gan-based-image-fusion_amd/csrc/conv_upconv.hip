@@ -89,8 +89,13 @@ __device__ __forceinline__ const char* up_src(const UpK& k, int i) {
   return (const char*)p;
 }
 
+#ifndef MIA_UPCONV_PREMOD
+#define MIA_UPCONV_PREMOD 1  // A/B build: 0 = modulate every fragment read (round 5)
+#endif
+
 template <typename T, bool PRO, bool DG, int BN_ = 64>
 __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
+  constexpr bool PREMOD = MIA_UPCONV_PREMOD;
   typedef HaloUpT<BN_> TL;
   typedef typename Vec<T>::type VT;
   constexpr int VEC = Vec<T>::N, BK = ROWB / (int)sizeof(T);  // elements per chunk / per row
@@ -175,6 +180,20 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
       stab[i] = from_f<T>(sv * mul);
     }
   }
+  // PREMOD (round 6, as conv_halo.hip): the landed halo of channel block cb modulated in place
+  // ONCE — act(x)·s rounded to T exactly as modulate<T> on every fragment read (5 K-steps × 2
+  // column waves), so the outputs are bit-identical; zero padding stays zero. The per-fragment
+  // form cost 5-10 % of the fp16 up-conv and 45 % of the bf16 one (profiles/r06_upconv_premod_ab.txt)
+  auto premod = [&](int cb, int buf) {
+    char* hb = hbuf + buf * HBUF;
+    for (int c = tid; c < HROWS * 8; c += TL::NT) {
+      const int hr = c >> 3, pc = c & 7, lc = pc ^ fsw(hr);
+      VT v = *(const VT*)(hb + hr * ROWB + pc * 16);
+      const VT sv = *(const VT*)(stab + cb * BK + lc * VEC);
+      modulate<T>(v, sv, lrelu_in);
+      *(VT*)(hb + hr * ROWB + pc * 16) = v;
+    }
+  };
   if (bwave) {
     issue_b(0, 0);
   } else {
@@ -183,6 +202,10 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (PRO && PREMOD) {
+    premod(0, 0);
+    lds_handoff();
+  }
 
   f32x4 acc[4][FM][FN];
 #pragma unroll
@@ -212,7 +235,7 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
                             : (wm * FM + i + 1 - jy) * HSIDE + frow + 1 - jx;
           af[i] = *(const VT*)(ha + hr * ROWB + ((ch ^ fsw(hr)) << 4));
         }
-        if constexpr (PRO) {
+        if constexpr (PRO && !PREMOD) {  // round-5 form: every fragment read modulated
           const VT sv = *(const VT*)(stab + cb * BK + ch * VEC);
 #pragma unroll
           for (int i = 0; i < FM; ++i) modulate<T>(af[i], sv, lrelu_in);
@@ -249,6 +272,12 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of stage stg done
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (PRO && PREMOD) {
+        if (st == 4 && cb + 1 < ncb) {  // the next block's halo landed (step 4's wait): modulate it
+          premod(cb + 1, (cb + 1) & 1);
+          lds_handoff();
+        }
+      }
     }
   }
 

@@ -6,9 +6,6 @@
 namespace mia {
 
 constexpr int TPB = 256;
-#ifndef MIA_BLUR_WALK
-#define MIA_BLUR_WALK 1  // A/B build: 0 = the round-5 strip kernel for every up-conv blur
-#endif
 
 static inline int blocks_for(int64_t n, int per_block = TPB, int cap = 1 << 20) {
   int64_t b = (n + per_block - 1) / per_block;
@@ -253,143 +250,6 @@ __global__ __launch_bounds__(256) void blur4_strip_kernel(
             o[e] = from_f<T>(r);
           }
           *(VT*)(obase + ((size_t)oy * Hout + ox) * C) = o;
-        }
-      }
-    }
-  }
-}
-
-// Round 6: the same FIR on column tiles that walk down the image. A block owns 32 output columns ×
-// one group of 8 channel vectors (64 fp16 / bf16 or 32 fp32 channels) × a segment of up to 64
-// output rows; each input row segment (35 pixels × 8 vectors) is loaded ONCE (coalesced 128-B
-// pixel slices) into a 3-row LDS ring, every thread (one output column × one vector) filters its
-// 4 input pixels horizontally from LDS and accumulates the 4 output rows the input row feeds in
-// registers. Global traffic is the input once (+ 3 apron rows per segment, 35 / 32 columns) and
-// the output once; the strip kernel above re-read each input vector ≈ 3.4 times from L2 and ran
-// at 4.5 TB/s (profiles/r05_bench_fp16_b128_e4e_kernel_trace.csv.gz). Row i + 2 is loaded into
-// registers during row i, written to LDS during row i + 1 (one LDS hand-off barrier per row).
-// Same FMAs in the same order per output as the strip kernel.
-constexpr int kWalkNV = 8, kWalkTW = 32, kWalkIW = kWalkTW + 3, kWalkSeg = 64;
-constexpr int kWalkRowV = kWalkIW * kWalkNV;       // 280 vectors per input row segment
-constexpr int kWalkLPT = (kWalkRowV + 255) / 256;  // 2 loads per thread per row
-
-template <typename T, bool FWD, bool NOISE>
-__global__ __launch_bounds__(256) void blur4_walk_kernel(
-    const T* __restrict__ in, T* __restrict__ out, const float* __restrict__ demod,
-    const float* __restrict__ noise, float nw, const float* __restrict__ bias, int N, int R, int C,
-    int act_out) {
-  typedef typename Vec<T>::type VT;
-  constexpr int V = Vec<T>::N;
-  __shared__ VT ring[3][kWalkRowV];
-  const int Hin = FWD ? 2 * R + 1 : 2 * R;
-  const int Hout = FWD ? 2 * R : 2 * R + 1;
-  const int off0 = FWD ? -1 : -2;
-  const int ncg = C / (V * kWalkNV), nct = (Hout + kWalkTW - 1) / kWalkTW;
-  const int nseg = (Hout + kWalkSeg - 1) / kWalkSeg;
-  const int64_t items = (int64_t)N * nseg * nct * ncg;
-  const int tid = threadIdx.x, oc = tid >> 3, vv = tid & 7;  // output column, vector in group
-  const VT zero = {};
-  for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
-    const int cg = (int)(it % ncg);
-    const int64_t r1 = it / ncg;
-    const int ct = (int)(r1 % nct);
-    const int64_t r2 = r1 / nct;
-    const int sg = (int)(r2 % nseg);
-    const int n = (int)(r2 / nseg);
-    const int ox0 = ct * kWalkTW, oy0 = sg * kWalkSeg;
-    const int rows_out = min(kWalkSeg, Hout - oy0), nin = rows_out + 3;
-    const int ix0 = ox0 + off0, iy0 = oy0 + off0;
-    const int c0 = (cg * kWalkNV + vv) * V;  // this thread's first channel
-    const int ox = ox0 + oc;
-    const bool col_ok = ox < Hout;
-    float dm[V], bs[V];
-    if (FWD) {
-      load8f_or_4(demod + (size_t)n * C + c0, dm);
-      if (bias) {
-        load8f_or_4(bias + c0, bs);
-      } else {
-#pragma unroll
-        for (int e = 0; e < V; ++e) bs[e] = 0.f;
-      }
-    }
-    // this thread's loads of an input row: vector q = l·256 + tid of the row segment
-    const T* base = in + (size_t)n * Hin * Hin * C + (size_t)cg * kWalkNV * V;
-    int qoff[kWalkLPT];
-    bool qok[kWalkLPT];
-#pragma unroll
-    for (int l = 0; l < kWalkLPT; ++l) {
-      const int q = l * 256 + tid, px = q >> 3, col = ix0 + px;
-      qok[l] = q < kWalkRowV && col >= 0 && col < Hin;
-      qoff[l] = qok[l] ? col * C + (q & 7) * V : 0;
-    }
-    auto load_row = [&](int r, VT (&buf)[kWalkLPT]) {
-      const int y = iy0 + r;
-      const bool rv = y >= 0 && y < Hin && r < nin;
-      const T* rb = base + (size_t)(rv ? y : 0) * Hin * C;
-#pragma unroll
-      for (int l = 0; l < kWalkLPT; ++l) buf[l] = rv && qok[l] ? *(const VT*)(rb + qoff[l]) : zero;
-    };
-    auto store_row = [&](int slot, const VT (&buf)[kWalkLPT]) {
-#pragma unroll
-      for (int l = 0; l < kWalkLPT; ++l) {
-        const int q = l * 256 + tid;
-        if (q < kWalkRowV) ring[slot][q] = buf[l];
-      }
-    };
-    auto noise_at = [&](int o) {  // nw·noise of output row o at this thread's column
-      if (!(FWD && NOISE) || o < 0 || o >= rows_out || !col_ok) return 0.f;
-      return nw * noise[(size_t)(oy0 + o) * Hout + ox];
-    };
-    VT buf[2][kWalkLPT];
-    // the ring slot of row r is r % 3; before row i: row i in LDS, row i + 1 in buf[(i + 1) & 1]
-    load_row(0, buf[0]);
-    load_row(1, buf[1]);
-    __syncthreads();  // the previous item's last reads of the ring are done
-    store_row(0, buf[0]);
-    load_row(2, buf[0]);
-    lds_handoff();
-    float acc[4][V];
-    float nz_cur = noise_at(-3), nz_next = noise_at(-2);
-    for (int i0 = 0; i0 < nin; i0 += 4) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int i = i0 + u;
-        if (i >= nin) break;
-        // row i + 1 → LDS (its slot last held row i − 2, read before the previous hand-off), row
-        // i + 3 into the freed registers, the noise of the output row completing at row i + 1
-        store_row((i + 1) % 3, buf[(u + 1) & 1]);
-        nz_cur = nz_next;
-        nz_next = noise_at(i - 2);
-        load_row(i + 3, buf[(u + 1) & 1]);
-        lds_handoff();
-        const VT* rw = ring[i % 3];
-        float h[V];
-        {
-          VT x0 = rw[oc * kWalkNV + vv], x1 = rw[(oc + 1) * kWalkNV + vv];
-          VT x2 = rw[(oc + 2) * kWalkNV + vv], x3 = rw[(oc + 3) * kWalkNV + vv];
-#pragma unroll
-          for (int e = 0; e < V; ++e)
-            h[e] = kBlur4[0] * to_f(x0[e]) + kBlur4[1] * to_f(x1[e]) + kBlur4[2] * to_f(x2[e]) +
-                   kBlur4[3] * to_f(x3[e]);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int o = i - j, sl = (u - j) & 3;
-          if (o < 0 || o >= rows_out) continue;
-#pragma unroll
-          for (int e = 0; e < V; ++e) acc[sl][e] = (j == 0 ? 0.f : acc[sl][e]) + kBlur4[j] * h[e];
-          if (j != 3 || !col_ok) continue;
-          VT ov;
-#pragma unroll
-          for (int e = 0; e < V; ++e) {
-            float r = acc[sl][e];
-            if (FWD) {
-              r = r * dm[e] + nz_cur + bs[e];
-              if (act_out) r = lrelu_s2(r);
-            }
-            ov[e] = from_f<T>(r);
-          }
-          *(VT*)(out + (((size_t)n * Hout + oy0 + o) * Hout + ox) * C + c0) = ov;
         }
       }
     }
@@ -1109,20 +969,6 @@ extern "C" int mia_upconv_blur_fwd(const void* t, void* pre, const float* demod,
   MIA_CHECK_ARG(t && pre && demod && N > 0 && R > 0, "bad args");
   const int V = dtype == MIA_F32 ? 4 : 8;
   MIA_CHECK_ARG(C % V == 0, "C must be a multiple of the vector width");
-  if (MIA_BLUR_WALK && (C / V) % kWalkNV == 0 && 2 * R >= kWalkTW) {
-    const int64_t items = (int64_t)N * ((2 * R + kWalkSeg - 1) / kWalkSeg) *
-                          ((2 * R + kWalkTW - 1) / kWalkTW) * (C / (V * kWalkNV));
-    const int grid = (int)std::min<int64_t>(items, 4096);
-    MIA_DISPATCH_DTYPE(dtype, T,
-        if (noise) {
-          MIA_LAUNCH((blur4_walk_kernel<T, true, true>), dim3(grid), dim3(256), 0, (const T*)t,
-                     (T*)pre, demod, noise, noise_w, bias, N, R, C, act_out);
-        } else {
-          MIA_LAUNCH((blur4_walk_kernel<T, true, false>), dim3(grid), dim3(256), 0, (const T*)t,
-                     (T*)pre, demod, noise, noise_w, bias, N, R, C, act_out);
-        });
-    return MIA_OK;
-  }
   const int SY = (2 * R + 2 * kBlurKQ - 1) / (2 * kBlurKQ);
   const int64_t total = (int64_t)N * SY * R * (C / V);
   MIA_DISPATCH_DTYPE(dtype, T,
@@ -1143,16 +989,6 @@ extern "C" int mia_upconv_blur_bwd(const void* gy, void* gt, int N, int R, int C
   MIA_CHECK_ARG(gy && gt && N > 0 && R > 0, "bad args");
   const int V = dtype == MIA_F32 ? 4 : 8;
   MIA_CHECK_ARG(C % V == 0, "C must be a multiple of the vector width");
-  if (MIA_BLUR_WALK && (C / V) % kWalkNV == 0 && 2 * R >= kWalkTW) {
-    const int Hout = 2 * R + 1;
-    const int64_t items = (int64_t)N * ((Hout + kWalkSeg - 1) / kWalkSeg) *
-                          ((Hout + kWalkTW - 1) / kWalkTW) * (C / (V * kWalkNV));
-    const int grid = (int)std::min<int64_t>(items, 4096);
-    MIA_DISPATCH_DTYPE(dtype, T,
-        MIA_LAUNCH((blur4_walk_kernel<T, false, false>), dim3(grid), dim3(256), 0, (const T*)gy,
-                   (T*)gt, nullptr, nullptr, 0.f, nullptr, N, R, C, 0));
-    return MIA_OK;
-  }
   const int SY = (2 * R + 1 + 2 * kBlurKQ - 1) / (2 * kBlurKQ);
   const int64_t total = (int64_t)N * SY * (R + 1) * (C / V);
   MIA_DISPATCH_DTYPE(dtype, T,

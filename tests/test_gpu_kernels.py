@@ -1717,10 +1717,8 @@ def test_survey_named_aliases(cuda, dtype):
 def test_upconv_blur_fwd_bwd_vs_fp64(cuda, dtype, N, R, C):
     """mia_upconv_blur_fwd / _bwd (the up-sampling StyledConv's Blur, rosinality upfirdn2d with
     [1,3,3,1]⊗[1,3,3,1]/64·4, pad (1,1), + demod + noise + bias + lrelu·√2; and its adjoint)
-    against fp64 on the device's own (rounded) inputs. Round 6: the row-walking LDS kernel takes
-    every launch with C a multiple of 8 vectors and 2R ≥ 32 (here R = 16, 24, 32, 40; a partial
-    last column tile at R = 24 / 40 and the 2R + 1 adjoint rows / columns); the strip kernel the
-    rest (R = 8, fp16 / bf16 C = 32)."""
+    against fp64 on the device's own (rounded) inputs, at strip-ragged sizes (2R not a multiple
+    of the 8-row strips at R = 24 / 40; the 2R + 1 adjoint rows / columns) and C = 32 … 512."""
     g = torch.Generator().manual_seed(R * 7 + C)
     S = 2 * R + 1
     t = torch.randn(N, S, S, C, generator=g).to(dtype)

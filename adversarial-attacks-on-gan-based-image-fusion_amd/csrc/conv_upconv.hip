@@ -89,13 +89,8 @@ __device__ __forceinline__ const char* up_src(const UpK& k, int i) {
   return (const char*)p;
 }
 
-#ifndef MIA_UPCONV_PREMOD
-#define MIA_UPCONV_PREMOD 1  // A/B build: 0 = modulate every fragment read (round 5)
-#endif
-
 template <typename T, bool PRO, bool DG, int BN_ = 64>
 __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
-  constexpr bool PREMOD = MIA_UPCONV_PREMOD;
   typedef HaloUpT<BN_> TL;
   typedef typename Vec<T>::type VT;
   constexpr int VEC = Vec<T>::N, BK = ROWB / (int)sizeof(T);  // elements per chunk / per row
@@ -180,10 +175,11 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
       stab[i] = from_f<T>(sv * mul);
     }
   }
-  // PREMOD (round 6, as conv_halo.hip): the landed halo of channel block cb modulated in place
-  // ONCE — act(x)·s rounded to T exactly as modulate<T> on every fragment read (5 K-steps × 2
-  // column waves), so the outputs are bit-identical; zero padding stays zero. The per-fragment
-  // form cost 5-10 % of the fp16 up-conv and 45 % of the bf16 one (profiles/r06_upconv_premod_ab.txt)
+  // PRO (round 6, as conv_halo.hip): the landed halo of channel block cb modulated in place ONCE —
+  // act(x)·s rounded to T exactly as modulate<T> on every fragment read (5 K-steps × 2 column
+  // waves) would, so the outputs are bit-identical to the round-5 per-fragment form; zero padding
+  // stays zero. bf16 up-conv forwards −28 … −33 % per call, fp16 −3 … −9 %
+  // (profiles/r06_upconv_premod_ab.txt)
   auto premod = [&](int cb, int buf) {
     char* hb = hbuf + buf * HBUF;
     for (int c = tid; c < HROWS * 8; c += TL::NT) {
@@ -202,7 +198,7 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (PRO && PREMOD) {
+  if constexpr (PRO) {
     premod(0, 0);
     lds_handoff();
   }
@@ -234,11 +230,6 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
           const int hr = DG ? (wm * FM + i + jy) * HSIDE + frow + jx
                             : (wm * FM + i + 1 - jy) * HSIDE + frow + 1 - jx;
           af[i] = *(const VT*)(ha + hr * ROWB + ((ch ^ fsw(hr)) << 4));
-        }
-        if constexpr (PRO && !PREMOD) {  // round-5 form: every fragment read modulated
-          const VT sv = *(const VT*)(stab + cb * BK + ch * VEC);
-#pragma unroll
-          for (int i = 0; i < FM; ++i) modulate<T>(af[i], sv, lrelu_in);
         }
 #pragma unroll
         for (int slot = 0; slot < 2; ++slot) {
@@ -272,7 +263,7 @@ __global__ __launch_bounds__(256, 2) void upconv_halo_kernel(const UpK k) {
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of stage stg done
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (PRO && PREMOD) {
+      if constexpr (PRO) {
         if (st == 4 && cb + 1 < ncb) {  // the next block's halo landed (step 4's wait): modulate it
           premod(cb + 1, (cb + 1) & 1);
           lds_handoff();

@@ -3,9 +3,9 @@ launches): run the up-sampling StyledConv shapes of the 256² / 1024² generator
 build, save outputs + per-call times; `--compare A B` checks two saved runs bit for bit (tuning
 aid, not product).
 
-    MIA_LIB_VARIANT=premod0 python tools/probe/upconv_premod_ab.py --out gpurun_out/up0.pt
-    python tools/probe/upconv_premod_ab.py --out gpurun_out/up1.pt
-    python tools/probe/upconv_premod_ab.py --compare gpurun_out/up0.pt gpurun_out/up1.pt
+    MIA_LIB_VARIANT=premod0 python tools/probe/upconv_premod_ab.py --out /tmp/up0.pt
+    python tools/probe/upconv_premod_ab.py --out /tmp/up1.pt
+    python tools/probe/upconv_premod_ab.py --compare /tmp/up0.pt /tmp/up1.pt
 """
 import argparse
 import math

@@ -1,4 +1,4 @@
-# Reproduce at commit 8a0f0e5-or-later-with-MIA_UPCONV_PREMOD (the PREMOD=0 path was removed after this A/B; see profiles/r06_upconv_premod_ab.txt).
+# Reproduce at commit bb82676 (before the MIA_UPCONV_PREMOD=0 path was removed; results in profiles/r06_upconv_premod_ab.txt).
 # round 6: the 2-byte up-conv forward with its halo modulated once in LDS per channel block
 # (conv_upconv.hip PREMOD, the product) against the round-5 per-fragment modulation
 # (libmiattack_premod0.so: make variant VARIANT=premod0 VARIANT_FLAGS=-DMIA_UPCONV_PREMOD=0):

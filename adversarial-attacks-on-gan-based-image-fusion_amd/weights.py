@@ -183,7 +183,8 @@ def make_e4e_weights(size, seed=0, start_from_latent_avg=True):
     """Seeded Encoder4Editing(50, 'ir_se') state dict (eval-mode BatchNorm running statistics
     included) for a generator of output size ``size`` (style_count = n_latent). Scales keep the
     24-unit residual stack O(1): He-normal convs, BatchNorm γ of the residual branch ≈ 0.3,
-    PReLU slopes ≈ 0.25 (PyTorch's init; kept > 0)."""
+    PReLU slopes ≈ 0.25 (PyTorch's init; kept > 0 here — the encoder also takes slopes ≤ 0,
+    tests/test_gpu_e4e.py::test_e4e_negative_prelu_slopes_vs_forced_oracle)."""
     g = torch.Generator().manual_seed(int(seed))
     p = {}
 

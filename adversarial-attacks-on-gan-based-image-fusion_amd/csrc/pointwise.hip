@@ -119,6 +119,8 @@ __constant__ float kBlur4[4] = {0.25f, 0.75f, 0.75f, 0.25f};
 //   backward: out = gT (N,2R+1,2R+1,C), in = gy (N,2R,2R,C),     input row of output row 0 is −2
 // (the adjoint flips the taps; the kernel is symmetric so the weights are the same).
 constexpr int kBlurKQ = 4;
+static __device__ __attribute__((aligned(16))) uint4 g_blur_zero[1];  // zero page (out-of-range taps)
+
 
 // V consecutive fp32 values (V = 8 or 4) with 16-byte loads
 template <int V>
@@ -147,12 +149,23 @@ __global__ __launch_bounds__(256) void blur4_strip_kernel(
   const int nc = C / V;
   const int64_t total = (int64_t)N * SY * Q * nc;
   for (int64_t i = blockIdx.x * (int64_t)TPB + threadIdx.x; i < total; i += (int64_t)gridDim.x * TPB) {
-    const int cv = (int)(i % nc);
-    const int64_t r1 = i / nc;
-    const int qx = (int)(r1 % Q);
-    const int64_t r2 = r1 / Q;
-    const int sy = (int)(r2 % SY);
-    const int n = (int)(r2 / SY);
+    int cv, qx, sy, n;
+    if (total < (1LL << 31)) {  // 32-bit divisions: a third of the 64-bit ones' VALU
+      unsigned u = (unsigned)i;
+      cv = (int)(u % (unsigned)nc);
+      u /= (unsigned)nc;
+      qx = (int)(u % (unsigned)Q);
+      u /= (unsigned)Q;
+      sy = (int)(u % (unsigned)SY);
+      n = (int)(u / (unsigned)SY);
+    } else {
+      cv = (int)(i % nc);
+      const int64_t r1 = i / nc;
+      qx = (int)(r1 % Q);
+      const int64_t r2 = r1 / Q;
+      sy = (int)(r2 % SY);
+      n = (int)(r2 / SY);
+    }
     const int x0 = 2 * qx + off0, y0 = sy * OR + off0;
     const int oy0 = sy * OR, ox0 = 2 * qx;
     float dm[V], bs[V];
@@ -177,8 +190,9 @@ __global__ __launch_bounds__(256) void blur4_strip_kernel(
       for (int b = 0; b < 2; ++b)
         nzs[a][b] = NOISE ? noise[min(oy0 + a, Hout - 1) * Hout + min(ox0 + b, Hout - 1)] : 0.f;
     float acc[OR][2][V];
-    // software pipeline: rows rl+1, rl+2 are in flight while row rl is filtered. Loads are unconditional
-    // (clamped addresses) and out-of-range taps are zeroed afterwards, so nothing serialises them.
+    // software pipeline: rows rl+1, rl+2 are in flight while row rl is filtered. Loads are
+    // unconditional: an out-of-range tap reads the zero page (round 6: the address is selected,
+    // not the loaded values zeroed; with 32-bit index math −1 … −4 %, profiles/r06_blur_v2_ab.txt).
     int xc[5];
     bool xv[5];
 #pragma unroll
@@ -188,15 +202,19 @@ __global__ __launch_bounds__(256) void blur4_strip_kernel(
       xc[lc] = min(max(xx, 0), Hin - 1);
     }
     VT nx1[5], nx2[5];
+    // out-of-range taps load the zero page (the address is selected, not the 8 loaded values)
+    auto src = [&](int yy, int lc) {
+      const bool ok = yy >= 0 && yy < Hin && xv[lc];
+      return ok ? base + ((size_t)yy * Hin + xc[lc]) * C : (const T*)g_blur_zero;
+    };
 #pragma unroll
     for (int lc = 0; lc < 5; ++lc) {
-      nx1[lc] = *(const VT*)(base + ((size_t)min(max(y0, 0), Hin - 1) * Hin + xc[lc]) * C);
-      nx2[lc] = *(const VT*)(base + ((size_t)min(max(y0 + 1, 0), Hin - 1) * Hin + xc[lc]) * C);
+      nx1[lc] = *(const VT*)src(y0, lc);
+      nx2[lc] = *(const VT*)src(y0 + 1, lc);
     }
 #pragma unroll
     for (int rl = 0; rl < IR; ++rl) {
       const int yy = y0 + rl;
-      const bool rv = yy >= 0 && yy < Hin;
       VT v[5];
 #pragma unroll
       for (int lc = 0; lc < 5; ++lc) {
@@ -204,16 +222,9 @@ __global__ __launch_bounds__(256) void blur4_strip_kernel(
         nx1[lc] = nx2[lc];
       }
       if (rl + 2 < IR) {
-        const int yc = min(max(yy + 2, 0), Hin - 1);
 #pragma unroll
-        for (int lc = 0; lc < 5; ++lc)
-          nx2[lc] = *(const VT*)(base + ((size_t)yc * Hin + xc[lc]) * C);
+        for (int lc = 0; lc < 5; ++lc) nx2[lc] = *(const VT*)src(yy + 2, lc);
       }
-#pragma unroll
-      for (int lc = 0; lc < 5; ++lc)
-        if (!(rv && xv[lc]))
-#pragma unroll
-          for (int e = 0; e < V; ++e) v[lc][e] = (T)0.f;
       float h[2][V];
 #pragma unroll
       for (int b = 0; b < 2; ++b)

@@ -30,9 +30,7 @@ template <> __device__ __forceinline__ __bf16 from_f<__bf16>(float v) { return (
 constexpr float SQRT2 = 1.41421356237309504880f;
 
 // FusedLeakyReLU (rosinality op/fused_act): leaky_relu(v, 0.2) * sqrt(2); bias already in v.
-// (max(v, 0.2·v) is the same value for every v, ±0 included: one v_max instead of a compare, a
-// select and the VCC hazard between them)
-__device__ __forceinline__ float lrelu_s2(float v) { return fmaxf(v, 0.2f * v) * SQRT2; }
+__device__ __forceinline__ float lrelu_s2(float v) { return (v > 0.f ? v : 0.2f * v) * SQRT2; }
 __device__ __forceinline__ float lrelu_s2_grad(float pre) { return pre > 0.f ? SQRT2 : 0.2f * SQRT2; }
 // 1 / lrelu_s2_grad: the pre-activation from a stored activation a = lrelu_s2(pre) is a · this
 // (a multiply instead of a fp32 division in the backward-front epilogues)

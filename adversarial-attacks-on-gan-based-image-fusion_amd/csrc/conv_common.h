@@ -37,7 +37,7 @@ struct ConvK {
   int prered;                    // register epilogues: pre-reduce the sums across the M waves in
                                  // LDS before the atomics; on for the channel sum (SE pool) only:
                                  // measured, the extra barrier costs more than it saves for the
-                                 // sdot / q sums of the StyledConv dgrads (MIA_EPI_PRERED=0: off)
+                                 // sdot / q sums of the StyledConv dgrads
   int batched;                   // groups carry image / channel offsets: LDS-staged epilogue only
   int prio;                      // X6B tile: s_setprio(1) around the MFMA blocks
   // deterministic sums (mia_common.h RedQ): partial slots of sdot (q 0), bab_q (1), csum (2)

@@ -23,9 +23,52 @@ static int ew_grid(int64_t n) {
 __device__ __forceinline__ float chan_total(const float* __restrict__ v, int nch, int n, int C,
                                             int c) {
   if (nch == 0) return v[(size_t)n * C + c];
+  const float* p = v + (size_t)n * nch * C + c;
   float s = 0.f;
-  for (int q = 0; q < nch; ++q) s += v[((size_t)n * nch + q) * C + c];
+  int q = 0;
+  for (; q + 8 <= nch; q += 8) {  // loads batched ahead of the in-order adds (bit-identical)
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = p[(size_t)(q + u) * C];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += t[u];
+  }
+  for (; q < nch; ++q) s += p[(size_t)q * C];
   return s;
+}
+
+// Σ_{j<Cr} w[j]·x[j] in j order with the (strided) weight loads batched by 8 — the SE FCs' inner
+// loops, one L2 round trip per batch instead of per term (bit-identical to the plain loop)
+__device__ __forceinline__ float dot_strided(const float* __restrict__ w, size_t stride,
+                                             const float* x, int Cr) {
+  float a = 0.f;
+  int j = 0;
+  for (; j + 8 <= Cr; j += 8) {
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = w[(size_t)(j + u) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) a = __builtin_fmaf(t[u], x[j + u], a);  // (fused, as the loop's)
+  }
+  for (; j < Cr; ++j) a += w[(size_t)j * stride] * x[j];
+  return a;
+}
+
+// Σ over this lane's channels c = lane + 64·u < C (C ≤ 512) of w[c·stride]·x[c], in u order with
+// the weight loads issued first (bit-identical to the c += 64 loop)
+__device__ __forceinline__ float lane_dot8(const float* __restrict__ w, size_t stride,
+                                           const float* x, int lane, int C) {
+  float t[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int c = lane + 64 * u;
+    t[u] = c < C ? w[(size_t)c * stride] : 0.f;
+  }
+  float a = 0.f;
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (lane + 64 * u < C) a = __builtin_fmaf(t[u], x[lane + 64 * u], a);
+  return a;
 }
 
 // ---- SE forward: u = relu(W1·avg), s = sigmoid(W2·u), one block per image ----------------------
@@ -39,9 +82,7 @@ __global__ __launch_bounds__(256) void se_fwd_kernel(const float* __restrict__ c
   for (int c = tid; c < C; c += 256) avg[c] = chan_total(csum, nch, n, C, c) * inv_hw;
   __syncthreads();
   for (int j = wid; j < Cr; j += 4) {
-    float a = 0.f;
-    for (int c = lane; c < C; c += 64) a += w1[(size_t)j * C + c] * avg[c];
-    a = wave_sum(a);
+    const float a = wave_sum(lane_dot8(w1 + (size_t)j * C, 1, avg, lane, C));
     if (lane == 0) {
       const float r = a > 0.f ? a : 0.f;
       uu[j] = r;
@@ -50,8 +91,7 @@ __global__ __launch_bounds__(256) void se_fwd_kernel(const float* __restrict__ c
   }
   __syncthreads();
   for (int c = tid; c < C; c += 256) {
-    float z = 0.f;
-    for (int j = 0; j < Cr; ++j) z += w2[(size_t)c * Cr + j] * uu[j];
+    const float z = dot_strided(w2 + (size_t)c * Cr, 1, uu, Cr);
     s_out[(size_t)n * C + c] = 1.f / (1.f + __expf(-z));
   }
 }
@@ -72,15 +112,12 @@ __global__ __launch_bounds__(256) void se_bwd_kernel(const float* __restrict__ g
   }
   __syncthreads();
   for (int j = wid; j < Cr; j += 4) {
-    float a = 0.f;
-    for (int c = lane; c < C; c += 64) a += w2[(size_t)c * Cr + j] * gz[c];
-    a = wave_sum(a);
+    const float a = wave_sum(lane_dot8(w2 + j, Cr, gz, lane, C));
     if (lane == 0) gu[j] = u[(size_t)n * Cr + j] > 0.f ? a : 0.f;
   }
   __syncthreads();
   for (int c = tid; c < C; c += 256) {
-    float a = 0.f;
-    for (int j = 0; j < Cr; ++j) a += w1[(size_t)j * C + c] * gu[j];
+    const float a = dot_strided(w1 + c, C, gu, Cr);
     gavg[(size_t)n * C + c] = a * inv_hw;
   }
 }

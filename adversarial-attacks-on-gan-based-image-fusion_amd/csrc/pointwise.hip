@@ -334,8 +334,34 @@ __global__ void upfirdn2d_bwd_kernel(const float* __restrict__ gy, float* __rest
 // pixel (each lane a slice of channels); the 3 partial dot products are reduced by shuffles.
 __constant__ float kUp4[4] = {0.25f, 0.75f, 0.75f, 0.25f};  // [1,3,3,1]/sum · 2 (per axis)
 
-template <typename T>
-__global__ void torgb_fwd_kernel(const T* __restrict__ pre, const float* __restrict__ s,
+// The ToRGB skip term upfirdn2d(skip, [1,3,3,1]⊗[1,3,3,1]/16·4, up = 2, pad = (2, 1)) at output
+// (y, x): the two taps per axis that land on input samples, added in upfir_at's order with its
+// expression (bit-identical), loaded unconditionally from clamped addresses (out-of-range taps
+// zeroed) so that the four loads issue back-to-back.
+__device__ __forceinline__ float skip_up2(const float* __restrict__ sk, int Hs, int Ws, int y,
+                                          int x) {
+  const int py = y & 1, px = x & 1;
+  const int iy0 = (y - 2 + py) >> 1, ix0 = (x - 2 + px) >> 1;
+  float v[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int iy = iy0 + a, ix = ix0 + b;
+      const bool ok = iy >= 0 && iy < Hs && ix >= 0 && ix < Ws;
+      const float t = sk[min(max(iy, 0), Hs - 1) * Ws + min(max(ix, 0), Ws - 1)];
+      v[a][b] = ok ? t : 0.f;
+    }
+  float acc = 0.f;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc += v[a][b] * kUp4[py + 2 * a] * kUp4[px + 2 * b];
+  return acc;
+}
+
+template <typename T, int LV>
+__global__ __launch_bounds__(TPB) void torgb_fwd_kernel(const T* __restrict__ pre, const float* __restrict__ s,
                                  const float* __restrict__ wr, const float* __restrict__ bias,
                                  const float* __restrict__ skip, float* __restrict__ rgb, int H,
                                  int W, int Cin, int tpp, int cpt, int pix_per_block, int act_in) {
@@ -346,13 +372,38 @@ __global__ void torgb_fwd_kernel(const T* __restrict__ pre, const float* __restr
   const int n = blockIdx.y;
   for (int i = threadIdx.x; i < 3 * Cin; i += TPB) wm[i] = wr[i] * s[(size_t)n * Cin + (i % Cin)];
   __syncthreads();
-  const int HW = H * W;
+  const int HW = H * W, Hs = H / 2, Ws = W / 2;
   const int t = threadIdx.x;
   const int g = t % tpp, sub = t / tpp, ppp = TPB / tpp;
   const int p_begin = blockIdx.x * pix_per_block;
   const int p_end = min(p_begin + pix_per_block, HW);
   const T* img = pre + (size_t)n * HW * Cin;
+  // The 12 sums (pixel u, channel c) of a lane group sit in 16 slots k = 4u + c (c = 3 empty) and
+  // are reduce-scattered over the group's lanes: at level o (o = 1, 2, 4, 8 while o < tpp) a lane
+  // keeps the half of its slots picked by lane bit o and adds the partner's copy of that half —
+  // 8 + 4 + 2 + 1 shuffles instead of a butterfly's 12 per level; levels o ≥ 16 add the one slot
+  // left. Each addition pairs the same lanes in the same level order as a butterfly (own +
+  // partner), so every sum is bit-identical to it. LV = min(4, log2 tpp) scatter levels (a
+  // template parameter: levels skipped at run time would keep both versions of the slots live).
+  // This lane ends with slots base … base + nsl − 1.
+  constexpr int nsl = 16 >> LV;
+  int base = 0;
+#pragma unroll
+  for (int lv = 0; lv < LV; ++lv)
+    if (g & (1 << lv)) base += 8 >> lv;
+  const bool owner = g < 16;  // lanes g ≥ 16 hold copies of lanes g − 16's slots
+  auto skip_at = [&](int k, int pb) {  // the up-sampled skip term of slot k (0 if none)
+    const int u = k >> 2, c = k & 3, p = pb + u * ppp + sub;
+    if (!skip || !owner || c == 3 || p >= p_end) return 0.f;
+    const int y = p / W, x = p - (p / W) * W;
+    return skip_up2(skip + ((size_t)n * 3 + c) * Hs * Ws, Hs, Ws, y, x);
+  };
   for (int pb = p_begin; pb < p_end; pb += ppp * U) {
+    // the skip terms first: their loads overlap the channel loads instead of following the
+    // reduction (tpp ≥ 4, the launcher's check: at most 4 slots per lane)
+    float skv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) skv[i] = i < nsl ? skip_at(base + i, pb) : 0.f;
     float a[U][3];
 #pragma unroll
     for (int u = 0; u < U; ++u) a[u][0] = a[u][1] = a[u][2] = 0.f;
@@ -370,34 +421,45 @@ __global__ void torgb_fwd_kernel(const T* __restrict__ pre, const float* __restr
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const float x = act_in ? lrelu_s2(to_f(v[u][e])) : to_f(v[u][e]);
-          a[u][0] += x * w0;
-          a[u][1] += x * w1;
-          a[u][2] += x * w2;
+          // fused explicitly: a contractible a += x·w may be left unfused when the vectorizer
+          // pairs the products, which made the 2-byte outputs depend on code generation
+          a[u][0] = __builtin_fmaf(x, w0, a[u][0]);
+          a[u][1] = __builtin_fmaf(x, w1, a[u][1]);
+          a[u][2] = __builtin_fmaf(x, w2, a[u][2]);
         }
       }
     }
-    // butterfly: every lane of the group ends with the full sums
-    for (int o = 1; o < tpp; o <<= 1)
+    float sl[16];
 #pragma unroll
-      for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
+      sl[4 * u] = a[u][0];
+      sl[4 * u + 1] = a[u][1];
+      sl[4 * u + 2] = a[u][2];
+      sl[4 * u + 3] = 0.f;
+    }
 #pragma unroll
-        for (int c = 0; c < 3; ++c) a[u][c] += __shfl_xor(a[u][c], o, 64);
-    // lanes g = 3u + c (g < 3U ≤ tpp) each finish one (pixel, channel); tpp < 12 loops
-    for (int k = g; k < 3 * U; k += tpp) {
-      const int u = k / 3, c = k - 3 * (k / 3);
-      const int p = pb + u * ppp + sub;
-      if (p >= p_end) continue;
-      float r = bias[c];
+    for (int lv = 0; lv < LV; ++lv) {
+      const int o = 1 << lv, h = 8 >> lv;
+      const bool hi = (g & o) != 0;
 #pragma unroll
-      for (int uu = 0; uu < U; ++uu)
-#pragma unroll
-        for (int cc2 = 0; cc2 < 3; ++cc2)
-          if (uu == u && cc2 == c) r += a[uu][cc2];
-      if (skip) {
-        const int y = p / W, x = p - (p / W) * W;
-        const int Hs = H / 2, Ws = W / 2;
-        r += upfir_at(skip + ((size_t)n * 3 + c) * Hs * Ws, Hs, Ws, y, x, kUp4, 4, 2, 1, 2);
+      for (int i = 0; i < h; ++i) {
+        // (the asm hides that both operands are loads of sl: folding the selects into one
+        // select-indexed load would keep sl in memory as a 16-way compare chain)
+        float x = sl[i], y = sl[h + i];
+        asm volatile("" : "+v"(x), "+v"(y));
+        const float keep = hi ? y : x, send = hi ? x : y;
+        sl[i] = keep + __shfl_xor(send, o, 64);
       }
+    }
+    for (int o = 16; o < tpp; o <<= 1) sl[0] += __shfl_xor(sl[0], o, 64);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = base + i, u = k >> 2, c = k & 3;
+      const int p = pb + u * ppp + sub;
+      if (i >= nsl || !owner || c == 3 || p >= p_end) continue;
+      float r = bias[c];
+      r += sl[i];
+      if (skip) r += skv[i];
       rgb[((size_t)n * 3 + c) * HW + p] = r;
     }
   }
@@ -1053,13 +1115,23 @@ extern "C" int mia_torgb_fwd(const void* pre, const float* style, const float* w
   int tpp = 1;
   while (tpp * 2 <= nch && tpp * 2 <= 64) tpp *= 2;
   MIA_CHECK_ARG(nch % tpp == 0, "Cin/V must be a power of two times tpp");
+  // (the kernel's reduce-scatter leaves each lane ≤ 4 of its 16 sum slots from 4 lanes on)
+  MIA_CHECK_ARG(tpp >= 4, "Cin must be at least 4 vectors (16 fp32 / 32 fp16 / bf16 channels)");
   const int cpt = nch / tpp;
   const int ppb = (TPB / tpp) * 16;  // 4 passes of U = 4 pixels per lane group
   dim3 grid((H * W + ppb - 1) / ppb, N);
   const size_t sh = 3 * Cin * sizeof(float);
-  MIA_DISPATCH_DTYPE(dtype, T,
-      MIA_LAUNCH(torgb_fwd_kernel<T>, grid, dim3(TPB), sh, (const T*)pre, style, wr, bias, skip,
-                 rgb, H, W, Cin, tpp, cpt, ppb, act_in));
+  MIA_DISPATCH_DTYPE(dtype, T, {
+    if (tpp >= 16)
+      MIA_LAUNCH((torgb_fwd_kernel<T, 4>), grid, dim3(TPB), sh, (const T*)pre, style, wr, bias,
+                 skip, rgb, H, W, Cin, tpp, cpt, ppb, act_in);
+    else if (tpp == 8)
+      MIA_LAUNCH((torgb_fwd_kernel<T, 3>), grid, dim3(TPB), sh, (const T*)pre, style, wr, bias,
+                 skip, rgb, H, W, Cin, tpp, cpt, ppb, act_in);
+    else
+      MIA_LAUNCH((torgb_fwd_kernel<T, 2>), grid, dim3(TPB), sh, (const T*)pre, style, wr, bias,
+                 skip, rgb, H, W, Cin, tpp, cpt, ppb, act_in);
+  });
   return MIA_OK;
 }
 

@@ -232,8 +232,19 @@ __global__ __launch_bounds__(256) void demod_bwd_kernel(const float* __restrict_
   const int ci = blockIdx.x * 64 + lane;
   const int per = (Cout + 3) / 4, c0 = qtr * per, c1 = min(c0 + per, Cout);
   float acc = 0.f;
-  if (ci < Cin)
-    for (int co = c0; co < c1; ++co) acc += r[co] * wsq[(size_t)co * Cin + ci];
+  if (ci < Cin) {
+    // the weight loads in batches of 8 ahead of their (in-order) FMAs: one L2 round trip per batch
+    // instead of one per output channel (same sum order, bit-identical)
+    int co = c0;
+    for (; co + 8 <= c1; co += 8) {
+      float w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) w[u] = wsq[(size_t)(co + u) * Cin + ci];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc = __builtin_fmaf(r[co + u], w[u], acc);  // fused, as before
+    }
+    for (; co < c1; ++co) acc += r[co] * wsq[(size_t)co * Cin + ci];
+  }
   part[qtr * 64 + lane] = acc;
   __syncthreads();
   if (qtr == 0 && ci < Cin) {

@@ -217,7 +217,9 @@ __global__ __launch_bounds__(TL::NT, TL::NW == 4 && TL::STAGES <= 3 ? (TL::BM < 
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = G.kpad / BK;
+  // K-steps of this group's taps (= kpad / BK for a full weight row; an edge group of the up-conv
+  // runs only the leading taps of its rows, kpad staying the row stride)
+  const int nk = (ntap * Cin + BK - 1) / BK;
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) issue(s, s);
@@ -523,6 +525,11 @@ int conv_red_begin(ConvK& k, RedQ& r, int nslots, hipStream_t st, bool zero) {
 
 static int bk_for(int dtype) { return dtype == MIA_F32 ? 32 : 64; }
 
+// the up-conv edge groups on their leading (in-range) taps only; tuning A/B: =0 the full windows
+#ifndef MIA_UPCONV_EDGE_TRIM
+#define MIA_UPCONV_EDGE_TRIM 1
+#endif
+
 static int kpad_for(int k, int dtype) {
   const int bk = bk_for(dtype);
   return (k + bk - 1) / bk * bk;
@@ -557,7 +564,8 @@ static int run_conv(ConvK& k, int dtype, hipStream_t st) {
     const ConvGroup& G = k.g[g];
     MIA_CHECK_ARG(G.w, "w is required");
     MIA_CHECK_ARG(G.kh >= 1 && G.kh <= 3 && G.kw >= 1 && G.kw <= 3, "taps 1..3");
-    MIA_CHECK_ARG(G.kpad == kpad_for(G.kh * G.kw * a.Cin, dtype), "Kpad must be mia_conv_kpad()");
+    MIA_CHECK_ARG(G.kpad >= kpad_for(G.kh * G.kw * a.Cin, dtype) && G.kpad % bk_for(dtype) == 0,
+                  "Kpad must be mia_conv_kpad()");
     MIA_CHECK_ARG(G.ho > 0 && G.wo > 0, "empty output grid");
     MIA_CHECK_ARG((int64_t)a.N * G.ho * G.wo < (1LL << 31), "too many pixels");
     MIA_CHECK_ARG(!(a.sdot || a.bab_demod) || (k.ng == 1 && G.ho * G.wo == k.HT * k.WT),
@@ -598,6 +606,7 @@ extern "C" int mia_conv_kpad(int cin, int dtype) { return kpad_for(9 * cin, dtyp
 extern "C" int mia_conv3x3(const mia_conv_args* args, int dtype, void* stream) {
   MIA_CHECK_ARG(args != nullptr, "null args");
   const mia_conv_args& a = *args;
+  MIA_CHECK_ARG(a.Kpad == kpad_for(9 * a.Cin, dtype), "Kpad must be mia_conv_kpad()");
   ConvK k = {};
   k.a = a;
   k.stride = 1;
@@ -780,7 +789,12 @@ extern "C" int mia_upconv_fwd_halo_split(const void* x, const void* const* w_pha
   k.cout_mod = Cout;
   k.ystride = Cout;
   // {phase, row group?}: (0,0) row y = R (x ∈ [0,R]), (0,1) row y = R (x ∈ [0,R)),
-  //                      (0,0) column x = R (y ∈ [0,R)), (1,0) column x = R (y ∈ [0,R))
+  //                      (0,0) column x = R (y ∈ [0,R)), (1,0) column x = R (y ∈ [0,R)).
+  // Only the window's first tap row (row groups) / column (columns) lies inside the input; where
+  // those taps lead the weight row (both row groups, the (1,0) column) the group runs just them
+  // (kh or kw = 1, the row stride kept in kpad): the MFMAs on the zero taps are skipped, the
+  // sums unchanged (each skipped product was an exact zero). The (0,0) column's valid taps
+  // (t = 0, 2) are not contiguous in K and keep the full window.
   const int phs[4] = {0, 1, 0, 2};
   const bool rowg[4] = {true, true, false, false};
   for (int g = 0; g < 4; ++g) {
@@ -795,10 +809,12 @@ extern "C" int mia_upconv_fwd_halo_split(const void* x, const void* const* w_pha
       G.ho = 1; G.wo = R + 1 - px;
       G.pad_y = (G.kh - 1) - R; G.pad_x = G.kw - 1;
       G.by = 2 * R + py; G.bx = px;
+      if (MIA_UPCONV_EDGE_TRIM) G.kh = 1;  // taps ty = 0 (input row R − 1) lead the row
     } else {
       G.ho = R; G.wo = 1;
       G.pad_y = G.kh - 1; G.pad_x = (G.kw - 1) - R;
       G.by = py; G.bx = 2 * R + px;
+      if (MIA_UPCONV_EDGE_TRIM && G.kh == 1) G.kw = 1;  // tap tx = 0 (input column R − 1)
     }
     G.m = pixels_clamped(N, G.ho, G.wo);
   }

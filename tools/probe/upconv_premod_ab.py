@@ -1,7 +1,8 @@
 """A/B of the 2-byte up-conv forward's style modulation (conv_upconv.hip upconv_halo_kernel, PRO
 launches): run the up-sampling StyledConv shapes of the 256² / 1024² generators with the loaded
 build, save outputs + per-call times; `--compare A B` checks two saved runs bit for bit (tuning
-aid, not product).
+aid, not product). `--dtypes fp32,fp16` picks the dtypes (fp32: the split-once kernel + its
+generic edge launch, as the product calls it).
 
     MIA_LIB_VARIANT=premod0 python tools/probe/upconv_premod_ab.py --out /tmp/up0.pt
     python tools/probe/upconv_premod_ab.py --out /tmp/up1.pt
@@ -24,10 +25,10 @@ SHAPES = [(128, 128, 256, 128), (128, 64, 512, 256), (128, 32, 512, 512), (128, 
           (32, 256, 128, 64), (32, 512, 64, 32)]
 
 
-def run(out):
+def run(out, dtypes):
     dev = torch.device("cuda:0")
     res = {}
-    for dtype in (torch.float16, torch.bfloat16):
+    for dtype in dtypes:
         for N, R, cin, cout in SHAPES:
             g = torch.Generator().manual_seed(R + cin)
             x = torch.randn(N, R, R, cin, generator=g).to(dtype).to(dev)
@@ -53,7 +54,7 @@ def run(out):
 
 
 def compare(a, b):
-    A, B = torch.load(a), torch.load(b)
+    A, B = torch.load(a, weights_only=True), torch.load(b, weights_only=True)
     for k in A:
         nd = int((A[k] != B[k]).sum())
         print(f"{k:32s} {'bit-identical' if nd == 0 else f'{nd} values differ'}")
@@ -64,8 +65,10 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--out")
     ap.add_argument("--compare", nargs=2)
+    ap.add_argument("--dtypes", default="fp16,bf16", help="comma list of fp32, fp16, bf16")
     a = ap.parse_args()
     if a.compare:
         compare(*a.compare)
     else:
-        run(a.out)
+        DT = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
+        run(a.out, [DT[d] for d in a.dtypes.split(",")])

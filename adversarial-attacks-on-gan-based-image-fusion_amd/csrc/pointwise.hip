@@ -118,7 +118,13 @@ __constant__ float kBlur4[4] = {0.25f, 0.75f, 0.75f, 0.25f};
 //   forward : out = pre (N,2R,2R,C),    in = T  (N,2R+1,2R+1,C), input row of output row 0 is −1
 //   backward: out = gT (N,2R+1,2R+1,C), in = gy (N,2R,2R,C),     input row of output row 0 is −2
 // (the adjoint flips the taps; the kernel is symmetric so the weights are the same).
-constexpr int kBlurKQ = 4;
+#ifndef MIA_BLUR_PF  // input rows in flight per thread (tuning A/B: -DMIA_BLUR_PF=3, 4)
+#define MIA_BLUR_PF 2
+#endif
+#ifndef MIA_BLUR_KQ  // output rows per strip / 2 (tuning A/B: -DMIA_BLUR_KQ=2, 3)
+#define MIA_BLUR_KQ 4
+#endif
+constexpr int kBlurKQ = MIA_BLUR_KQ;
 static __device__ __attribute__((aligned(16))) uint4 g_blur_zero[1];  // zero page (out-of-range taps)
 
 
@@ -190,7 +196,7 @@ __global__ __launch_bounds__(256) void blur4_strip_kernel(
       for (int b = 0; b < 2; ++b)
         nzs[a][b] = NOISE ? noise[min(oy0 + a, Hout - 1) * Hout + min(ox0 + b, Hout - 1)] : 0.f;
     float acc[OR][2][V];
-    // software pipeline: rows rl+1, rl+2 are in flight while row rl is filtered. Loads are
+    // software pipeline: rows rl+1 … rl+PF are in flight while row rl is filtered. Loads are
     // unconditional: an out-of-range tap reads the zero page (round 6: the address is selected,
     // not the loaded values zeroed; with 32-bit index math −1 … −4 %, profiles/r06_blur_v2_ab.txt).
     int xc[5];
@@ -201,29 +207,30 @@ __global__ __launch_bounds__(256) void blur4_strip_kernel(
       xv[lc] = xx >= 0 && xx < Hin;
       xc[lc] = min(max(xx, 0), Hin - 1);
     }
-    VT nx1[5], nx2[5];
+    constexpr int PF = MIA_BLUR_PF;  // input rows in flight ahead of the one being filtered
+    VT nx[PF][5];
     // out-of-range taps load the zero page (the address is selected, not the 8 loaded values)
     auto src = [&](int yy, int lc) {
       const bool ok = yy >= 0 && yy < Hin && xv[lc];
       return ok ? base + ((size_t)yy * Hin + xc[lc]) * C : (const T*)g_blur_zero;
     };
 #pragma unroll
-    for (int lc = 0; lc < 5; ++lc) {
-      nx1[lc] = *(const VT*)src(y0, lc);
-      nx2[lc] = *(const VT*)src(y0 + 1, lc);
-    }
+    for (int q = 0; q < PF; ++q)
+#pragma unroll
+      for (int lc = 0; lc < 5; ++lc) nx[q][lc] = *(const VT*)src(y0 + q, lc);
 #pragma unroll
     for (int rl = 0; rl < IR; ++rl) {
       const int yy = y0 + rl;
       VT v[5];
 #pragma unroll
       for (int lc = 0; lc < 5; ++lc) {
-        v[lc] = nx1[lc];
-        nx1[lc] = nx2[lc];
-      }
-      if (rl + 2 < IR) {
+        v[lc] = nx[0][lc];
 #pragma unroll
-        for (int lc = 0; lc < 5; ++lc) nx2[lc] = *(const VT*)src(yy + 2, lc);
+        for (int q = 0; q + 1 < PF; ++q) nx[q][lc] = nx[q + 1][lc];
+      }
+      if (rl + PF < IR) {
+#pragma unroll
+        for (int lc = 0; lc < 5; ++lc) nx[PF - 1][lc] = *(const VT*)src(yy + PF, lc);
       }
       float h[2][V];
 #pragma unroll

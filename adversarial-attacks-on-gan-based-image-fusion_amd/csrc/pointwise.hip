@@ -118,8 +118,10 @@ __constant__ float kBlur4[4] = {0.25f, 0.75f, 0.75f, 0.25f};
 //   forward : out = pre (N,2R,2R,C),    in = T  (N,2R+1,2R+1,C), input row of output row 0 is −1
 //   backward: out = gT (N,2R+1,2R+1,C), in = gy (N,2R,2R,C),     input row of output row 0 is −2
 // (the adjoint flips the taps; the kernel is symmetric so the weights are the same).
-#ifndef MIA_BLUR_PF  // input rows in flight per thread (tuning A/B: -DMIA_BLUR_PF=3, 4)
-#define MIA_BLUR_PF 2
+// input rows in flight per thread: 4 (round 6; 2 before: fp32 forward / adjoint −1.5 / −3.9 %,
+// fp16 −2.9 / −2.5 % per generator pass, still 2 waves per SIMD; profiles/r06_blur_pf_ab.txt)
+#ifndef MIA_BLUR_PF
+#define MIA_BLUR_PF 4
 #endif
 #ifndef MIA_BLUR_KQ  // output rows per strip / 2 (tuning A/B: -DMIA_BLUR_KQ=2, 3)
 #define MIA_BLUR_KQ 4

@@ -39,7 +39,7 @@ def run(a):
     g = torch.Generator(device=dev).manual_seed(7)
     N = a.batch
     out = {}
-    tot = 0.0
+    tot = tot_b = 0.0
     for R, C in ((4, 512), (8, 512), (16, 512), (32, 512), (64, 512), (128, 256), (256, 128)):
         pre = torch.randn(N, R, R, C, device=dev, generator=g).to(T)
         st = torch.randn(N, C, device=dev, generator=g)
@@ -50,9 +50,36 @@ def run(a):
         us = timeit(lambda: ops.torgb_fwd(pre, st, wr, b, skip, rgb))
         tot += us
         out[f"torgb_{R}"] = rgb.clone()
-        print(f"torgb_fwd R={R:3d} C={C:3d}: {us:8.1f} us  {pre.numel() * pre.element_size() / us / 1e6:5.2f} TB/s",
+        grgb = torch.randn(N, 3, R, R, device=dev, generator=g)
+        ga = torch.empty_like(pre)
+        gs = torch.empty(N, C, device=dev)
+        ub = timeit(lambda: ops.torgb_bwd(grgb, pre, st, wr, ga, gs, accumulate=False))
+        gs.zero_()
+        ops.torgb_bwd(grgb, pre, st, wr, ga, gs, accumulate=False)
+        out[f"torgb_bwd_{R}"] = torch.cat([ga.float().flatten(), gs.flatten()])
+        tot_b += ub
+        print(f"torgb R={R:3d} C={C:3d}: fwd {us:8.1f} us {pre.numel() * pre.element_size() / us / 1e6:5.2f} TB/s"
+              f" | bwd {ub:8.1f} us {2 * pre.numel() * pre.element_size() / ub / 1e6:5.2f} TB/s", flush=True)
+    print(f"torgb per generator forward: fwd {tot:.1f} us, bwd {tot_b:.1f} us "
+          f"(x20 per PGD-20 step: {tot * 20 / 1e3:.2f} + {tot_b * 20 / 1e3:.2f} ms)")
+    for R, C in ((256, 128), (64, 512)):
+        act = torch.randn(N, R, R, C, device=dev, generator=g).to(T)
+        st = torch.randn(N, C, device=dev, generator=g)
+        wr = torch.randn(3, C, device=dev, generator=g) / C ** 0.5
+        grgb = torch.randn(N, 3, R, R, device=dev, generator=g)
+        gy = torch.empty_like(act)
+        gs = torch.empty(N, C, device=dev)
+        q = torch.empty(N, C, device=dev)
+        dm = torch.rand(N, C, device=dev, generator=g) + 0.5
+        nz = torch.randn(R * R, device=dev, generator=g)
+        bz = torch.randn(C, device=dev, generator=g)
+        uf = timeit(lambda: ops.torgb_bwd_front(grgb, act, st, wr, gy, gs, dm, nz, 0.3, bz, q))
+        gs.zero_()
+        q.zero_()
+        ops.torgb_bwd_front(grgb, act, st, wr, gy, gs, dm, nz, 0.3, bz, q)
+        out[f"torgb_front_{R}"] = torch.cat([gy.float().flatten(), gs.flatten(), q.flatten()])
+        print(f"torgb_bwd_front R={R:3d} C={C:3d}: {uf:8.1f} us {2 * act.numel() * act.element_size() / uf / 1e6:5.2f} TB/s",
               flush=True)
-    print(f"torgb_fwd per generator forward: {tot:.1f} us (x20 per PGD-20 step: {tot * 20 / 1e3:.2f} ms)")
     tot = 0.0
     for Cin, Cout, calls in ((512, 512, 10), (256, 512, 1), (128, 256, 1), (512, 256, 1)):
         q = torch.randn(N, Cout, device=dev, generator=g)

@@ -1,5 +1,6 @@
 """Network- and step-level parity on the GPU: VGG vs the reference's golden vectors, synthesis and
 the full attack gradient vs the CPU oracle, PGD outputs under the sign-stable protocol."""
+import math
 import os
 
 import numpy as np
@@ -145,6 +146,42 @@ def test_synthesis_vs_oracle(cuda, size, dtype, tol):
     ref = stylegan2_ref.synthesis({k: v.double() for k, v in gp.items()}, lat.double(), size)
     assert img.shape == (2, 3, size, size)
     assert rel_err(img, ref) < tol
+
+
+@pytest.mark.parametrize("size,dtype,tol", [(256, torch.float32, 5e-6), (256, torch.float16, 3e-3),
+                                            (128, torch.bfloat16, 2e-2)])
+def test_upsampling_styledconv_vs_oracle(cuda, size, dtype, tol):
+    """Every up-sampling StyledConv of the product generator — the sub-pixel transposed conv (the
+    halo / split-once kernel and its edge launch, or the phase GEMMs below 16²) followed by
+    mia_upconv_blur_fwd (Blur + demod + noise + bias + lrelu·√2) — against the oracle's
+    styled_conv(upsample=True) = rosinality ModulatedConv2d(upsample=True) + NoiseInjection +
+    FusedLeakyReLU (oracle/stylegan2_ref.py:61-114; decoder call attack_main2.py:619-621) in fp64,
+    on the layer's own device input and style (teacher-forced per layer). The tolerance is the
+    dtype's weight / activation rounding."""
+    from gfa_amd.stylegan2 import SynthesisNet
+    gp = make_generator_weights(size, seed=5)
+    net = SynthesisNet(gp, size, dtype=dtype, device=cuda)
+    ws = Workspace(cuda)
+    lat = torch.randn(1, net.n_latent, 512, generator=torch.Generator().manual_seed(6))
+    net.forward(lat.to(cuda), ws)
+    torch.cuda.synchronize()
+    p64 = {k: v.double() for k, v in gp.items()}
+    errs = []
+    for L in net.convs:
+        if not L["up"]:
+            continue
+        x = L["_x"].permute(0, 3, 1, 2).double().cpu()
+        s = L["_s"].double().cpu()
+        r = L["res"]
+        noise = L["noise"].double().cpu().view(1, 1, r, r)  # the layer's fixed noise plane
+        with torch.no_grad():
+            ref = stylegan2_ref.styled_conv(p64, L["name"], x, None, noise, upsample=True, s=s)
+        got = L["_pre"].permute(0, 3, 1, 2)
+        assert got.shape == ref.shape, (L["name"], got.shape, ref.shape)
+        errs.append((L["res"], rel_err(got, ref)))
+    print(f"{dtype} up-sampling StyledConvs (output res, max rel err): {errs}")
+    assert len(errs) == int(math.log2(size)) - 2
+    assert all(e < tol for _, e in errs), errs
 
 
 def _engine(size, dtype, N, cuda, seed=0):

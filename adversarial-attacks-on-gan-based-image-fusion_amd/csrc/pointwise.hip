@@ -409,7 +409,7 @@ __global__ __launch_bounds__(TPB) void torgb_fwd_kernel(const T* __restrict__ pr
   };
   for (int pb = p_begin; pb < p_end; pb += ppp * U) {
     // the skip terms first: their loads overlap the channel loads instead of following the
-    // reduction (tpp ≥ 4, the launcher's check: at most 4 slots per lane)
+    // reduction (the first 4 of the lane's slots: all of them from tpp = 4 on)
     float skv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) skv[i] = i < nsl ? skip_at(base + i, pb) : 0.f;
@@ -462,13 +462,13 @@ __global__ __launch_bounds__(TPB) void torgb_fwd_kernel(const T* __restrict__ pr
     }
     for (int o = 16; o < tpp; o <<= 1) sl[0] += __shfl_xor(sl[0], o, 64);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < nsl; ++i) {
       const int k = base + i, u = k >> 2, c = k & 3;
       const int p = pb + u * ppp + sub;
-      if (i >= nsl || !owner || c == 3 || p >= p_end) continue;
+      if (!owner || c == 3 || p >= p_end) continue;
       float r = bias[c];
       r += sl[i];
-      if (skip) r += skv[i];
+      if (skip) r += i < 4 ? skv[i] : skip_at(k, pb);
       rgb[((size_t)n * 3 + c) * HW + p] = r;
     }
   }
@@ -1114,6 +1114,22 @@ extern "C" int mia_upfirdn2d_bwd(const float* gy, float* gx, int planes, int H, 
              planes, H, W, Ho, Wo, kf, ktaps, up, down, pad0);
 }
 
+// the ToRGB forward with lv = min(4, log2 tpp) reduce-scatter levels (each lane keeps 16 >> lv
+// of the lane group's 16 sum slots)
+template <typename T>
+static int launch_torgb_fwd(dim3 grid, size_t sh, const T* pre, const float* style,
+                            const float* wr, const float* bias, const float* skip, float* rgb,
+                            int H, int W, int Cin, int tpp, int cpt, int ppb, int act_in,
+                            hipStream_t st) {
+  const int lv = tpp >= 16 ? 4 : tpp == 8 ? 3 : tpp == 4 ? 2 : tpp == 2 ? 1 : 0;
+  auto fn = lv == 4 ? torgb_fwd_kernel<T, 4> : lv == 3 ? torgb_fwd_kernel<T, 3>
+          : lv == 2 ? torgb_fwd_kernel<T, 2> : lv == 1 ? torgb_fwd_kernel<T, 1>
+                    : torgb_fwd_kernel<T, 0>;
+  hipLaunchKernelGGL(fn, grid, dim3(TPB), sh, st, pre, style, wr, bias, skip, rgb, H, W, Cin, tpp,
+                     cpt, ppb, act_in);
+  return check_launch("torgb_fwd_kernel");
+}
+
 extern "C" int mia_torgb_fwd(const void* pre, const float* style, const float* wr,
                              const float* bias, const float* skip, float* rgb, int N, int H, int W,
                              int Cin, int act_in, int dtype, void* stream) {
@@ -1124,23 +1140,13 @@ extern "C" int mia_torgb_fwd(const void* pre, const float* style, const float* w
   int tpp = 1;
   while (tpp * 2 <= nch && tpp * 2 <= 64) tpp *= 2;
   MIA_CHECK_ARG(nch % tpp == 0, "Cin/V must be a power of two times tpp");
-  // (the kernel's reduce-scatter leaves each lane ≤ 4 of its 16 sum slots from 4 lanes on)
-  MIA_CHECK_ARG(tpp >= 4, "Cin must be at least 4 vectors (16 fp32 / 32 fp16 / bf16 channels)");
   const int cpt = nch / tpp;
   const int ppb = (TPB / tpp) * 16;  // 4 passes of U = 4 pixels per lane group
   dim3 grid((H * W + ppb - 1) / ppb, N);
   const size_t sh = 3 * Cin * sizeof(float);
-  MIA_DISPATCH_DTYPE(dtype, T, {
-    if (tpp >= 16)
-      MIA_LAUNCH((torgb_fwd_kernel<T, 4>), grid, dim3(TPB), sh, (const T*)pre, style, wr, bias,
-                 skip, rgb, H, W, Cin, tpp, cpt, ppb, act_in);
-    else if (tpp == 8)
-      MIA_LAUNCH((torgb_fwd_kernel<T, 3>), grid, dim3(TPB), sh, (const T*)pre, style, wr, bias,
-                 skip, rgb, H, W, Cin, tpp, cpt, ppb, act_in);
-    else
-      MIA_LAUNCH((torgb_fwd_kernel<T, 2>), grid, dim3(TPB), sh, (const T*)pre, style, wr, bias,
-                 skip, rgb, H, W, Cin, tpp, cpt, ppb, act_in);
-  });
+  MIA_DISPATCH_DTYPE(dtype, T,
+      return launch_torgb_fwd<T>(grid, sh, (const T*)pre, style, wr, bias, skip, rgb, H, W, Cin,
+                                 tpp, cpt, ppb, act_in, (hipStream_t)stream));
   return MIA_OK;
 }
 

@@ -454,7 +454,7 @@ def test_upfirdn2d(cuda, up, down, pad):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
-@pytest.mark.parametrize("cin", [32, 128, 512])
+@pytest.mark.parametrize("cin", [8, 16, 32, 128, 512])  # 1 … 64 lanes per pixel (every level count)
 @pytest.mark.parametrize("stored", ["pre", "act"])
 def test_torgb_fwd_bwd(cuda, dtype, cin, stored):
     g = torch.Generator().manual_seed(cin)

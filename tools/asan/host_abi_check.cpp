@@ -103,9 +103,6 @@ int main() {
                                nullptr), "mse_fwd_bwd no output");
   expect_error(mia_mse_fwd_bwd(dummy, dummy, dummy, dummy, 1, 64, 1.f, 1.f, 1, MIA_F16, nullptr),
                "mse_fwd_bwd fp16 accumulate");
-  // ToRGB forward: at least 4 channel vectors per pixel (the reduce-scatter's lane groups)
-  expect_error(mia_torgb_fwd(dummy, dummy, dummy, dummy, nullptr, dummy, 1, 8, 8, 8, 0, MIA_F32,
-                             nullptr), "torgb_fwd Cin 8");
   expect_error(mia_reserve_reduction_scratch(-1, nullptr), "scratch negative");
   EXPECT(mia_reserve_reduction_scratch(0, nullptr) == MIA_OK, "scratch zero");
 

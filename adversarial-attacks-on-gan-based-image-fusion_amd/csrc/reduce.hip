@@ -132,6 +132,22 @@ int red_begin(RedQ& r, float* d0, float* d1, float* d2, int nslots, int count, h
   return MIA_OK;
 }
 
+// Σ_{k<n} src[k·stride] added in k order, the loads issued 8 ahead of their adds (one memory
+// round trip per 8 slots instead of per slot; bit-identical to the plain loop)
+__device__ __forceinline__ float ordered_sum(const float* __restrict__ src, int n, int stride) {
+  float s = 0.f;
+  int k = 0;
+  for (; k + 8 <= n; k += 8) {
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = src[(size_t)(k + u) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += t[u];
+  }
+  for (; k < n; ++k) s += src[(size_t)k * stride];
+  return s;
+}
+
 __global__ __launch_bounds__(256) void red_finish_kernel(const float* __restrict__ part,
                                                          float* d0, float* d1, float* d2,
                                                          int nslots, int count) {
@@ -141,9 +157,7 @@ __global__ __launch_bounds__(256) void red_finish_kernel(const float* __restrict
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= count) return;
   const float* src = part + (size_t)q * nslots * count + i;
-  float s = 0.f;
-  for (int k = 0; k < nslots; ++k) s += src[(size_t)k * count];
-  dst[i] += s;
+  dst[i] += ordered_sum(src, nslots, count);
 }
 
 // chunk c of quantity q: tmp[q][c][i] = Σ_{slot in chunk c} part[q][slot][i], in slot order
@@ -157,9 +171,7 @@ __global__ __launch_bounds__(256) void red_chunk_kernel(const float* __restrict_
   if (i >= count) return;
   const int k0 = c * RED_CHUNK, k1 = min(k0 + RED_CHUNK, nslots);
   const float* src = part + ((size_t)q * nslots + k0) * count + i;
-  float s = 0.f;
-  for (int k = k0; k < k1; ++k, src += count) s += *src;
-  tmp[((size_t)q * gridDim.y + c) * count + i] = s;
+  tmp[((size_t)q * gridDim.y + c) * count + i] = ordered_sum(src, k1 - k0, count);
 }
 
 int red_finish(const RedQ& r, hipStream_t st) {

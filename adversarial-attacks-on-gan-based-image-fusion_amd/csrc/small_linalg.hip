@@ -205,7 +205,15 @@ __global__ __launch_bounds__(256) void style_demod_kernel(const float* __restric
   if (co >= Cout) return;
   const float* w = wsq + (size_t)co * Cin;
   float acc = 0.f;
-  for (int ci = lane; ci < Cin; ci += 64) acc += s2[ci] * w[ci];
+  int ci = lane;
+  for (; ci + 7 * 64 < Cin; ci += 8 * 64) {  // the row loads 8 ahead of the in-order FMAs
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = w[ci + 64 * u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = __builtin_fmaf(s2[ci + 64 * u], t[u], acc);
+  }
+  for (; ci < Cin; ci += 64) acc = __builtin_fmaf(s2[ci], w[ci], acc);
   acc = wave_sum(acc);
   if (lane == 0) demod[(size_t)n * Cout + co] = rsqrtf(scale2 * acc + 1e-8f);
 }

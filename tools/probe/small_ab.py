@@ -93,6 +93,13 @@ def run(a):
         out[f"demod_{Cin}_{Cout}"] = gs.clone()
         tot += us * calls
         print(f"demod_bwd Cin={Cin} Cout={Cout}: {us:7.1f} us", flush=True)
+    for Cin, Cout in ((512, 512), (256, 128)):
+        s = torch.randn(N, Cin, device=dev, generator=g)
+        wsq = torch.rand(Cout, Cin, device=dev, generator=g)
+        dm = torch.empty(N, Cout, device=dev)
+        us = timeit(lambda: ops.style_demod(s, wsq, dm))
+        out[f"style_demod_{Cin}_{Cout}"] = dm.clone()
+        print(f"style_demod Cin={Cin} Cout={Cout}: {us:7.1f} us", flush=True)
     for C, hw in ((64, 128 * 128), (128, 64 * 64), (256, 32 * 32), (512, 16 * 16)):
         Cr = C // 16
         nch = ops.chan_sum_parts(N, hw)

@@ -730,6 +730,46 @@ __global__ void image_to_nhwc_kernel(const float* __restrict__ x, T* __restrict_
   }
 }
 
+// The same with cpad a multiple of the 16-byte vector (the product's CPAD = 8): one thread per
+// output pixel, its 3 planes' loads coalesced across the wave and its cpad channels written as
+// whole 16-byte vectors (the element-per-thread form wrote 2- / 4-byte scalars at 1.8 TB/s).
+// Same sums in the same order: bit-identical.
+template <typename T>
+__global__ __launch_bounds__(TPB) void image_to_nhwc_vec_kernel(const float* __restrict__ x,
+                                                                T* __restrict__ y, int N, int S,
+                                                                int pf, int cpad) {
+  typedef typename Vec<T>::type VT;
+  constexpr int V = Vec<T>::N;
+  const int R = S / pf;
+  const int64_t total = (int64_t)N * R * R;
+  const float inv = 1.f / (float)(pf * pf);
+  for (int64_t pix = blockIdx.x * (int64_t)TPB + threadIdx.x; pix < total;
+       pix += (int64_t)gridDim.x * TPB) {
+    const int xo = (int)(pix % R);
+    const int yo = (int)((pix / R) % R);
+    const int n = (int)(pix / ((int64_t)R * R));
+    float v[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float* xp = x + (((size_t)n * 3 + c) * S + (size_t)yo * pf) * S + xo * pf;
+      float a = 0.f;
+      for (int dy = 0; dy < pf; ++dy)
+        for (int dx = 0; dx < pf; ++dx) a += xp[dy * S + dx];
+      v[c] = a * inv;
+    }
+    T* out = y + pix * cpad;
+    for (int q = 0; q < cpad / V; ++q) {
+      VT o;
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const int ch = q * V + e;
+        o[e] = from_f<T>(ch < 3 ? v[ch < 3 ? ch : 0] : 0.f);
+      }
+      *(VT*)(out + q * V) = o;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // MSE pieces (K10).
 template <typename T>
@@ -1254,6 +1294,13 @@ extern "C" int mia_image_to_nhwc(const float* x, void* y, int N, int S, int pf, 
   MIA_CHECK_ARG(x && y && pf >= 1 && S % pf == 0 && cpad >= 3, "bad args");
   const int R = S / pf;
   const int64_t total = (int64_t)N * R * R * cpad;
+  const int V = dtype == MIA_F32 ? 4 : 8;
+  if (cpad % V == 0) {
+    const int64_t pixels = (int64_t)N * R * R;
+    MIA_DISPATCH_DTYPE(dtype, T,
+        MIA_LAUNCH(image_to_nhwc_vec_kernel<T>, dim3(blocks_for(pixels, TPB, 65536)), dim3(TPB),
+                   0, x, (T*)y, N, S, pf, cpad));
+  }
   MIA_DISPATCH_DTYPE(dtype, T,
       MIA_LAUNCH(image_to_nhwc_kernel<T>, dim3(blocks_for(total, TPB, 65536)), dim3(TPB), 0, x,
                  (T*)y, N, S, pf, cpad));

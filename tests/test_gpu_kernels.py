@@ -432,6 +432,28 @@ def test_maxpool_fwd_bwd(cuda, dtype, H, ceil, tap):
     assert rel_err(nchw(gi), ref_b) < TOL[dtype]
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("S,pf,cpad", [(16, 1, 8), (64, 4, 8), (32, 2, 3), (48, 1, 16)])
+def test_image_to_nhwc(cuda, dtype, S, pf, cpad):
+    """mia_image_to_nhwc (NCHW image → avg_pool(pf) → NHWC, channels ≥ 3 zero): both forms (the
+    16-byte-vector one for cpad a multiple of the vector, the element one otherwise) against the
+    same sums in the same order on the host — bit-exact."""
+    g = torch.Generator().manual_seed(S + pf + cpad)
+    N = 3
+    x = torch.rand(N, 3, S, S, generator=g) * 2 - 1
+    R = S // pf
+    acc = torch.zeros(N, 3, R, R)
+    for dy in range(pf):
+        for dx in range(pf):
+            acc = acc + x[:, :, dy::pf, dx::pf]
+    ref = torch.zeros(N, R, R, cpad)
+    ref[..., :3] = (acc * (1.0 / (pf * pf))).permute(0, 2, 3, 1)
+    y = torch.full((N, R, R, cpad), 7.0, dtype=dtype, device=cuda)
+    ops.image_to_nhwc(x.to(cuda), y, pf, cpad)
+    torch.cuda.synchronize()
+    assert torch.equal(y.cpu(), ref.to(dtype))
+
+
 @pytest.mark.parametrize("up,down,pad", [(2, 1, (2, 1)), (1, 1, (1, 1)), (1, 2, (1, 1)),
                                          (2, 2, (1, 2))])
 def test_upfirdn2d(cuda, up, down, pad):

@@ -93,6 +93,13 @@ def run(a):
         out[f"demod_{Cin}_{Cout}"] = gs.clone()
         tot += us * calls
         print(f"demod_bwd Cin={Cin} Cout={Cout}: {us:7.1f} us", flush=True)
+    for S, pf in ((256, 1), (256, 2)):
+        img = torch.rand(N, 3, S, S, device=dev, generator=g) * 2 - 1
+        y = torch.empty(N, S // pf, S // pf, 8, dtype=T, device=dev)
+        us = timeit(lambda: ops.image_to_nhwc(img, y, pf, 8))
+        out[f"image_to_nhwc_{S}_{pf}"] = y.float().clone()
+        print(f"image_to_nhwc S={S} pf={pf}: {us:7.1f} us "
+              f"{(img.numel() * 4 + y.numel() * y.element_size()) / us / 1e6:5.2f} TB/s", flush=True)
     for Cin, Cout in ((512, 512), (256, 128)):
         s = torch.randn(N, Cin, device=dev, generator=g)
         wsq = torch.rand(Cout, Cin, device=dev, generator=g)

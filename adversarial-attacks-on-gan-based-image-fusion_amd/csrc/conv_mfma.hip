@@ -35,6 +35,10 @@
 #include <cstdio>
 #include "halo_epilogue.h"
 
+#ifndef MIA_F32_PRO_SMALLTILE  // tile-count threshold of the fp32 PRO 64×64 tile (0 = off; A/B)
+#define MIA_F32_PRO_SMALLTILE 128
+#endif
+
 namespace mia {
 
 // s_waitcnt leaving at most `steps` K-steps of DMA (PER vm instructions each) in flight
@@ -448,6 +452,13 @@ static int launch_bn(ConvK& k, hipStream_t st) {
   // take the X6B 128×128 tile in launch_conv before reaching here; the 64×64 tile has no
   // pre-split-B form, and on the on-the-fly split it would double the split VALU per MFMA)
   if (sizeof(T) == 2 && tiles < small_below) return launch_tile<T, Tile64x64, PRO, SMALLC>(k, st);
+  // fp32 modulated-input launches of < 128 128×128 tiles (the generator's first StyledConv, 4²:
+  // 64 tiles, one block per four CUs on the K = 9·512 loop) on 64×64 tiles: 352 → 186 µs per
+  // call. From 256 tiles on (the 8² StyledConv, the 4 → 8 and 8 → 16 up-convs, the up-conv
+  // edges) the 64×64 tile's doubled split VALU per MFMA costs more than its blocks gain
+  // (profiles/r06_f32_small_pro_tile_ab.txt)
+  if (sizeof(T) == 4 && PRO && tiles < MIA_F32_PRO_SMALLTILE)
+    return launch_tile<T, Tile64x64, PRO, SMALLC>(k, st);
   if constexpr (!SMALLC && !PRO) {
     using namespace epi;
     switch (reg_epi_mask(k, sizeof(T))) {

@@ -123,7 +123,7 @@ __constant__ float kBlur4[4] = {0.25f, 0.75f, 0.75f, 0.25f};
 #ifndef MIA_BLUR_PF
 #define MIA_BLUR_PF 4
 #endif
-#ifndef MIA_BLUR_KQ  // output rows per strip / 2 (tuning A/B: -DMIA_BLUR_KQ=2, 3)
+#ifndef MIA_BLUR_KQ  // output rows per strip / 2 (swept 2 … 6: profiles/r06_blur_kq_sweep.txt)
 #define MIA_BLUR_KQ 4
 #endif
 constexpr int kBlurKQ = MIA_BLUR_KQ;
